@@ -1,0 +1,36 @@
+# Build of the MI355X (gfx950) Reed-Solomon shard codec.
+#   make            -> slime_amd/lib/libslime_rs.so (product) + oracle/liboracle.so (test checker)
+# hipcc cross-compiles for gfx950 without a GPU present.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Iinclude -Islime_amd/csrc
+SRC      := slime_amd/csrc
+OBJ      := build/obj
+LIB      := slime_amd/lib/libslime_rs.so
+
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/rs_capi.o
+HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
+
+all: $(LIB) oracle
+
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libslime_rs.so -Wl,--no-undefined
+
+$(OBJ):
+	@mkdir -p $@
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""RS encode+decode throughput, device-resident, need=8/total=12 (BASELINE.json).
+
+One step = one pass of the hot path over one batch of synthetic objects
+resident in HBM:
+  encode     all total-need parity shards of every object   (CreateParity x r, one launch)
+  decode     rebuild data shards {0,1,2,3} of every object   (RecoverData, erased rows only, one launch)
+from the symbol-domain shards (MapToGF already applied; the codec is timed
+separately by tools/).  Objects are partitioned across ranks (one process per
+GPU, no data-path collective: "weak" scaling, each rank owns its own batch).
+
+value = (sum of object bytes encoded + decoded over all ranks) / (max over
+ranks of the timed K steps), in GiB/s.  roofline: algorithmic HBM bytes per
+launch of the dominant kernel (rs_apply_kernel<8>) / its average duration,
+from HIP events recorded on the launch stream.  cpu_baseline: the oracle's
+faithful scalar C restatement of the reference's Go path, on a bounded sample.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--objects B] [--object-mib S]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (must precede slime_amd: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from slime_amd import device as D  # noqa: E402
+
+GIB = 1 << 30
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def ceil_div(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--need", type=int, default=8)
+    ap.add_argument("--total", type=int, default=12)
+    ap.add_argument("--objects", type=int, default=128, help="objects per GPU (C3/C4: 128)")
+    ap.add_argument("--object-mib", type=int, default=256, help="object size in MiB (C3/C4: 256)")
+    ap.add_argument("--erase", type=str, default="0,1,2,3", help="erased shards for the decode leg")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle CPU path on rank 0 at N=1")
+    ap.add_argument("--cpu-sample-mib", type=int, default=32, help="object size of the CPU sample")
+    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
+    return ap.parse_args()
+
+
+def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int) -> dict:
+    """Reference algorithm (oracle C port, %p twice per term, r passes) on host cores."""
+    import threading
+
+    import numpy as np
+
+    from oracle import oracle_c as OC
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    L = (sample_mib << 20) // 4 // need
+    rng = np.random.default_rng(0x5113E)
+    objs = [rng.integers(0, 4294967291, size=(total, L), dtype=np.uint64).astype(np.uint32) for _ in range(threads)]
+    have = [i for i in range(total) if i not in erase][:need]
+
+    def work(o):
+        OC.encode_object(o, need, total)
+        chunks = [o[i] for i in have]
+        rc, _ = OC.recover_data(chunks, have)  # RecoverData recomputes all need rows (vector.go:80-85)
+        assert rc == 0
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=work, args=(o,)) for o in objs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    nbytes = 2 * threads * need * L * 4  # encode + decode of each object
+    return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} objects x {sample_mib} MiB, need={need} total={total}: encode (r CreateParity "
+                      f"passes) + RecoverData(erase {erase}), one object per thread; {dt:.1f} s",
+            "seconds": round(dt, 2)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        # Control plane only (barrier + max-over-ranks timing): objects are
+        # independent, the data path exchanges nothing between GPUs.
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = local
+
+    need, total = args.need, args.total
+    r = total - need
+    erase = [int(x) for x in args.erase.split(",") if x != ""]
+    have = [i for i in range(total) if i not in erase][:need]
+    S = args.object_mib << 20
+    L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) symbols (multi_store.go:272)
+    nobj = args.objects
+    lay = D.layout_of(total, L)
+
+    buf = torch.empty(nobj * total * L, dtype=torch.int32, device=f"cuda:{dev}")
+    rec = torch.empty(nobj * len(erase) * L, dtype=torch.int32, device=f"cuda:{dev}")
+    # Data shards: deterministic symbols, distinct per rank (synthetic objects).
+    D.fill_symbols(buf, 0x5113E + 7919 * rank)
+    enc = D.Plan.encode(need, total, dev)
+    dec = D.Plan.reconstruct(need, total, have, erase, dev)
+    rec_lay = D.layout_of(len(erase), L)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * L)
+        if ev is not None:
+            ev[1].record(stream)
+        dec(buf, lay, rec, rec_lay, L, nobj, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+
+    # Correctness of what was timed: recovered shards == original data shards.
+    v = buf.view(nobj, total, L)
+    ok = bool(torch.equal(rec.view(nobj, len(erase), L)[:, [i for i, t in enumerate(erase) if t < need]],
+                          v[:, [t for t in erase if t < need]]))
+
+    t = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, enc_ms_max, dec_ms_max, bad = t.tolist()
+
+    obj_bytes = nobj * S
+    total_bytes = 2 * obj_bytes * world * args.steps
+    value = total_bytes / GIB / elapsed
+    # Algorithmic HBM bytes per launch: encode 4L(k + r),
+    # decode 4L(k + e) per object.
+    enc_alg = nobj * 4 * L * (need + r)
+    dec_alg = nobj * 4 * L * (need + len(erase))
+    launch_ms = (enc_ms + dec_ms) / 2
+    achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tj = json.load(open(args.traffic))
+            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}":
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": "RS encode+decode GiB/s device-resident at need=8/total=12, 1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 symbols in [0,p), seeded per rank; MapToGF domain)",
+            "config": {
+                "workload": f"C3+C4: need={need} total={total}, {args.object_mib} MiB objects x {nobj} per GPU; "
+                            f"encode all parity + decode erased {erase}",
+                "need": need, "total": total, "object_mib": args.object_mib, "objects_per_gpu": nobj,
+                "symbols_per_shard": L, "erased": erase, "parallelism": f"object-partition x{world} (no RCCL)",
+            },
+            "encode_gibs": round(obj_bytes / GIB / (enc_ms * 1e-3), 2),
+            "decode_gibs": round(obj_bytes / GIB / (dec_ms * 1e-3), 2),
+            "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4),
+                          "encode_max_rank": round(enc_ms_max, 4), "decode_max_rank": round(dec_ms_max, 4)},
+            "verified": bad == 0.0,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"rs_apply_kernel<{need},vec>",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg},
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if bad:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * slime_rs.h — C-ABI of the MI355X-native Reed-Solomon shard codec that
+ * replaces encryptio/slime's internal/rs and internal/rs/gf (Go) behind their
+ * unchanged Go API.  Field: GF(p), p = 2^32 - 5, 32-bit symbols
+ * (internal/rs/doc.go:1-2, internal/rs/gf/map.go:7).
+ *
+ * Two layers:
+ *   1. Go-API entry points (host memory in, host memory out).  Each one is
+ *      what the cgo shim of the corresponding Go function binds (see
+ *      INTEGRATION.md).  They validate exactly like the reference and return
+ *      a status code; slime_rs_status_string() gives the reference's panic
+ *      text, which the shim re-raises with panic().
+ *   2. Device-resident batch API (new, additive): plans + layouts over
+ *      objects already in HBM, launched on a caller-supplied hipStream_t.
+ *      This is the hot path the benchmark measures.
+ *
+ * Every compute entry point runs on the GPU (HIP kernels for gfx950). There is
+ * no CPU fallback: without a usable device they return SLIME_RS_ERR_NO_DEVICE.
+ * Host-only entry points (matrix construction, gf scalars) need no device.
+ * All functions are thread-safe.
+ */
+#ifndef SLIME_RS_H
+#define SLIME_RS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------
+ * Codes 1..8 correspond one-to-one to the reference's panics; the strings
+ * returned by slime_rs_status_string() are the reference's exact messages. */
+enum slime_rs_status {
+  SLIME_RS_OK = 0,
+  SLIME_RS_ERR_VARYING_LENGTH = 1, /* "CreateParity called on data chunks of varying length" vector.go:21 */
+  SLIME_RS_ERR_LEN_MISMATCH = 2,   /* "RecoverData: len(chunks) != len(indices)"            vector.go:52 */
+  SLIME_RS_ERR_EMPTY = 3,          /* "RecoverData: len(chunks) == 0"                       vector.go:56 */
+  SLIME_RS_ERR_NO_INDICES = 4,     /* "RecoverData: No indices given"                       vector.go:66 */
+  SLIME_RS_ERR_SINGULAR_NONZERO = 5, /* "Couldn't ensure nonzero m[i][i]"                   matrix.go:68 */
+  SLIME_RS_ERR_SINGULAR_ONE = 6,   /* "Couldn't ensure one m[i][i]"                         matrix.go:77 */
+  SLIME_RS_ERR_SINGULAR_ZERO = 7,  /* "Couldn't ensure zero m[i][j]"                        matrix.go:92 */
+  SLIME_RS_ERR_INDEX_RANGE = 8,    /* Go runtime "index out of range" panic                  */
+  SLIME_RS_ERR_INVALID_ARG = 9,    /* C-ABI misuse (null pointer, bad shape)                  */
+  SLIME_RS_ERR_NO_DEVICE = 10,     /* no usable HIP device: compute calls fail loudly         */
+  SLIME_RS_ERR_HIP = 11,           /* HIP runtime error (detail in slime_rs_last_error())     */
+  SLIME_RS_ERR_MAPPING_FALLBACK = 12 /* no candidate mapping fits (only with a bounded search) */
+};
+
+/* Reference panic message (codes 1..8) or a short description. Static storage. */
+const char *slime_rs_status_string(int status);
+/* Detail of the last failure on the calling thread ("" if none). */
+const char *slime_rs_last_error(void);
+/* Library version string. */
+const char *slime_rs_version(void);
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int slime_rs_device_count(void);
+/* Device the calling thread's Go-API entry points run on (default 0). */
+int slime_rs_select_device(int device);
+
+/* ==== internal/rs/gf ===================================================== */
+
+/* gf.MaxVal = 1<<32 - 5  (internal/rs/gf/map.go:7) */
+#define SLIME_GF_MAXVAL 4294967291u
+uint32_t slime_gf_max_val(void);
+/* gf.MInverse (internal/rs/gf/gf.go:5): in^(p-2) mod p. Host-only. */
+uint32_t slime_gf_minverse(uint32_t in);
+/* gf.Raise (internal/rs/gf/gf.go:46): x^n mod p, Raise(x,0) = 1. Host-only. */
+uint32_t slime_gf_raise(uint32_t x, uint32_t n);
+
+/* gf.MapToGF (internal/rs/gf/map.go:15).  out must hold (len+3)/4 words.
+ * Mapping 0 if every big-endian word is < p, else 1<<31 if that fits, else
+ * the first fitting value from the library's random candidate stream (the
+ * reference draws rand.Uint32(); see slime_gf_seed).  Runs on the GPU. */
+int slime_gf_map_to_gf(const uint8_t *in, uint64_t len, uint32_t *mapping, uint32_t *out);
+/* gf.MapToGFWith (internal/rs/gf/map.go:74). out holds (len+3)/4 words. GPU. */
+int slime_gf_map_to_gf_with(const uint8_t *in, uint64_t len, uint32_t n, uint32_t *out);
+/* gf.MapFromGF (internal/rs/gf/map.go:103). out holds 4*count bytes. GPU. */
+int slime_gf_map_from_gf(uint32_t n, const uint32_t *in, uint64_t count, uint8_t *out);
+/* Seed the MapToGF fallback candidate stream (default: std::random_device,
+ * like the reference's crypto-seeded math/rand, main.go:128-136). */
+void slime_gf_seed(uint64_t seed);
+
+/* ==== internal/rs: matrices (host-only, exact) =========================== */
+
+/* vandermondeMatrix (internal/rs/matrix.go:8): out is (d+p) x d row-major. */
+int slime_rs_vandermonde_matrix(int d, int p, uint32_t *out);
+/* ParityMatrix (internal/rs/matrix.go:27): out is (d+p) x d row-major. */
+int slime_rs_parity_matrix(int d, int p, uint32_t *out);
+/* ParityMatrixCached (internal/rs/matrixcache.go:11): *out points at a shared,
+ * read-only (d+p) x d matrix that lives for the life of the process. */
+int slime_rs_parity_matrix_cached(int d, int p, const uint32_t **out);
+/* solveSubIdentity (internal/rs/matrix.go:35), in place on rows x cols. */
+int slime_rs_solve_sub_identity(uint32_t *m, int rows, int cols);
+/* invertMatrix (internal/rs/matrix.go:112): inv = m^-1, both d x d. */
+int slime_rs_invert_matrix(const uint32_t *m, int d, uint32_t *inv);
+
+/* ==== internal/rs: Go-API data entry points (host memory, GPU compute) ===== */
+
+/* CreateParity (internal/rs/vector.go:18).  data[i] points at lens[i] words;
+ * out receives lens[0] words (the shim handles Go's `out` reuse rule). */
+int slime_rs_create_parity(const uint32_t *const *data, const uint64_t *lens, int ndata, int index,
+                           uint32_t *out);
+/* All total-ndata parity rows in one pass (the batched form of the
+ * reference's per-row loop, multi_store.go:528-531): out[i] receives row
+ * ndata+i, each lens[0] words. */
+int slime_rs_create_parities(const uint32_t *const *data, const uint64_t *lens, int ndata, int total,
+                             uint32_t *const *out);
+/* RecoverData (internal/rs/vector.go:50).  chunks[i] has lens[i] words and
+ * code-row index indices[i]; out[0..nchunks-1] each receive lens[0] words of
+ * data rows 0..nchunks-1. */
+int slime_rs_recover_data(const uint32_t *const *chunks, const uint64_t *lens, int nchunks, const int *indices,
+                          int nindices, uint32_t *const *out);
+
+/* ==== device-resident batch API (hot path) =============================== */
+
+/* Symbol layout of a batch of objects in device memory: shard s of object o
+ * starts at base + o*obj_stride + s*shard_stride (uint32 elements). */
+typedef struct slime_rs_layout {
+  uint64_t obj_stride;
+  uint64_t shard_stride;
+} slime_rs_layout_t;
+
+typedef struct slime_rs_plan *slime_rs_plan_t;
+
+/* Encode: inputs = src shards 0..need-1, outputs = parity rows need..total-1
+ * written to dst shards 0..total-need-1. */
+int slime_rs_plan_encode(int device, int need, int total, slime_rs_plan_t *plan);
+/* Reconstruct: inputs = src shards have[0..need-1] (code-row indices of the
+ * survivors, any order, distinct), outputs = code rows want[0..nwant-1]
+ * (data rows < need, or parity rows) written to dst shards 0..nwant-1.
+ * Bit-identical to RecoverData (+CreateParity for parity targets). */
+int slime_rs_plan_reconstruct(int device, int need, int total, const int *have, const int *want, int nwant,
+                              slime_rs_plan_t *plan);
+/* Arbitrary rows x k coefficient matrix (host, row-major) applied to src
+ * shards in_shards[0..k-1], written to dst shards 0..rows-1. */
+int slime_rs_plan_matrix(int device, const uint32_t *coeff, int rows, int k, const int *in_shards,
+                         slime_rs_plan_t *plan);
+/* Launch the plan over nobj objects of L symbols per shard.  src and dst are
+ * device pointers on the plan's device; stream is a hipStream_t (NULL = the
+ * null stream).  Asynchronous; capturable into a hipGraph. */
+int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t *src, slime_rs_layout_t src_layout, uint32_t *dst,
+                          slime_rs_layout_t dst_layout, uint64_t L, uint64_t nobj, void *stream);
+/* Shape of a plan: rows written and inputs read per column. */
+int slime_rs_plan_shape(slime_rs_plan_t plan, int *rows, int *k);
+/* Host copy of the plan's coefficient rows (rows x k, row-major). */
+int slime_rs_plan_coefficients(slime_rs_plan_t plan, uint32_t *out);
+int slime_rs_plan_destroy(slime_rs_plan_t plan);
+
+/* Device codec (internal/rs/gf/map.go) over device buffers, asynchronous on
+ * `stream`.  pack: words[i] = BE(bytes[4i..4i+3]) ^ mapping (zero low bytes
+ * in a partial last word); if flags != NULL it is OR-ed with bit0 = some
+ * unmapped word >= p, bit1 = some (word ^ 1<<31) >= p  (MapToGF's choice).
+ * unpack: bytes = BE(words[i] ^ mapping). */
+int slime_gf_pack_device(const uint8_t *bytes, uint64_t len, uint32_t mapping, uint32_t *words, uint32_t *flags,
+                         void *stream);
+int slime_gf_unpack_device(const uint32_t *words, uint64_t count, uint32_t mapping, uint8_t *bytes, void *stream);
+
+/* Deterministic synthetic symbols (benchmarks/tests): word g of the buffer is
+ * a pure function of (seed, g), uniform over [0, p). Asynchronous. */
+int slime_rs_fill_symbols(int device, uint32_t *dst, uint64_t count, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLIME_RS_H */

@@ -1,0 +1,139 @@
+"""ctypes binding of libslime_rs.so (the C-ABI in include/slime_rs.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``) at
+slime_amd/lib/libslime_rs.so.  There is no fallback: if it is missing, every
+import of this module raises.
+
+HIP runtime ownership: PyTorch-ROCm ships its own libamdhip64 with the same
+soname (libamdhip64.so.7) as /opt/rocm's.  If torch is importable it is
+imported FIRST, so the dynamic loader binds our library to torch's already
+loaded runtime and device pointers/streams from torch tensors are valid here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # noqa: SIM105 - see module docstring
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libslime_rs.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is not built; run `make` at the repo root or __graft_entry__.build()")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_intp = ctypes.POINTER(ctypes.c_int)
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class Layout(ctypes.Structure):
+    """slime_rs_layout_t: shard s of object o at base + o*obj_stride + s*shard_stride."""
+    _fields_ = [("obj_stride", ctypes.c_uint64), ("shard_stride", ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) for every symbol include/slime_rs.h declares.
+SIGNATURES = [
+    ("slime_rs_status_string", ctypes.c_char_p, [ctypes.c_int]),
+    ("slime_rs_last_error", ctypes.c_char_p, []),
+    ("slime_rs_version", ctypes.c_char_p, []),
+    ("slime_rs_device_count", ctypes.c_int, []),
+    ("slime_rs_select_device", ctypes.c_int, [ctypes.c_int]),
+    ("slime_gf_max_val", ctypes.c_uint32, []),
+    ("slime_gf_minverse", ctypes.c_uint32, [ctypes.c_uint32]),
+    ("slime_gf_raise", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
+    ("slime_gf_map_to_gf", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, c_u32p, ctypes.c_void_p]),
+    ("slime_gf_map_to_gf_with", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    ("slime_gf_map_from_gf", ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    ("slime_gf_seed", None, [ctypes.c_uint64]),
+    ("slime_rs_vandermonde_matrix", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_parity_matrix", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_parity_matrix_cached", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_u32p)]),
+    ("slime_rs_solve_sub_identity", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    ("slime_rs_invert_matrix", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_create_parity", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_create_parities", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_recover_data", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_plan_encode", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("slime_rs_plan_reconstruct", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+      ctypes.POINTER(ctypes.c_void_p)]),
+    ("slime_rs_plan_matrix", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("slime_rs_plan_execute", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, Layout, ctypes.c_void_p, Layout, ctypes.c_uint64, ctypes.c_uint64,
+      ctypes.c_void_p]),
+    ("slime_rs_plan_shape", ctypes.c_int, [ctypes.c_void_p, c_intp, c_intp]),
+    ("slime_rs_plan_coefficients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_plan_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("slime_gf_pack_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_gf_unpack_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_fill_symbols", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+]
+
+for _name, _res, _args in SIGNATURES:
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+# Status codes (enum slime_rs_status).
+OK = 0
+ERR_VARYING_LENGTH = 1
+ERR_LEN_MISMATCH = 2
+ERR_EMPTY = 3
+ERR_NO_INDICES = 4
+ERR_SINGULAR_NONZERO = 5
+ERR_SINGULAR_ONE = 6
+ERR_SINGULAR_ZERO = 7
+ERR_INDEX_RANGE = 8
+ERR_INVALID_ARG = 9
+ERR_NO_DEVICE = 10
+ERR_HIP = 11
+ERR_MAPPING_FALLBACK = 12
+
+PANIC_CODES = range(1, 9)
+
+
+class Panic(Exception):
+    """Raised where the reference panics; str(e) is the reference's panic text."""
+
+    def __init__(self, code: int, message: str, detail: str = ""):
+        super().__init__(message)
+        self.code = code
+        self.detail = detail
+
+
+class NativeError(RuntimeError):
+    """A non-panic failure of the native library (no device, HIP error, misuse)."""
+
+    def __init__(self, code: int, detail: str):
+        super().__init__(f"slime_rs error {code}: {detail}")
+        self.code = code
+
+
+def check(rc: int) -> None:
+    """Turn a C-ABI status into the reference's behaviour (panic) or an error."""
+    if rc == OK:
+        return
+    detail = lib.slime_rs_last_error().decode()
+    if rc in PANIC_CODES:
+        msg = lib.slime_rs_status_string(rc).decode()
+        if rc == ERR_INDEX_RANGE and detail:
+            msg = detail  # Go's runtime panic text carries the index
+        raise Panic(rc, msg, detail)
+    raise NativeError(rc, detail)
+
+
+def device_count() -> int:
+    return int(lib.slime_rs_device_count())

@@ -1,0 +1,60 @@
+// Internal launcher interface between the host library (rs_capi.cpp) and the
+// HIP kernels (rs_apply.hip, gf_codec.hip). Not part of the public C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace slime {
+
+// One matrix application over a batch of objects:
+//   out[o*out_obj + out_idx[i]*out_shard + b]
+//       = sum_j coeff[i][j] * in[o*in_obj + in_idx[j]*in_shard + b]   (mod p)
+// for o < nobj, i < rows, b < ncols.  Strides are in uint32 elements.
+// coeff / in_idx / out_idx are DEVICE pointers (a plan's tables).
+struct ApplyLaunch {
+  const uint32_t* in;
+  uint32_t* out;
+  uint64_t in_obj_stride;
+  uint64_t in_shard_stride;
+  uint64_t out_obj_stride;
+  uint64_t out_shard_stride;
+  const uint32_t* coeff;    // rows x coeff_stride(k), row-major, canonical residues
+  const uint32_t* in_idx;   // k input shard indices
+  const uint32_t* out_idx;  // rows output shard indices
+  uint64_t ncols;
+  uint32_t nobj;
+  uint32_t rows;
+  uint32_t k;
+  bool vec_ok;              // every base/stride/offset is 16-byte aligned
+};
+
+// Row stride (words) of a device coefficient table: padded to 16 words for the
+// k <= 16 kernels (one s_load_dwordx16 per row), exactly k otherwise.
+inline uint32_t coeff_stride(uint32_t k) { return k <= 16 ? 16u : k; }
+
+hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
+
+// out[i] = in[i] mod p  (RecoverData's unit rows for surviving data shards).
+hipError_t launch_canon_copy(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t stream);
+
+// --- byte <-> symbol codec (internal/rs/gf/map.go) -------------------------
+// Pack len bytes big-endian into ceil(len/4) words (zero low bytes in a partial
+// last word), XOR with `mapping`; words_out must hold ceil(len/4) words.
+// Also OR-reduces two flags into *flags (device): bit0 = some packed word >= p,
+// bit1 = some (word ^ 1<<31) >= p.  Pass flags == nullptr to skip.
+hipError_t launch_map_pack(const uint8_t* bytes, uint64_t len, uint32_t mapping, uint32_t* words_out,
+                           uint32_t* flags, hipStream_t stream);
+// In-place XOR of n words with a mapping value.
+hipError_t launch_xor_words(uint32_t* words, uint64_t n, uint32_t mapping, hipStream_t stream);
+// For each of ncand candidate mappings, set bad[c] = 1 if some word ^ cand[c] >= p.
+hipError_t launch_mapping_probe(const uint32_t* words, uint64_t n, const uint32_t* cand, uint32_t ncand,
+                                uint32_t* bad, hipStream_t stream);
+// Unpack n words (XOR mapping) to 4n big-endian bytes.
+hipError_t launch_map_unpack(const uint32_t* words, uint64_t n, uint32_t mapping, uint8_t* bytes_out,
+                             hipStream_t stream);
+
+// Synthetic symbols for benchmarks/tests: word g = splitmix64-derived value
+// reduced into [0, p), a pure function of (seed, g).
+hipError_t launch_fill_symbols(uint32_t* dst, uint64_t n, uint64_t seed, hipStream_t stream);
+
+}  // namespace slime

@@ -1,0 +1,719 @@
+// C-ABI of the MI355X Reed-Solomon shard codec (include/slime_rs.h).
+//
+// Go-API entry points mirror internal/rs and internal/rs/gf: same argument
+// meaning, same validation order, and the reference's panic text through
+// slime_rs_status_string().  All data-path work runs on the GPU through the
+// kernels in rs_apply.hip / gf_codec.hip; with no device the compute entry
+// points fail with SLIME_RS_ERR_NO_DEVICE (there is no CPU fallback).
+#include "slime_rs.h"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "gfp_host.hpp"
+#include "kernels.hpp"
+#include "rs_matrix.hpp"
+
+struct slime_rs_plan {
+  int device = 0;
+  uint32_t rows = 0, k = 0;
+  std::vector<uint32_t> coeff;  // rows x k, host copy
+  uint32_t* table = nullptr;    // device: coeff (rows x coeff_stride(k)) | in_idx (k) | out_idx (rows)
+  const uint32_t* d_coeff = nullptr;
+  const uint32_t* d_in_idx = nullptr;
+  const uint32_t* d_out_idx = nullptr;
+};
+
+namespace slime {
+namespace {
+
+thread_local std::string t_error;
+thread_local int t_device = 0;
+
+int fail(Status st, std::string detail) {
+  t_error = std::move(detail);
+  return (int)st;
+}
+int fail_hip(hipError_t e, const char* what) {
+  return fail(Status::Hip, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    const hipError_t e_ = (expr);                       \
+    if (e_ != hipSuccess) return fail_hip(e_, #expr);   \
+  } while (0)
+
+int visible_devices() {
+  static const int n = [] {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    return c;
+  }();
+  return n;
+}
+
+int check_device(int dev) {
+  const int n = visible_devices();
+  if (n == 0)
+    return fail(Status::NoDevice, "no HIP device visible: slime_rs data-path calls need an MI355X (gfx950) GPU");
+  if (dev < 0 || dev >= n) return fail(Status::InvalidArg, "device ordinal " + std::to_string(dev) + " out of range");
+  return 0;
+}
+
+// Switch the calling thread to `dev` for the scope, restoring its previous device.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// ---- plans -----------------------------------------------------------------
+
+int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, const std::vector<uint32_t>& in_idx,
+               const std::vector<uint32_t>& out_idx, slime_rs_plan** out) {
+  if (int rc = check_device(device)) return rc;
+  auto plan = std::make_unique<slime_rs_plan>();
+  plan->device = device;
+  plan->rows = rows;
+  plan->k = k;
+  plan->coeff.assign(coeff, coeff + (size_t)rows * k);
+  const uint32_t cs = coeff_stride(k);
+  const size_t ncoef = (size_t)rows * cs;
+  const size_t n_in = (k + 3) & ~3u, n_out = (rows + 3) & ~3u;
+  std::vector<uint32_t> host(ncoef + n_in + n_out, 0u);
+  for (uint32_t i = 0; i < rows; ++i)
+    for (uint32_t j = 0; j < k; ++j) host[(size_t)i * cs + j] = coeff[(size_t)i * k + j] % kP;
+  std::copy(in_idx.begin(), in_idx.end(), host.begin() + ncoef);
+  std::copy(out_idx.begin(), out_idx.end(), host.begin() + ncoef + n_in);
+  DeviceScope ds(device);
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, host.size() * sizeof(uint32_t)));
+  if (hipMemcpy(p, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p);
+    return fail(Status::Hip, "plan table upload failed");
+  }
+  plan->table = (uint32_t*)p;
+  plan->d_coeff = plan->table;
+  plan->d_in_idx = plan->table + ncoef;
+  plan->d_out_idx = plan->table + ncoef + n_in;
+  *out = plan.release();
+  return 0;
+}
+
+void destroy_plan(slime_rs_plan* plan) {
+  if (!plan) return;
+  if (plan->table) {
+    DeviceScope ds(plan->device);
+    (void)hipFree(plan->table);
+  }
+  delete plan;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, uint64_t src_shard, uint32_t* dst,
+            uint64_t dst_obj, uint64_t dst_shard, uint64_t L, uint64_t nobj, hipStream_t stream) {
+  if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "nobj exceeds 2^32-1");
+  ApplyLaunch a;
+  a.in = src;
+  a.out = dst;
+  a.in_obj_stride = src_obj;
+  a.in_shard_stride = src_shard;
+  a.out_obj_stride = dst_obj;
+  a.out_shard_stride = dst_shard;
+  a.coeff = plan->d_coeff;
+  a.in_idx = plan->d_in_idx;
+  a.out_idx = plan->d_out_idx;
+  a.ncols = L;
+  a.nobj = (uint32_t)nobj;
+  a.rows = plan->rows;
+  a.k = plan->k;
+  a.vec_ok = aligned16(src) && aligned16(dst) && ((src_obj | src_shard | dst_obj | dst_shard) & 3u) == 0;
+  DeviceScope ds(plan->device);
+  HIP_TRY(launch_apply(a, stream));
+  return 0;
+}
+
+// Plans the host entry points reuse, keyed by (device, kind, shape, indices).
+using PlanKey = std::tuple<int, char, int, int, std::vector<int>>;
+std::mutex g_plan_mu;
+std::map<PlanKey, slime_rs_plan*> g_plans;
+
+int cached_plan(const PlanKey& key, slime_rs_plan** out,
+                int (*make)(const PlanKey&, slime_rs_plan**)) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) {
+    *out = it->second;
+    return 0;
+  }
+  slime_rs_plan* p = nullptr;
+  if (int rc = make(key, &p)) return rc;
+  g_plans[key] = p;
+  *out = p;
+  return 0;
+}
+
+// ---- per-call device workspaces (host entry points) ----------------------------
+
+struct Workspace {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* dbuf = nullptr;
+  size_t dcap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= dcap) return 0;
+    DeviceScope ds(device);
+    if (dbuf) (void)hipFree(dbuf);
+    dbuf = nullptr;
+    dcap = 0;
+    size_t want = std::max<size_t>(bytes, 1u << 20);
+    HIP_TRY(hipMalloc((void**)&dbuf, want));
+    dcap = want;
+    return 0;
+  }
+};
+
+std::mutex g_ws_mu;
+std::vector<Workspace*> g_ws_free;
+
+int acquire_ws(int device, Workspace** out) {
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (size_t i = 0; i < g_ws_free.size(); ++i) {
+      if (g_ws_free[i]->device == device) {
+        *out = g_ws_free[i];
+        g_ws_free.erase(g_ws_free.begin() + (long)i);
+        return 0;
+      }
+    }
+  }
+  auto ws = std::make_unique<Workspace>();
+  ws->device = device;
+  DeviceScope ds(device);
+  HIP_TRY(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking));
+  *out = ws.release();
+  return 0;
+}
+
+void release_ws(Workspace* ws) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  g_ws_free.push_back(ws);
+}
+
+struct WsLease {
+  Workspace* ws = nullptr;
+  ~WsLease() {
+    if (ws) release_ws(ws);
+  }
+};
+
+size_t round16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+// ---- MapToGF fallback candidates (the reference's rand.Uint32() stream) ------
+
+std::mutex g_rng_mu;
+std::mt19937_64 g_rng{std::random_device{}()};
+
+const char* status_text(int st) {
+  switch (st) {
+    case 0: return "ok";
+    case 1: return "CreateParity called on data chunks of varying length";
+    case 2: return "RecoverData: len(chunks) != len(indices)";
+    case 3: return "RecoverData: len(chunks) == 0";
+    case 4: return "RecoverData: No indices given";
+    case 5: return "Couldn't ensure nonzero m[i][i]";
+    case 6: return "Couldn't ensure one m[i][i]";
+    case 7: return "Couldn't ensure zero m[i][j]";
+    case 8: return "runtime error: index out of range";
+    case 9: return "invalid argument";
+    case 10: return "no HIP device";
+    case 11: return "HIP runtime error";
+    case 12: return "no mapping value found";
+    default: return "unknown status";
+  }
+}
+
+int status_of(Status st, const char* what) {
+  if (st == Status::Ok) return 0;
+  return fail(st, std::string(what) + ": " + status_text((int)st));
+}
+
+}  // namespace
+}  // namespace slime
+
+using namespace slime;
+
+extern "C" {
+
+const char* slime_rs_status_string(int status) { return status_text(status); }
+const char* slime_rs_last_error(void) { return t_error.c_str(); }
+const char* slime_rs_version(void) { return "slime_rs 0.1 (gfx950, GF(2^32-5))"; }
+int slime_rs_device_count(void) { return visible_devices(); }
+
+int slime_rs_select_device(int device) {
+  if (int rc = check_device(device)) return rc;
+  t_device = device;
+  return 0;
+}
+
+// ---- gf scalars / host matrices -------------------------------------------------
+
+uint32_t slime_gf_max_val(void) { return kP; }
+uint32_t slime_gf_minverse(uint32_t in) { return gf_minverse(in); }
+uint32_t slime_gf_raise(uint32_t x, uint32_t n) { return gf_raise(x, n); }
+
+void slime_gf_seed(uint64_t seed) {
+  std::lock_guard<std::mutex> lk(g_rng_mu);
+  g_rng.seed(seed);
+}
+
+int slime_rs_vandermonde_matrix(int d, int p, uint32_t* out) {
+  if (d < 0 || p < 0 || (!out && d > 0)) return fail(Status::InvalidArg, "vandermonde: bad shape");
+  const Matrix m = vandermonde(d, p);
+  if (!m.v.empty()) memcpy(out, m.v.data(), m.v.size() * sizeof(uint32_t));
+  return 0;
+}
+
+int slime_rs_parity_matrix(int d, int p, uint32_t* out) {
+  if (d <= 0 || p < 0 || !out) return fail(Status::InvalidArg, "parity_matrix: bad shape");
+  Matrix m;
+  if (Status st = parity_matrix(d, p, &m); st != Status::Ok) return status_of(st, "ParityMatrix");
+  memcpy(out, m.v.data(), m.v.size() * sizeof(uint32_t));
+  return 0;
+}
+
+int slime_rs_parity_matrix_cached(int d, int p, const uint32_t** out) {
+  if (d <= 0 || p < 0 || !out) return fail(Status::InvalidArg, "parity_matrix_cached: bad shape");
+  const Matrix* m = nullptr;
+  if (Status st = parity_matrix_cached(d, p, &m); st != Status::Ok) return status_of(st, "ParityMatrixCached");
+  *out = m->v.data();
+  return 0;
+}
+
+int slime_rs_solve_sub_identity(uint32_t* m, int rows, int cols) {
+  if (rows <= 0 || cols <= 0 || rows < cols || !m) return fail(Status::InvalidArg, "solveSubIdentity: bad shape");
+  Matrix w((size_t)rows, (size_t)cols);
+  memcpy(w.v.data(), m, w.v.size() * sizeof(uint32_t));
+  const Status st = reduce_cols(w);
+  memcpy(m, w.v.data(), w.v.size() * sizeof(uint32_t));  // partial progress is visible, as in Go
+  return status_of(st, "solveSubIdentity");
+}
+
+int slime_rs_invert_matrix(const uint32_t* m, int d, uint32_t* inv) {
+  if (d <= 0 || !m || !inv) return fail(Status::InvalidArg, "invertMatrix: bad shape");
+  Matrix a((size_t)d, (size_t)d), r;
+  memcpy(a.v.data(), m, a.v.size() * sizeof(uint32_t));
+  if (Status st = invert(a, &r); st != Status::Ok) return status_of(st, "invertMatrix");
+  memcpy(inv, r.v.data(), r.v.size() * sizeof(uint32_t));
+  return 0;
+}
+
+// ---- plans (device-resident batch API) ------------------------------------------
+
+int slime_rs_plan_matrix(int device, const uint32_t* coeff, int rows, int k, const int* in_shards,
+                         slime_rs_plan_t* plan) {
+  if (!plan || !coeff || !in_shards || rows <= 0 || k <= 0) return fail(Status::InvalidArg, "plan_matrix: bad args");
+  std::vector<uint32_t> in_idx(k), out_idx(rows);
+  for (int j = 0; j < k; ++j) {
+    if (in_shards[j] < 0) return fail(Status::InvalidArg, "plan_matrix: negative shard index");
+    in_idx[j] = (uint32_t)in_shards[j];
+  }
+  for (int i = 0; i < rows; ++i) out_idx[i] = (uint32_t)i;
+  return build_plan(device, (uint32_t)rows, (uint32_t)k, coeff, in_idx, out_idx, plan);
+}
+
+int slime_rs_plan_encode(int device, int need, int total, slime_rs_plan_t* plan) {
+  if (!plan || need <= 0 || total <= need) return fail(Status::InvalidArg, "plan_encode: need 0 < need < total");
+  const Matrix* m = nullptr;
+  if (Status st = parity_matrix_cached(need, total - need, &m); st != Status::Ok)
+    return status_of(st, "ParityMatrix");
+  std::vector<int> in(need);
+  for (int j = 0; j < need; ++j) in[j] = j;
+  return slime_rs_plan_matrix(device, m->row(need), total - need, need, in.data(), plan);
+}
+
+int slime_rs_plan_reconstruct(int device, int need, int total, const int* have, const int* want, int nwant,
+                              slime_rs_plan_t* plan) {
+  if (!plan || !have || !want || need <= 0 || total < need || nwant <= 0)
+    return fail(Status::InvalidArg, "plan_reconstruct: bad args");
+  for (int i = 0; i < need; ++i)
+    if (have[i] < 0 || have[i] >= total) return fail(Status::IndexRange, "plan_reconstruct: have index out of range");
+  for (int i = 0; i < nwant; ++i)
+    if (want[i] < 0 || want[i] >= total) return fail(Status::IndexRange, "plan_reconstruct: want index out of range");
+  // inv maps the survivors to the data rows (RecoverData, vector.go:69-80).
+  Matrix hv((size_t)need, (size_t)need), inv;
+  std::vector<uint32_t> row;
+  for (int i = 0; i < need; ++i) {
+    if (Status st = code_row(need, have[i], &row); st != Status::Ok) return status_of(st, "ParityMatrix");
+    std::copy(row.begin(), row.end(), hv.v.begin() + (size_t)i * need);
+  }
+  if (Status st = invert(hv, &inv); st != Status::Ok) return status_of(st, "invertMatrix");
+  // Target row t: data row t of inv, or (parity) code_row(t) * inv.
+  std::vector<uint32_t> coeff((size_t)nwant * need);
+  for (int w = 0; w < nwant; ++w) {
+    const int t = want[w];
+    if (t < need) {
+      std::copy(inv.row(t), inv.row(t) + need, coeff.begin() + (size_t)w * need);
+      continue;
+    }
+    if (Status st = code_row(need, t, &row); st != Status::Ok) return status_of(st, "ParityMatrix");
+    for (int q = 0; q < need; ++q) {
+      uint64_t acc = 0;
+      for (int j = 0; j < need; ++j) acc = (acc + mulmod(row[j], inv.at(j, q))) % kP;
+      coeff[(size_t)w * need + q] = (uint32_t)acc;
+    }
+  }
+  return slime_rs_plan_matrix(device, coeff.data(), nwant, need, have, plan);
+}
+
+int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t* src, slime_rs_layout_t src_layout, uint32_t* dst,
+                          slime_rs_layout_t dst_layout, uint64_t L, uint64_t nobj, void* stream) {
+  if (!plan) return fail(Status::InvalidArg, "plan_execute: null plan");
+  if (L == 0 || nobj == 0) return 0;
+  if (!src || !dst) return fail(Status::InvalidArg, "plan_execute: null buffer");
+  return execute(plan, src, src_layout.obj_stride, src_layout.shard_stride, dst, dst_layout.obj_stride,
+                 dst_layout.shard_stride, L, nobj, (hipStream_t)stream);
+}
+
+int slime_rs_plan_shape(slime_rs_plan_t plan, int* rows, int* k) {
+  if (!plan) return fail(Status::InvalidArg, "plan_shape: null plan");
+  if (rows) *rows = (int)plan->rows;
+  if (k) *k = (int)plan->k;
+  return 0;
+}
+
+int slime_rs_plan_coefficients(slime_rs_plan_t plan, uint32_t* out) {
+  if (!plan || !out) return fail(Status::InvalidArg, "plan_coefficients: bad args");
+  memcpy(out, plan->coeff.data(), plan->coeff.size() * sizeof(uint32_t));
+  return 0;
+}
+
+int slime_rs_plan_destroy(slime_rs_plan_t plan) {
+  destroy_plan(plan);
+  return 0;
+}
+
+// ---- device codec / fill ------------------------------------------------------------
+
+int slime_gf_pack_device(const uint8_t* bytes, uint64_t len, uint32_t mapping, uint32_t* words, uint32_t* flags,
+                         void* stream) {
+  if (len == 0) return 0;
+  if (!bytes || !words) return fail(Status::InvalidArg, "pack_device: null buffer");
+  if (int rc = check_device(0)) return rc;
+  HIP_TRY(launch_map_pack(bytes, len, mapping, words, flags, (hipStream_t)stream));
+  return 0;
+}
+
+int slime_gf_unpack_device(const uint32_t* words, uint64_t count, uint32_t mapping, uint8_t* bytes, void* stream) {
+  if (count == 0) return 0;
+  if (!bytes || !words) return fail(Status::InvalidArg, "unpack_device: null buffer");
+  if (int rc = check_device(0)) return rc;
+  HIP_TRY(launch_map_unpack(words, count, mapping, bytes, (hipStream_t)stream));
+  return 0;
+}
+
+int slime_rs_fill_symbols(int device, uint32_t* dst, uint64_t count, uint64_t seed, void* stream) {
+  if (count == 0) return 0;
+  if (!dst) return fail(Status::InvalidArg, "fill_symbols: null buffer");
+  if (int rc = check_device(device)) return rc;
+  DeviceScope ds(device);
+  HIP_TRY(launch_fill_symbols(dst, count, seed, (hipStream_t)stream));
+  return 0;
+}
+
+// ---- Go-API data entry points (host memory) ------------------------------------------
+
+static int make_rows_plan(const PlanKey& key, slime_rs_plan** out) {
+  // kind 'P': code rows key.indices[...] of a need = key.k code, inputs 0..need-1.
+  const int dev = std::get<0>(key), need = std::get<2>(key);
+  const std::vector<int>& rows = std::get<4>(key);
+  std::vector<uint32_t> coeff;
+  std::vector<uint32_t> row;
+  for (int r : rows) {
+    if (Status st = code_row(need, r, &row); st != Status::Ok) return status_of(st, "ParityMatrix");
+    coeff.insert(coeff.end(), row.begin(), row.end());
+  }
+  std::vector<int> in(need);
+  for (int j = 0; j < need; ++j) in[j] = j;
+  return slime_rs_plan_matrix(dev, coeff.data(), (int)rows.size(), need, in.data(), out);
+}
+
+static int run_rows(int need, const std::vector<int>& rows, const uint32_t* const* data, uint64_t L,
+                    uint32_t* const* out) {
+  const int dev = t_device;
+  if (int rc = check_device(dev)) return rc;
+  slime_rs_plan* plan = nullptr;
+  if (int rc = cached_plan(PlanKey{dev, 'P', need, 0, rows}, &plan, make_rows_plan)) return rc;
+  WsLease lease;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  Workspace* ws = lease.ws;
+  DeviceScope ds(dev);
+  const size_t shard = round16(L * 4) / 4;  // keep every shard 16-byte aligned
+  if (int rc = ws->reserve(shard * 4 * ((size_t)need + rows.size()))) return rc;
+  uint32_t* d_in = (uint32_t*)ws->dbuf;
+  uint32_t* d_out = d_in + shard * need;
+  for (int j = 0; j < need; ++j)
+    HIP_TRY(hipMemcpyAsync(d_in + shard * j, data[j], L * 4, hipMemcpyHostToDevice, ws->stream));
+  if (int rc = execute(plan, d_in, 0, shard, d_out, 0, shard, L, 1, ws->stream)) return rc;
+  for (size_t i = 0; i < rows.size(); ++i)
+    HIP_TRY(hipMemcpyAsync(out[i], d_out + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+int slime_rs_create_parity(const uint32_t* const* data, const uint64_t* lens, int ndata, int index, uint32_t* out) {
+  if (ndata < 0 || (ndata > 0 && (!data || !lens))) return fail(Status::InvalidArg, "CreateParity: bad args");
+  for (int i = 1; i < ndata; ++i)
+    if (lens[i] != lens[0]) return status_of(Status::VaryingLength, "CreateParity");
+  if (ndata == 0) return fail(Status::IndexRange, "runtime error: index out of range [0] with length 0");
+  if (index < 0) return fail(Status::IndexRange, "runtime error: index out of range [" + std::to_string(index) + "]");
+  std::vector<uint32_t> row;
+  if (Status st = code_row(ndata, index, &row); st != Status::Ok) return status_of(st, "ParityMatrixCached");
+  const uint64_t L = lens[0];
+  if (L == 0) return 0;
+  if (!out) return fail(Status::InvalidArg, "CreateParity: null out");
+  for (int j = 0; j < ndata; ++j)
+    if (!data[j]) return fail(Status::InvalidArg, "CreateParity: null data chunk");
+  return run_rows(ndata, std::vector<int>{index}, data, L, &out);
+}
+
+int slime_rs_create_parities(const uint32_t* const* data, const uint64_t* lens, int ndata, int total,
+                             uint32_t* const* out) {
+  if (ndata <= 0 || total < ndata || !data || !lens) return fail(Status::InvalidArg, "CreateParities: bad args");
+  for (int i = 1; i < ndata; ++i)
+    if (lens[i] != lens[0]) return status_of(Status::VaryingLength, "CreateParity");
+  if (total == ndata || lens[0] == 0) return 0;
+  if (!out) return fail(Status::InvalidArg, "CreateParities: null out");
+  for (int j = 0; j < ndata; ++j)
+    if (!data[j]) return fail(Status::InvalidArg, "CreateParities: null data chunk");
+  for (int i = 0; i < total - ndata; ++i)
+    if (!out[i]) return fail(Status::InvalidArg, "CreateParities: null out row");
+  std::vector<int> rows;
+  for (int r = ndata; r < total; ++r) rows.push_back(r);
+  return run_rows(ndata, rows, data, lens[0], out);
+}
+
+static int make_recover_plan(const PlanKey& key, slime_rs_plan** out) {
+  // kind 'R': erased data rows of a need-row recovery from survivors `have`.
+  const int dev = std::get<0>(key), need = std::get<2>(key);
+  const std::vector<int>& have = std::get<4>(key);
+  std::vector<char> present(need, 0);
+  for (int h : have)
+    if (h < need) present[h] = 1;
+  std::vector<int> want;
+  for (int t = 0; t < need; ++t)
+    if (!present[t]) want.push_back(t);
+  if (want.empty()) {
+    *out = nullptr;  // nothing to compute: every data row survived
+    return 0;
+  }
+  // `have` indexes code rows; the staged chunk buffer holds them at 0..need-1.
+  const int total = std::max(need, *std::max_element(have.begin(), have.end()) + 1);
+  slime_rs_plan* tmp = nullptr;
+  if (int rc = slime_rs_plan_reconstruct(dev, need, total, have.data(), want.data(), (int)want.size(), &tmp))
+    return rc;
+  // Re-point inputs at the staged positions 0..need-1 (plan tables are ours).
+  std::vector<int> pos(need);
+  for (int q = 0; q < need; ++q) pos[q] = q;
+  slime_rs_plan* staged = nullptr;
+  const int rc = slime_rs_plan_matrix(dev, tmp->coeff.data(), (int)tmp->rows, need, pos.data(), &staged);
+  destroy_plan(tmp);
+  if (rc) return rc;
+  *out = staged;
+  return 0;
+}
+
+int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, int nchunks, const int* indices,
+                          int nindices, uint32_t* const* out) {
+  if (nchunks < 0 || nindices < 0) return fail(Status::InvalidArg, "RecoverData: negative count");
+  if (nchunks != nindices) return status_of(Status::LenMismatch, "RecoverData");
+  if (nchunks == 0) return status_of(Status::Empty, "RecoverData");
+  if (!chunks || !lens || !indices) return fail(Status::InvalidArg, "RecoverData: bad args");
+  int max_index = -1;
+  for (int i = 0; i < nindices; ++i) max_index = std::max(max_index, indices[i]);
+  if (max_index == -1) return status_of(Status::NoIndices, "RecoverData");
+  const int need = nchunks;
+  for (int i = 0; i < nindices; ++i)
+    if (indices[i] < 0)
+      return fail(Status::IndexRange, "runtime error: index out of range [" + std::to_string(indices[i]) + "]");
+  // ParityMatrixCached(len(chunks), maxIndex) + invertMatrix(have): same
+  // failure conditions as the reference (duplicate rows -> singular).
+  {
+    Matrix hv((size_t)need, (size_t)need), inv;
+    std::vector<uint32_t> row;
+    for (int i = 0; i < need; ++i) {
+      if (Status st = code_row(need, indices[i], &row); st != Status::Ok) return status_of(st, "ParityMatrixCached");
+      std::copy(row.begin(), row.end(), hv.v.begin() + (size_t)i * need);
+    }
+    if (Status st = invert(hv, &inv); st != Status::Ok) return status_of(st, "RecoverData");
+  }
+  const uint64_t L = lens[0];
+  for (int i = 1; i < need; ++i)
+    if (lens[i] < L)
+      return fail(Status::IndexRange, "runtime error: index out of range [" + std::to_string(lens[i]) +
+                                          "] with length " + std::to_string(lens[i]));
+  if (L == 0) return 0;
+  if (!out) return fail(Status::InvalidArg, "RecoverData: null out");
+  for (int i = 0; i < need; ++i)
+    if (!chunks[i] || !out[i]) return fail(Status::InvalidArg, "RecoverData: null buffer");
+
+  const int dev = t_device;
+  if (int rc = check_device(dev)) return rc;
+  std::vector<int> have(indices, indices + nindices);
+  slime_rs_plan* plan = nullptr;
+  if (int rc = cached_plan(PlanKey{dev, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
+
+  // Surviving data rows are unit rows of the inverse (x mod p); the erased
+  // ones come from the plan, in ascending row order.
+  std::vector<int> slot_of(need, -1);
+  for (int q = 0; q < need; ++q)
+    if (indices[q] < need) slot_of[indices[q]] = q;
+  std::vector<int> erased;
+  for (int t = 0; t < need; ++t)
+    if (slot_of[t] < 0) erased.push_back(t);
+
+  WsLease lease;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  Workspace* ws = lease.ws;
+  DeviceScope ds(dev);
+  const size_t shard = round16(L * 4) / 4;  // every staged shard 16-byte aligned
+  if (int rc = ws->reserve(shard * 4 * ((size_t)need * 2 + erased.size()))) return rc;
+  uint32_t* d_in = (uint32_t*)ws->dbuf;      // need staged chunks
+  uint32_t* d_copy = d_in + shard * need;    // canonical copies of surviving data rows
+  uint32_t* d_rec = d_copy + shard * need;   // recovered rows, erased order
+  for (int q = 0; q < need; ++q)
+    HIP_TRY(hipMemcpyAsync(d_in + shard * q, chunks[q], L * 4, hipMemcpyHostToDevice, ws->stream));
+  for (int t = 0; t < need; ++t)
+    if (slot_of[t] >= 0) HIP_TRY(launch_canon_copy(d_in + shard * slot_of[t], d_copy + shard * t, L, ws->stream));
+  if (plan && (int)plan->rows != (int)erased.size()) return fail(Status::InvalidArg, "RecoverData: plan mismatch");
+  if (plan)
+    if (int rc = execute(plan, d_in, 0, shard, d_rec, 0, shard, L, 1, ws->stream)) return rc;
+  for (size_t i = 0; i < erased.size(); ++i)
+    HIP_TRY(hipMemcpyAsync(out[erased[i]], d_rec + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
+  for (int t = 0; t < need; ++t)
+    if (slot_of[t] >= 0) HIP_TRY(hipMemcpyAsync(out[t], d_copy + shard * t, L * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+// ---- gf codec (host memory) -----------------------------------------------------------
+
+static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease) {
+  const int dev = t_device;
+  if (int rc = check_device(dev)) return rc;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  *wsp = lease.ws;
+  return (*wsp)->reserve(bytes_needed);
+}
+
+int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out) {
+  const uint64_t nw = (len + 3) / 4;
+  if (nw == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapToGFWith: null buffer");
+  WsLease lease;
+  Workspace* ws = nullptr;
+  const size_t bbytes = round16(len);
+  if (int rc = codec_setup(bbytes + round16(nw * 4), &ws, lease)) return rc;
+  DeviceScope ds(ws->device);
+  uint8_t* d_bytes = ws->dbuf;
+  uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
+  HIP_TRY(hipMemcpyAsync(d_bytes, in, len, hipMemcpyHostToDevice, ws->stream));
+  HIP_TRY(launch_map_pack(d_bytes, len, n, d_words, nullptr, ws->stream));
+  HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
+  if (!mapping) return fail(Status::InvalidArg, "MapToGF: null mapping");
+  const uint64_t nw = (len + 3) / 4;
+  *mapping = 0;
+  if (nw == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapToGF: null buffer");
+  WsLease lease;
+  Workspace* ws = nullptr;
+  const size_t bbytes = round16(len), wbytes = round16(nw * 4);
+  constexpr uint32_t kCand = 64;
+  if (int rc = codec_setup(bbytes + wbytes + 16 + 2 * kCand * 4, &ws, lease)) return rc;
+  DeviceScope ds(ws->device);
+  uint8_t* d_bytes = ws->dbuf;
+  uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
+  uint32_t* d_flags = (uint32_t*)(ws->dbuf + bbytes + wbytes);
+  uint32_t* d_cand = d_flags + 4;
+  uint32_t* d_bad = d_cand + kCand;
+  uint32_t flags = 0;
+  HIP_TRY(hipMemcpyAsync(d_bytes, in, len, hipMemcpyHostToDevice, ws->stream));
+  HIP_TRY(hipMemsetAsync(d_flags, 0, 4, ws->stream));
+  HIP_TRY(launch_map_pack(d_bytes, len, 0, d_words, d_flags, ws->stream));
+  HIP_TRY(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  uint32_t m = 0;
+  if (flags & 1u) {
+    if (!(flags & 2u)) {
+      m = 1u << 31;  // map.go:47: try just switching the high bit first
+    } else {
+      // map.go:64-66: random candidates until one fits; 64 per device pass.
+      bool found = false;
+      for (int round = 0; round < (1 << 16) && !found; ++round) {
+        uint32_t cand[kCand], bad[kCand];
+        {
+          std::lock_guard<std::mutex> lk(g_rng_mu);
+          for (uint32_t c = 0; c < kCand; ++c) cand[c] = (uint32_t)(g_rng() >> 32);
+        }
+        HIP_TRY(hipMemcpyAsync(d_cand, cand, sizeof(cand), hipMemcpyHostToDevice, ws->stream));
+        HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(bad), ws->stream));
+        HIP_TRY(launch_mapping_probe(d_words, nw, d_cand, kCand, d_bad, ws->stream));
+        HIP_TRY(hipMemcpyAsync(bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+        for (uint32_t c = 0; c < kCand; ++c)
+          if (!bad[c]) {
+            m = cand[c];
+            found = true;
+            break;
+          }
+      }
+      if (!found) return status_of(Status::MappingFallback, "MapToGF");
+    }
+    HIP_TRY(launch_xor_words(d_words, nw, m, ws->stream));
+  }
+  HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  *mapping = m;
+  return 0;
+}
+
+int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t* out) {
+  if (count == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapFromGF: null buffer");
+  WsLease lease;
+  Workspace* ws = nullptr;
+  const size_t wbytes = round16(count * 4);
+  if (int rc = codec_setup(2 * wbytes, &ws, lease)) return rc;
+  DeviceScope ds(ws->device);
+  uint32_t* d_words = (uint32_t*)ws->dbuf;
+  uint8_t* d_bytes = ws->dbuf + wbytes;
+  HIP_TRY(hipMemcpyAsync(d_words, in, count * 4, hipMemcpyHostToDevice, ws->stream));
+  HIP_TRY(launch_map_unpack(d_words, count, n, d_bytes, ws->stream));
+  HIP_TRY(hipMemcpyAsync(out, d_bytes, count * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+"""Device-resident batch API (the hot path) over torch tensors in HBM.
+
+Objects are laid out ``[object][shard][L]`` uint32 symbols (torch has no
+general uint32 arithmetic, so buffers are ``torch.int32`` tensors holding the
+same bits).  A plan carries the coefficient rows on the device; executing it
+launches the gfx950 kernel on the given (default: current) torch stream.
+PyTorch here is plumbing only: memory, streams, events.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+lib = N.lib
+
+
+def _stream_handle(device: int, stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev_index(t: torch.Tensor) -> int:
+    if t.device.type != "cuda":
+        raise ValueError("slime_amd.device needs tensors on a HIP device (torch 'cuda')")
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def layout_of(nshards: int, L: int, shard_stride: Optional[int] = None) -> N.Layout:
+    ss = L if shard_stride is None else shard_stride
+    return N.Layout(obj_stride=ss * nshards, shard_stride=ss)
+
+
+class Plan:
+    """A compiled coefficient matrix on one device (slime_rs_plan_t)."""
+
+    def __init__(self, handle: ctypes.c_void_p, device: int, in_max: int):
+        self._h = handle
+        self.device = device
+        self.in_max = in_max  # highest source shard index a launch reads
+        rows, k = ctypes.c_int(), ctypes.c_int()
+        N.check(lib.slime_rs_plan_shape(self._h, ctypes.byref(rows), ctypes.byref(k)))
+        self.rows, self.k = rows.value, k.value
+
+    @classmethod
+    def encode(cls, need: int, total: int, device: int = 0) -> "Plan":
+        h = ctypes.c_void_p()
+        N.check(lib.slime_rs_plan_encode(device, need, total, ctypes.byref(h)))
+        return cls(h, device, need - 1)
+
+    @classmethod
+    def reconstruct(cls, need: int, total: int, have: Sequence[int], want: Sequence[int], device: int = 0) -> "Plan":
+        h = ctypes.c_void_p()
+        hv = (ctypes.c_int * len(have))(*have)
+        wv = (ctypes.c_int * len(want))(*want)
+        N.check(lib.slime_rs_plan_reconstruct(device, need, total, hv, wv, len(want), ctypes.byref(h)))
+        return cls(h, device, max(have))
+
+    @classmethod
+    def matrix(cls, coeff: np.ndarray, in_shards: Sequence[int], device: int = 0) -> "Plan":
+        c = np.ascontiguousarray(coeff, dtype=np.uint32)
+        h = ctypes.c_void_p()
+        sv = (ctypes.c_int * len(in_shards))(*in_shards)
+        N.check(lib.slime_rs_plan_matrix(device, c.ctypes.data, c.shape[0], c.shape[1], sv, ctypes.byref(h)))
+        return cls(h, device, max(in_shards))
+
+    def coefficients(self) -> np.ndarray:
+        out = np.zeros((self.rows, self.k), dtype=np.uint32)
+        N.check(lib.slime_rs_plan_coefficients(self._h, out.ctypes.data))
+        return out
+
+    def __call__(self, src: torch.Tensor, src_layout: N.Layout, dst: torch.Tensor, dst_layout: N.Layout, L: int,
+                 nobj: int, stream: Optional[torch.cuda.Stream] = None, src_offset: int = 0,
+                 dst_offset: int = 0) -> None:
+        """Launch over nobj objects; offsets are in uint32 elements from the tensors' starts."""
+        for t in (src, dst):
+            if t.dtype not in (torch.int32, torch.uint32) or not t.is_contiguous():
+                raise TypeError("plan buffers must be contiguous int32/uint32 tensors")
+            if _dev_index(t) != self.device:
+                raise ValueError("tensor is not on the plan's device")
+        self._check_extent(src, src_offset, src_layout, L, nobj, self.in_max)
+        self._check_extent(dst, dst_offset, dst_layout, L, nobj, self.rows - 1)
+        N.check(lib.slime_rs_plan_execute(self._h, ctypes.c_void_p(src.data_ptr() + 4 * src_offset), src_layout,
+                                          ctypes.c_void_p(dst.data_ptr() + 4 * dst_offset), dst_layout, L, nobj,
+                                          _stream_handle(self.device, stream)))
+
+    @staticmethod
+    def _check_extent(t: torch.Tensor, off: int, lay: N.Layout, L: int, nobj: int, max_shard: int) -> None:
+        # Host-side bounds check before launching a hand-written kernel.
+        if nobj == 0 or L == 0:
+            return
+        last = off + (nobj - 1) * lay.obj_stride + max_shard * lay.shard_stride + L
+        if off < 0 or last > t.numel():
+            raise ValueError(f"layout addresses element {last} of a {t.numel()}-element tensor")
+
+    def close(self) -> None:
+        if self._h:
+            lib.slime_rs_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
+def fill_symbols(t: torch.Tensor, seed: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Deterministic synthetic symbols in [0, p) — word g is a function of (seed, g)."""
+    dev = _dev_index(t)
+    N.check(lib.slime_rs_fill_symbols(dev, ctypes.c_void_p(t.data_ptr()), t.numel(), seed & (2**64 - 1),
+                                      _stream_handle(dev, stream)))
+
+
+def pack_bytes(src: torch.Tensor, mapping: int, words: torch.Tensor, flags: Optional[torch.Tensor] = None,
+               stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Device MapToGFWith: uint8 tensor -> int32 word tensor (big-endian, XOR mapping)."""
+    dev = _dev_index(src)
+    if words.numel() < (src.numel() + 3) // 4:
+        raise ValueError("words tensor too small")
+    fp = ctypes.c_void_p(flags.data_ptr()) if flags is not None else None
+    N.check(lib.slime_gf_pack_device(ctypes.c_void_p(src.data_ptr()), src.numel(), mapping & 0xFFFFFFFF,
+                                     ctypes.c_void_p(words.data_ptr()), fp, _stream_handle(dev, stream)))
+
+
+def unpack_words(words: torch.Tensor, mapping: int, dst: torch.Tensor,
+                 stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Device MapFromGF: int32 word tensor -> uint8 tensor of 4x the length."""
+    dev = _dev_index(words)
+    if dst.numel() < 4 * words.numel():
+        raise ValueError("byte tensor too small")
+    N.check(lib.slime_gf_unpack_device(ctypes.c_void_p(words.data_ptr()), words.numel(), mapping & 0xFFFFFFFF,
+                                       ctypes.c_void_p(dst.data_ptr()), _stream_handle(dev, stream)))

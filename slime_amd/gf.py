@@ -1,0 +1,64 @@
+"""Python mirror of slime's ``internal/rs/gf`` Go API over the MI355X C-ABI.
+
+MaxVal, MInverse and Raise are host scalars; MapToGF / MapToGFWith /
+MapFromGF run their byte<->symbol codec on the GPU (gf_codec.hip).
+Reference: /root/reference/internal/rs/gf/{gf,map}.go.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+lib = N.lib
+
+MaxVal = 4294967291  # map.go:7  (1<<32 - 5)
+
+
+def MInverse(v: int) -> int:
+    """gf.go:5 — v^(p-2) mod p."""
+    return int(lib.slime_gf_minverse(v & 0xFFFFFFFF))
+
+
+def Raise(x: int, n: int) -> int:
+    """gf.go:46 — x^n mod p, Raise(x, 0) = 1."""
+    return int(lib.slime_gf_raise(x & 0xFFFFFFFF, n & 0xFFFFFFFF))
+
+
+def _bytes(b) -> np.ndarray:
+    return np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b, np.uint8)
+
+
+def MapToGF(data) -> tuple[int, np.ndarray]:
+    """map.go:15 — (mapping, symbols); mapping 0, else 1<<31, else a random fitting value."""
+    src = _bytes(data)
+    out = np.zeros((src.size + 3) // 4, dtype=np.uint32)
+    m = ctypes.c_uint32(0)
+    N.check(lib.slime_gf_map_to_gf(src.ctypes.data if src.size else None, src.size, ctypes.byref(m),
+                                   out.ctypes.data if out.size else None))
+    return int(m.value), out
+
+
+def MapToGFWith(data, n: int) -> np.ndarray:
+    """map.go:74 — big-endian symbols XOR n."""
+    src = _bytes(data)
+    out = np.zeros((src.size + 3) // 4, dtype=np.uint32)
+    N.check(lib.slime_gf_map_to_gf_with(src.ctypes.data if src.size else None, src.size, n & 0xFFFFFFFF,
+                                        out.ctypes.data if out.size else None))
+    return out
+
+
+def MapFromGF(n: int, v) -> bytes:
+    """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v))."""
+    words = np.ascontiguousarray(v, dtype=np.uint32)
+    out = np.zeros(words.size * 4, dtype=np.uint8)
+    N.check(lib.slime_gf_map_from_gf(n & 0xFFFFFFFF, words.ctypes.data if words.size else None, words.size,
+                                     out.ctypes.data if out.size else None))
+    return out.tobytes()
+
+
+def Seed(seed: int) -> None:
+    """Seed MapToGF's random-fallback candidate stream (reference: rand.Uint32())."""
+    lib.slime_gf_seed(seed & 0xFFFFFFFFFFFFFFFF)

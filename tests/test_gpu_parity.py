@@ -1,0 +1,308 @@
+"""GPU parity: the gfx950 HIP path (through the C-ABI) against the oracle.
+
+Bit-exact comparisons (integer field arithmetic) on seeded inputs at sizes the
+C oracle finishes in seconds, the committed golden vectors, the reference's
+KATs, and size-independent properties at full BASELINE sizes (encode -> erase
+-> reconstruct round trips, linearity).  Edge cases the reference admits:
+empty and ragged vectors, non-canonical symbols (x >= p, 0xFFFFFFFF), every
+erasure pattern at 4/6, unaligned layouts, k > 16 (generic kernel).
+"""
+import itertools
+import random
+
+import numpy as np
+import pytest
+
+import slime_amd
+from slime_amd import _native as N
+from slime_amd import gf, rs
+from oracle import oracle_c as OC
+from oracle import oracle_py as OP
+
+pytestmark = pytest.mark.gpu
+
+P = gf.MaxVal
+EDGES = np.array([0, 1, 2, P - 1, P, P + 1, P + 4, 0xFFFFFFFF, 0x7FFFFFFF, 0x80000000], dtype=np.uint32)
+
+
+def rand_vecs(rng, k, L, canonical=False, edges=True):
+    hi = P if canonical else 2**32
+    vs = [rng.integers(0, hi, size=L, dtype=np.uint64).astype(np.uint32) for _ in range(k)]
+    if edges and not canonical:
+        for v in vs:
+            n = min(L, EDGES.size)
+            v[rng.choice(L, size=n, replace=False)] = EDGES[:n]
+    return vs
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    assert N.device_count() > 0
+    return torch
+
+
+# ---------------------------------------------------------------- Go-API layer
+
+def test_create_parity_kats(kats):
+    for case in kats["create_parity"]:
+        assert rs.CreateParity(case["data"], case["index"]).tolist() == case["out"]
+
+
+def test_golden_encode_decode(golden):
+    for case in golden["encode"]:
+        for i, row in enumerate(case["parity"]):
+            assert rs.CreateParity(case["data"], case["need"] + i).tolist() == row
+        assert [r.tolist() for r in rs.CreateParities(case["data"], case["total"])] == case["parity"]
+    for case in golden["decode"]:
+        assert [r.tolist() for r in rs.RecoverData(case["chunks"], case["have"])] == case["data"]
+
+
+@pytest.mark.parametrize("need,total", [(1, 2), (2, 3), (3, 5), (4, 6), (6, 8), (8, 12), (10, 14), (16, 20),
+                                        (17, 20), (20, 24), (32, 36)])
+@pytest.mark.parametrize("L", [1, 3, 4, 5, 7, 64, 1001, 4096 + 3])
+def test_create_parity_vs_oracle(need, total, L):
+    rng = np.random.default_rng(need * 1000 + L)
+    data = rand_vecs(rng, need, L)
+    for idx in [0, need - 1] + list(range(need, total)):
+        rc, want = OC.create_parity(data, idx)
+        assert rc == 0
+        got = rs.CreateParity(data, idx)
+        assert np.array_equal(got, want), (need, total, L, idx)
+    allp = rs.CreateParities(data, total)
+    for i, row in enumerate(allp):
+        assert np.array_equal(row, OC.create_parity(data, need + i)[1])
+
+
+def test_create_parity_reuses_out_buffer():
+    data = [np.arange(10, dtype=np.uint32), np.arange(10, dtype=np.uint32) * 3]
+    buf = np.full(32, 7, dtype=np.uint32)
+    out = rs.CreateParity(data, 2, buf)
+    assert out.base is buf or out.ctypes.data == buf.ctypes.data
+    assert np.array_equal(out, OC.create_parity(data, 2)[1])
+    assert np.all(buf[10:] == 7)
+
+
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (17, 21)])
+def test_recover_data_vs_oracle(need, total):
+    rng = np.random.default_rng(need)
+    L = 777
+    data = rand_vecs(rng, need, L, canonical=True, edges=False)
+    code = data + [OC.create_parity(data, need + i)[1] for i in range(total - need)]
+    pyrng = random.Random(total)
+    sets = list(itertools.combinations(range(total), need))
+    pyrng.shuffle(sets)
+    for have in sets[:40]:
+        have = list(have)
+        pyrng.shuffle(have)  # any order, as RecoverData allows
+        chunks = [code[i] for i in have]
+        got = rs.RecoverData(chunks, have)
+        rc, want = OC.recover_data(chunks, have)
+        assert rc == 0
+        for g, w, d in zip(got, want, data):
+            assert np.array_equal(g, w) and np.array_equal(g, d)
+
+
+def test_recover_data_noncanonical_survivors_match_reference():
+    # Surviving data rows go through applyMatrix in the reference: x*1 mod p.
+    chunks = [np.array([P, P + 3, 0xFFFFFFFF, 5], dtype=np.uint32), np.array([1, 2, 3, 4], dtype=np.uint32)]
+    got = rs.RecoverData(chunks, [0, 2])
+    rc, want = OC.recover_data(chunks, [0, 2])
+    assert rc == 0
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    assert got[0].tolist() == [0, 3, 4, 5]
+
+
+def test_recover_data_ragged_longer_chunks():
+    a = np.arange(1, 9, dtype=np.uint32)
+    b = np.arange(1, 13, dtype=np.uint32)  # longer than chunks[0]: extra ignored (vector.go:80-85)
+    got = rs.RecoverData([a, b], [0, 2])
+    rc, want = OC.recover_data([a, b], [0, 2])
+    assert rc == 0 and all(np.array_equal(g, w) for g, w in zip(got, want))
+    assert all(g.size == 8 for g in got)
+
+
+def test_map_kats_on_gpu(kats):
+    for case in kats["map_trivial"]:
+        data = bytes(case["in"])
+        n, v = gf.MapToGF(data)
+        assert n == case["n"] and v.tolist() == case["v"]
+        assert gf.MapFromGF(n, v)[: len(data)] == data
+    gf.Seed(99)
+    for case in kats["map_tricky"]:
+        data = bytes(case)
+        n, v = gf.MapToGF(data)
+        assert all(int(x) < P for x in v)
+        assert gf.MapFromGF(n, v)[: len(data)] == data
+        assert np.array_equal(gf.MapToGFWith(data, n), v)
+
+
+def test_map_golden_and_random(golden):
+    for case in golden["map"]:
+        data = bytes(case["bytes"])
+        n, v = gf.MapToGF(data)
+        assert n == case["n"] and v.tolist() == case["words"]
+        assert list(gf.MapFromGF(n, v)) == case["back"]
+    rng = np.random.default_rng(5)
+    for length in [1, 2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 100003]:
+        data = rng.integers(0, 256, size=length, dtype=np.uint8).tobytes()
+        for m in (0, 1 << 31, 0x12345678):
+            assert np.array_equal(gf.MapToGFWith(data, m), OC.map_to_gf_with(data, m))
+        n, v = gf.MapToGF(data)
+        rc, n2, v2 = OC.map_to_gf(data)
+        assert rc == 0 and n == n2 and np.array_equal(v, v2)
+        assert gf.MapFromGF(n, v) == OC.map_from_gf(n, v)
+
+
+def test_map_to_gf_high_bit_mapping():
+    # Every word >= p forces mapping 1<<31 (map.go:47-62).
+    data = bytes([0xFF, 0xFF, 0xFF, 0xFB]) * 1000 + bytes([1, 2])
+    n, v = gf.MapToGF(data)
+    rc, n2, v2 = OC.map_to_gf(data)
+    assert rc == 0 and n == n2 == 1 << 31 and np.array_equal(v, v2)
+
+
+# ------------------------------------------------------- device-resident batch API
+
+def _objects(torch, nobj, n, L, seed):
+    from slime_amd import device as D
+    buf = torch.empty(nobj * n * L, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, seed)
+    return buf
+
+
+def _host(t, nobj, n, L):
+    return t.cpu().numpy().view(np.uint32).reshape(nobj, n, L)
+
+
+@pytest.mark.parametrize("need,total,L,nobj", [(2, 3, 1000, 3), (4, 6, 4096, 5), (8, 12, 12345, 4),
+                                               (10, 14, 8191, 3), (8, 12, 3, 7), (16, 20, 1024, 2),
+                                               (20, 24, 999, 2)])
+def test_plan_encode_vs_oracle(torch_dev, need, total, L, nobj):
+    torch = torch_dev
+    from slime_amd import device as D
+    buf = _objects(torch, nobj, total, L, seed=need * 7919 + L)
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    h = _host(buf, nobj, total, L)
+    for o in range(nobj):
+        ref = np.ascontiguousarray(h[o].copy())
+        OC.encode_object(ref, need, total)
+        assert np.array_equal(h[o], ref), o
+
+
+@pytest.mark.parametrize("need,total", [(4, 6), (8, 12)])
+def test_plan_reconstruct_every_pattern(torch_dev, need, total):
+    torch = torch_dev
+    from slime_amd import device as D
+    nobj, L = 2, 2052
+    buf = _objects(torch, nobj, total, L, seed=total)
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    h = _host(buf, nobj, total, L)
+    sets = list(itertools.combinations(range(total), need))
+    if len(sets) > 60:
+        random.Random(1).shuffle(sets)
+        sets = sets[:60] + [tuple(range(4, 12)), (1, 2, 4, 5, 6, 7, 9, 10)]
+    for have in sets:
+        want = [i for i in range(total) if i not in have]  # every lost shard, data and parity
+        plan = D.Plan.reconstruct(need, total, list(have), want)
+        out = torch.empty(nobj * len(want) * L, dtype=torch.int32, device="cuda")
+        plan(buf, lay, out, D.layout_of(len(want), L), L, nobj)
+        torch.cuda.synchronize()
+        got = _host(out, nobj, len(want), L)
+        for o in range(nobj):
+            for w_i, t in enumerate(want):
+                assert np.array_equal(got[o, w_i], h[o, t]), (have, t)
+
+
+def test_plan_matrix_unaligned_layouts_and_noncanonical(torch_dev):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(11)
+    k, rows, L, nobj = 5, 3, 1031, 3
+    shard, objs = L + 1, (L + 1) * k + 3  # odd strides: forces the one-column path
+    host = rng.integers(0, 2**32, size=nobj * objs + 1, dtype=np.uint64).astype(np.uint32)
+    host[:EDGES.size] = EDGES
+    src = torch.from_numpy(host.view(np.int32)).cuda()
+    coeff = rng.integers(0, P, size=(rows, k), dtype=np.uint64).astype(np.uint32)
+    coeff[0] = P - 1
+    plan = D.Plan.matrix(coeff, list(range(k)))
+    dst = torch.zeros(nobj * rows * L + 1, dtype=torch.int32, device="cuda")
+    plan(src, D.N.Layout(objs, shard), dst, D.N.Layout(rows * L, L), L, nobj, src_offset=1, dst_offset=1)
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy().view(np.uint32)[1:].reshape(nobj, rows, L)
+    for o in range(nobj):
+        ins = [host[1 + o * objs + j * shard: 1 + o * objs + j * shard + L] for j in range(k)]
+        want = OC.apply_matrix(coeff, ins)
+        for i in range(rows):
+            assert np.array_equal(got[o, i], want[i])
+
+
+def test_full_size_roundtrip_and_linearity(torch_dev):
+    """BASELINE C3/C4 shape (8/12, 256 MiB objects) on a few objects: properties."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, nobj = 8, 12, 2
+    L = (256 << 20) // 4 // need
+    buf = _objects(torch, nobj, total, L, seed=0x5113E)
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    # erase data {0,1,2,3}: rebuild from 4..11 (C4 worst case)
+    have, want = list(range(4, 12)), [0, 1, 2, 3]
+    out = torch.empty(nobj * 4 * L, dtype=torch.int32, device="cuda")
+    D.Plan.reconstruct(need, total, have, want)(buf, lay, out, D.layout_of(4, L), L, nobj)
+    torch.cuda.synchronize()
+    v = buf.view(nobj, total, L)
+    r = out.view(nobj, 4, L)
+    assert torch.equal(r, v[:, :4, :])
+    # mixed erasure {0,3,8,11}
+    have2 = [1, 2, 4, 5, 6, 7, 9, 10]
+    out2 = torch.empty(nobj * 4 * L, dtype=torch.int32, device="cuda")
+    D.Plan.reconstruct(need, total, have2, [0, 3, 8, 11])(buf, lay, out2, D.layout_of(4, L), L, nobj)
+    torch.cuda.synchronize()
+    r2 = out2.view(nobj, 4, L)
+    for i, t in enumerate([0, 3, 8, 11]):
+        assert torch.equal(r2[:, i, :], v[:, t, :])
+    # sampled columns against the C oracle
+    h = v[0].cpu().numpy().view(np.uint32)
+    cols = np.random.default_rng(0).choice(L, size=4096, replace=False)
+    ref = OC.apply_matrix(rs.ParityMatrix(need, total - need)[need:], [h[j, cols] for j in range(need)])
+    for i in range(total - need):
+        assert np.array_equal(h[need + i, cols], ref[i])
+    del buf, out, out2
+    torch.cuda.empty_cache()
+
+
+def test_codec_device_roundtrip(torch_dev):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(2)
+    for n in (1, 3, 4, 17, 1 << 20, (1 << 20) + 5):
+        raw = rng.integers(0, 256, size=n, dtype=np.uint8)
+        src = torch.from_numpy(raw).cuda()
+        words = torch.empty((n + 3) // 4, dtype=torch.int32, device="cuda")
+        flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+        D.pack_bytes(src, 0x80000000, words, flags)
+        back = torch.empty(4 * words.numel(), dtype=torch.uint8, device="cuda")
+        D.unpack_words(words, 0x80000000, back)
+        torch.cuda.synchronize()
+        assert np.array_equal(words.cpu().numpy().view(np.uint32), OC.map_to_gf_with(raw.tobytes(), 0x80000000))
+        assert back.cpu().numpy()[:n].tobytes() == raw.tobytes()
+
+
+def test_fill_symbols_deterministic_and_canonical(torch_dev):
+    torch = torch_dev
+    from slime_amd import device as D
+    a = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
+    b = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
+    D.fill_symbols(a, 42)
+    D.fill_symbols(b, 42)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert int(a.cpu().numpy().view(np.uint32).max()) < P

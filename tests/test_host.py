@@ -1,0 +1,159 @@
+"""CPU tests of the product's host side: library boundary, exact matrices,
+and the reference's validation/panic behaviour (all reached before any device
+work).  No compute calls are made without a GPU except to check that they
+fail loudly."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import slime_amd
+from slime_amd import _native as N
+from slime_amd import gf, rs
+from oracle import oracle_c as OC
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HAS_GPU = N.device_count() > 0
+P = gf.MaxVal
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "slime_rs.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(slime_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    syms = header_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(N.lib, s), s
+    declared = {name for name, _, _ in N.SIGNATURES}
+    assert declared == set(syms), set(syms) ^ declared
+
+
+def test_library_is_in_tree_and_built_for_gfx950():
+    assert N.LIB_PATH.startswith(os.path.join(ROOT, "slime_amd", "lib"))
+    blob = open(N.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_max_val_and_scalars():
+    assert N.lib.slime_gf_max_val() == P == 4294967291
+    rng = np.random.default_rng(0)
+    for v in rng.integers(1, P, size=200, dtype=np.uint64):
+        v = int(v)
+        assert gf.MInverse(v) == OC.minverse(v)
+        assert (gf.MInverse(v) * v) % P == 1
+    for x, n in [(0, 0), (0, 5), (1, 9), (3, 0), (7, 13), (P, 1), (P + 1, 3), (0xFFFFFFFF, 7), (12345, P - 2)]:
+        assert gf.Raise(x, n) == OC.raise_(x & 0xFFFFFFFF, n)
+
+
+def test_vandermonde_and_parity_kats(kats):
+    for case in kats["vandermonde"]:
+        assert rs.vandermondeMatrix(case["d"], case["p"]).tolist() == case["m"]
+    for case in kats["parity_matrix"]:
+        assert rs.ParityMatrix(case["d"], case["p"]).tolist() == case["m"]
+        assert rs.ParityMatrixCached(case["d"], case["p"]).tolist() == case["m"]
+
+
+def test_parity_matrices_match_oracle():
+    for d in range(1, 21):
+        for p in (0, 1, 2, 4, 7, 20):
+            assert np.array_equal(rs.ParityMatrix(d, p), OC.parity_matrix(d, p)), (d, p)
+
+
+def test_parity_matrix_cached_is_shared_and_read_only():
+    a = rs.ParityMatrixCached(8, 4)
+    b = rs.ParityMatrixCached(8, 4)
+    assert a.ctypes.data == b.ctypes.data
+    with pytest.raises(ValueError):
+        a[0, 0] = 7
+
+
+def test_inverses_match_golden(golden):
+    for case in golden["inverses"]:
+        full = rs.ParityMatrix(case["need"], case["total"] - case["need"])
+        inv = rs.invertMatrix(full[case["have"]])
+        assert inv.tolist() == case["inv"]
+
+
+def test_solve_sub_identity_and_clone():
+    m = rs.vandermondeMatrix(5, 3)
+    c = rs.cloneMatrix(m)
+    rs.solveSubIdentity(c)
+    assert np.array_equal(c, rs.ParityMatrix(5, 3))
+    assert not np.array_equal(c, m)
+
+
+def test_singular_matrix_panics_like_reference():
+    m = rs.ParityMatrix(4, 2)
+    with pytest.raises(slime_amd.Panic, match=r"^Couldn't ensure nonzero m\[i\]\[i\]$"):
+        rs.invertMatrix(m[[0, 1, 1, 2]])
+
+
+# ---- the reference's panics from CreateParity / RecoverData (vector.go) ----
+
+def test_create_parity_varying_length_panics():
+    with pytest.raises(slime_amd.Panic, match="^CreateParity called on data chunks of varying length$"):
+        rs.CreateParity([[1, 2], [1, 2, 3]], 2)
+
+
+def test_create_parity_index_out_of_range():
+    with pytest.raises(slime_amd.Panic, match="index out of range"):
+        rs.CreateParity([], 0)
+    with pytest.raises(slime_amd.Panic, match="index out of range"):
+        rs.CreateParity([[1], [2]], -1)
+
+
+def test_recover_data_panics():
+    with pytest.raises(slime_amd.Panic, match=r"^RecoverData: len\(chunks\) != len\(indices\)$"):
+        rs.RecoverData([[1], [2]], [0])
+    with pytest.raises(slime_amd.Panic, match=r"^RecoverData: len\(chunks\) == 0$"):
+        rs.RecoverData([], [])
+    with pytest.raises(slime_amd.Panic, match="^RecoverData: No indices given$"):
+        rs.RecoverData([[1]], [-1])
+    with pytest.raises(slime_amd.Panic, match=r"^Couldn't ensure nonzero m\[i\]\[i\]$"):
+        rs.RecoverData([[1], [2]], [3, 3])
+    with pytest.raises(slime_amd.Panic, match="index out of range"):
+        rs.RecoverData([[1, 2], [2]], [0, 2])
+
+
+def test_zero_length_vectors_need_no_device():
+    assert rs.CreateParity([[], []], 3).size == 0
+    assert [x.size for x in rs.RecoverData([[], []], [2, 3])] == [0, 0]
+
+
+@pytest.mark.skipif(HAS_GPU, reason="checks the no-device failure mode")
+def test_compute_without_device_fails_loudly():
+    with pytest.raises(slime_amd.NativeError) as e:
+        rs.CreateParity([[1, 2], [3, 4]], 2)
+    assert e.value.code == N.ERR_NO_DEVICE
+    with pytest.raises(slime_amd.NativeError):
+        gf.MapToGF(b"abcd")
+    h = ctypes.c_void_p()
+    assert N.lib.slime_rs_plan_encode(0, 8, 12, ctypes.byref(h)) == N.ERR_NO_DEVICE
+
+
+def test_status_strings_are_reference_panics():
+    expect = {
+        1: "CreateParity called on data chunks of varying length",
+        2: "RecoverData: len(chunks) != len(indices)",
+        3: "RecoverData: len(chunks) == 0",
+        4: "RecoverData: No indices given",
+        5: "Couldn't ensure nonzero m[i][i]",
+        6: "Couldn't ensure one m[i][i]",
+        7: "Couldn't ensure zero m[i][j]",
+    }
+    for code, text in expect.items():
+        assert N.lib.slime_rs_status_string(code).decode() == text
+
+
+def test_product_never_imports_oracle():
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "slime_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("oracle/", ""), f

@@ -1,0 +1,48 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, smoke, microbenchmarks, bench, rocprofv3.
+# Usage (from the repo root, on the GPU box):  bash tools/gpu_session.sh [steps...]
+#   steps: tests smoke micro bench prof pmc   (default: all but pmc)
+# Every GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or
+# a signal) ends the session immediately.  A plain test failure (exit 1) is
+# recorded and the session continues.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=("$@")
+[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke micro bench prof)
+
+run() {  # run <name> <limit-seconds> <command...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "!!! $name ended with rc=$rc: stopping the session" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+  return 0
+}
+
+has() { for s in "${STEPS[@]}"; do [ "$s" = "$1" ] && return 0; done; return 1; }
+
+rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || true
+nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+
+has tests && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+has smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+has micro && run micro 600 python tools/microbench.py
+has bench && run bench 600 python bench.py
+has prof && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
+  python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0
+if has pmc; then
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o bench --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0
+fi
+echo "=== session done" | tee -a "$OUT/session.log"
