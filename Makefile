@@ -34,3 +34,15 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# Micro-benchmarks (tools only): make ubench
+ubench: tools/libubench.so
+tools/libubench.so: tools/ubench.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: ubench
+
+# Apply-kernel variant harness (tools only): make applyvar
+applyvar: tools/libapplyvar.so
+tools/libapplyvar.so: tools/apply_variants.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: applyvar

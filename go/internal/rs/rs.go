@@ -1,0 +1,238 @@
+// Package rs implements Reed-Solomon erasure coding using Vandermonde
+// coefficient matricies over GF(2^32-5).
+//
+// This is the drop-in replacement for encryptio/slime's internal/rs: the same
+// exported API (CreateParity, RecoverData, ParityMatrix, ParityMatrixCached)
+// and the unexported helpers the reference's own tests call
+// (vandermondeMatrix, solveSubIdentity, cloneMatrix, invertMatrix), backed by
+// the MI355X (gfx950) HIP implementation in libslime_rs.so through its C-ABI
+// (include/slime_rs.h).  Panics carry the reference's exact messages.
+//
+// Build: `make` at the slime-rs-mi355x repo root, then point cgo at it, e.g.
+//   CGO_CFLAGS=-I$SLIME_RS/include CGO_LDFLAGS="-L$SLIME_RS/slime_amd/lib -lslime_rs"
+package rs
+
+/*
+#cgo LDFLAGS: -lslime_rs
+#include <stdint.h>
+#include <stdlib.h>
+#include "slime_rs.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"runtime"
+	"sync"
+	"unsafe"
+)
+
+// raise turns a C-ABI status into the reference's panic.
+func raise(rc C.int) {
+	if rc == C.SLIME_RS_OK {
+		return
+	}
+	if rc >= 1 && rc <= 7 {
+		panic(C.GoString(C.slime_rs_status_string(rc)))
+	}
+	if rc == C.SLIME_RS_ERR_INDEX_RANGE {
+		panic(C.GoString(C.slime_rs_last_error()))
+	}
+	panic(fmt.Sprintf("slime_rs: %s: %s", C.GoString(C.slime_rs_status_string(rc)), C.GoString(C.slime_rs_last_error())))
+}
+
+// vectors pins the backing arrays of vs and returns a C array of their data
+// pointers plus their lengths (cgo forbids Go pointers in C memory unless
+// pinned; runtime.Pinner, Go >= 1.21).  Call free() when C has returned.
+type vectors struct {
+	ptrs   **C.uint32_t
+	lens   *C.uint64_t
+	pinner runtime.Pinner
+}
+
+func marshal(vs [][]uint32) *vectors {
+	n := len(vs)
+	if n == 0 {
+		n = 1
+	}
+	m := &vectors{
+		ptrs: (**C.uint32_t)(C.calloc(C.size_t(n), C.size_t(unsafe.Sizeof(uintptr(0))))),
+		lens: (*C.uint64_t)(C.calloc(C.size_t(n), 8)),
+	}
+	ps := unsafe.Slice(m.ptrs, n)
+	ls := unsafe.Slice(m.lens, n)
+	for i, v := range vs {
+		ls[i] = C.uint64_t(len(v))
+		if cap(v) > 0 {
+			p := &v[:1][0]
+			m.pinner.Pin(p)
+			ps[i] = (*C.uint32_t)(unsafe.Pointer(p))
+		}
+	}
+	return m
+}
+
+func (m *vectors) free() {
+	m.pinner.Unpin()
+	C.free(unsafe.Pointer(m.ptrs))
+	C.free(unsafe.Pointer(m.lens))
+}
+
+func matrixFromC(p *C.uint32_t, rows, cols int) [][]uint32 {
+	underlying := make([]uint32, rows*cols)
+	if rows*cols > 0 {
+		copy(underlying, unsafe.Slice((*uint32)(unsafe.Pointer(p)), rows*cols))
+	}
+	m := make([][]uint32, rows)
+	for i := range m {
+		m[i] = underlying[i*cols : (i+1)*cols : (i+1)*cols]
+	}
+	return m
+}
+
+func flatten(m [][]uint32) []uint32 {
+	if len(m) == 0 {
+		return nil
+	}
+	out := make([]uint32, 0, len(m)*len(m[0]))
+	for _, r := range m {
+		out = append(out, r...)
+	}
+	return out
+}
+
+// CreateParity returns code row `index` of the equal-length data vectors
+// (internal/rs/vector.go:18), computed on the GPU; `out` is reused when its
+// capacity allows.
+func CreateParity(data [][]uint32, index int, out []uint32) []uint32 {
+	for i := 1; i < len(data); i++ {
+		if len(data[i]) != len(data[0]) {
+			panic("CreateParity called on data chunks of varying length")
+		}
+	}
+	if len(data) == 0 {
+		_ = data[0] // the reference's index-out-of-range panic
+	}
+	if cap(out) < len(data[0]) {
+		out = make([]uint32, len(data[0]))
+	} else {
+		out = out[:len(data[0])]
+	}
+	m := marshal(data)
+	defer m.free()
+	var op *C.uint32_t
+	if len(out) > 0 {
+		var pin runtime.Pinner
+		pin.Pin(&out[0])
+		defer pin.Unpin()
+		op = (*C.uint32_t)(unsafe.Pointer(&out[0]))
+	}
+	raise(C.slime_rs_create_parity(m.ptrs, m.lens, C.int(len(data)), C.int(index), op))
+	return out
+}
+
+// CreateParities computes every parity row total-len(data)..total-1 in one GPU
+// pass (multi_store.go:528-531 calls CreateParity once per row instead).
+func CreateParities(data [][]uint32, total int) [][]uint32 {
+	for i := 1; i < len(data); i++ {
+		if len(data[i]) != len(data[0]) {
+			panic("CreateParity called on data chunks of varying length")
+		}
+	}
+	outs := make([][]uint32, total-len(data))
+	for i := range outs {
+		outs[i] = make([]uint32, len(data[0]))
+	}
+	m := marshal(data)
+	defer m.free()
+	o := marshal(outs)
+	defer o.free()
+	raise(C.slime_rs_create_parities(m.ptrs, m.lens, C.int(len(data)), C.int(total), o.ptrs))
+	return outs
+}
+
+// RecoverData rebuilds all data vectors from exactly len(chunks) surviving code
+// rows with the given indices (internal/rs/vector.go:50), on the GPU.
+func RecoverData(chunks [][]uint32, indices []int) [][]uint32 {
+	if len(chunks) != len(indices) {
+		panic("RecoverData: len(chunks) != len(indices)")
+	}
+	if len(chunks) == 0 {
+		panic("RecoverData: len(chunks) == 0")
+	}
+	data := make([][]uint32, len(chunks))
+	for i := range data {
+		data[i] = make([]uint32, len(chunks[0]))
+	}
+	idx := (*C.int)(C.calloc(C.size_t(len(indices)), C.size_t(unsafe.Sizeof(C.int(0)))))
+	defer C.free(unsafe.Pointer(idx))
+	is := unsafe.Slice(idx, len(indices))
+	for i, v := range indices {
+		is[i] = C.int(v)
+	}
+	m := marshal(chunks)
+	defer m.free()
+	o := marshal(data)
+	defer o.free()
+	raise(C.slime_rs_recover_data(m.ptrs, m.lens, C.int(len(chunks)), idx, C.int(len(indices)), o.ptrs))
+	return data
+}
+
+// vandermondeMatrix: (d+p) x d, entry [i][j] = (j+1)^i mod p (host, exact).
+func vandermondeMatrix(d, p int) [][]uint32 {
+	buf := make([]C.uint32_t, (d+p)*d+1)
+	raise(C.slime_rs_vandermonde_matrix(C.int(d), C.int(p), &buf[0]))
+	return matrixFromC(&buf[0], d+p, d)
+}
+
+// ParityMatrix: the systematic (d+p) x d code matrix (identity on top; any d
+// rows invertible), computed exactly on the host by libslime_rs.
+func ParityMatrix(d, p int) [][]uint32 {
+	buf := make([]C.uint32_t, (d+p)*d+1)
+	raise(C.slime_rs_parity_matrix(C.int(d), C.int(p), &buf[0]))
+	return matrixFromC(&buf[0], d+p, d)
+}
+
+var parityCache sync.Map // struct{ d, p int } -> [][]uint32
+
+// ParityMatrixCached: process-wide memo of ParityMatrix; callers must not
+// modify the returned rows (shared, as in the reference).
+func ParityMatrixCached(d, p int) [][]uint32 {
+	key := struct{ d, p int }{d, p}
+	if v, ok := parityCache.Load(key); ok {
+		return v.([][]uint32)
+	}
+	v, _ := parityCache.LoadOrStore(key, ParityMatrix(d, p))
+	return v.([][]uint32)
+}
+
+// solveSubIdentity column-reduces m in place so its top square block becomes
+// the identity; singular input panics with the reference's message.
+func solveSubIdentity(m [][]uint32) {
+	flat := flatten(m)
+	rc := C.slime_rs_solve_sub_identity((*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(len(m)), C.int(len(m[0])))
+	for i := range m {
+		copy(m[i], flat[i*len(m[0]):(i+1)*len(m[0])])
+	}
+	raise(rc)
+}
+
+// cloneMatrix deep-copies m into rows that share one backing array.
+func cloneMatrix(m [][]uint32) [][]uint32 {
+	flat := flatten(m)
+	n := make([][]uint32, len(m))
+	off := 0
+	for i, r := range m {
+		n[i] = flat[off : off+len(r) : off+len(r)]
+		off += len(r)
+	}
+	return n
+}
+
+func invertMatrix(m [][]uint32) [][]uint32 {
+	flat := flatten(m)
+	d := len(m[0])
+	inv := make([]C.uint32_t, d*d)
+	raise(C.slime_rs_invert_matrix((*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(d), &inv[0]))
+	return matrixFromC(&inv[0], d, d)
+}

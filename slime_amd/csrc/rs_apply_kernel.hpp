@@ -1,0 +1,141 @@
+// The GF(2^32-5) shard-matrix apply kernel template (device code), shared by
+// the product instantiations (rs_apply.hip) and the tuning harness
+// (tools/apply_variants.hip).  See rs_apply.hip for the design notes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gfp.hpp"
+
+namespace slime {
+namespace apply {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+// Device coefficient tables: rows padded to 16 words (64 B) for k <= 16 so a
+// row arrives in one s_load_dwordx16; row stride k for the generic kernel.
+constexpr int kCoeffStride = 16;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint32_t* p) {
+  u32x4 v;
+  if constexpr (NT)
+    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else
+    v = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint32_t* p, uint4 r) {
+  const u32x4 v = {r.x, r.y, r.z, r.w};
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  else
+    *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// One column per lane (tails, unaligned layouts, generic k).
+template <int K>
+__device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, uint32_t* __restrict__ ob,
+                                             const uint32_t* __restrict__ coeff,
+                                             const uint32_t* __restrict__ in_idx, uint64_t in_shard,
+                                             const uint32_t* __restrict__ out_idx, uint64_t out_shard,
+                                             uint32_t rows, uint32_t k, uint64_t b) {
+  if constexpr (K > 0) {
+    uint32_t x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ib[(uint64_t)in_idx[j] * in_shard + b];
+    for (uint32_t i = 0; i < rows; ++i) {
+      const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+      uint64_t lo = 0;
+      uint32_t hi = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) mac(lo, hi, x[j], c[j]);
+      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
+    }
+  } else {
+    for (uint32_t i = 0; i < rows; ++i) {
+      const uint32_t* c = coeff + (uint64_t)i * k;
+      uint64_t lo = 0;
+      uint32_t hi = 0;
+      for (uint32_t j = 0; j < k; ++j) mac(lo, hi, ib[(uint64_t)in_idx[j] * in_shard + b], c[j]);
+      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
+    }
+  }
+}
+
+// Accumulate one output row over 4 columns and store it.
+template <int K, bool NTS>
+__device__ __forceinline__ void row4(const uint4 (&x)[K], const u32x16& c, uint32_t* dst) {
+  uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
+  uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+  uint4 r;
+  r.x = fold96(lo0, hi0);
+  r.y = fold96(lo1, hi1);
+  r.z = fold96(lo2, hi2);
+  r.w = fold96(lo3, hi3);
+  st16<NTS>(dst, r);
+}
+
+// K > 0: compile-time number of input shards (1..16), 4 columns (16 B) per
+// lane per unit; a wave owns U*64 consecutive 16-byte units (U*1 KiB of every
+// shard stripe) per step, so each load instruction is a fully coalesced 1 KiB
+// and the wave streams U KiB contiguous per shard.  K == 0: generic k.
+// Objects: blockIdx.y strides over objects, so gridDim.y bounds how many
+// objects (x shards) are streamed concurrently.
+template <int K, bool VEC, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void rs_apply_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k) {
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
+  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+    const uint32_t* __restrict__ ib = in + (uint64_t)obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + (uint64_t)obj * out_obj_stride;
+    uint64_t done = 0;
+    if constexpr (VEC && K > 0) {
+      uint64_t ioff[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
+      const uint64_t nvec = ncols >> 2;
+      const uint32_t lane = threadIdx.x & 63;
+      const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+      const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+      const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+      for (uint64_t t = wave; t < ntiles; t += nwaves) {
+        const uint64_t g0 = t * (64 * U) + lane;
+        uint4 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t b = (g0 + 64 * u) << 2;
+          if (g0 + 64 * u < nvec) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[u][j] = ld16<NTL>(ib + ioff[j] + b);
+          }
+        }
+        for (uint32_t i = 0; i < rows; ++i) {
+          // One 64-byte row -> one s_load_dwordx16 (SGPRs).
+          const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+          uint32_t* const orow = ob + (uint64_t)out_idx[i] * out_shard;
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (g0 + 64 * u < nvec) row4<K, NTS>(x[u], c, orow + ((g0 + 64 * u) << 2));
+        }
+      }
+      done = nvec << 2;
+    }
+    for (uint64_t b = done + tid; b < ncols; b += nthr) apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx,
+                                                                        out_shard, rows, k, b);
+  }
+}
+
+}  // namespace apply
+}  // namespace slime

@@ -1,0 +1,46 @@
+// Tuning harness: variants of the product apply kernel template
+// (slime_amd/csrc/rs_apply_kernel.hpp) for A/B timing in one process.
+// Built into tools/libapplyvar.so by `make applyvar`; tools only.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rs_apply_kernel.hpp"
+
+using namespace slime::apply;
+
+namespace {
+template <int K, int U, bool NTL, bool NTS>
+void go(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os, const uint32_t* coeff,
+        const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy,
+        hipStream_t s) {
+  hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
+                     os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K);
+}
+}  // namespace
+
+extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is,
+                         uint64_t oo, uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                         uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define V(id, U, NTL, NTS)                                                                           \
+  case id:                                                                                          \
+    if (k == 8) go<8, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);   \
+    else if (k == 10) go<10, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s); \
+    else if (k == 4) go<4, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);  \
+    else return -2;                                                                                 \
+    break;
+  switch (variant) {
+    V(0, 1, true, false)
+    V(1, 1, false, false)
+    V(2, 1, true, true)
+    V(3, 1, false, true)
+    V(4, 2, true, false)
+    V(5, 2, false, false)
+    V(6, 2, true, true)
+    V(7, 2, false, true)
+    default:
+      return -1;
+  }
+#undef V
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""A/B the apply-kernel variants (tools/apply_variants.hip) on the C3/C4 shape.
+
+Variants: U (16-byte units per lane per step: 1 or 2, the wave streaming 1 or
+2 KiB of every shard), nt loads, nt stores; geometries: total resident blocks
+x objects in flight.  Interleaved rounds in one process (cdna guide rule 24);
+every variant's output is checked bit-exact against the product kernel.
+
+    make applyvar && python tools/apply_variants.py [--need 8 --total 12 --mib 256 --nobj 128]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import itertools
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from slime_amd import device as D  # noqa: E402
+
+VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain", 6: "U2 ntL ntS",
+            7: "U2 ntS"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--need", type=int, default=8)
+    ap.add_argument("--total", type=int, default=12)
+    ap.add_argument("--mib", type=int, default=256)
+    ap.add_argument("--nobj", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
+    lib.av_launch.restype = ctypes.c_int
+    lib.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_uint32, ctypes.c_void_p]
+    need, total, nobj = args.need, args.total, args.nobj
+    r = total - need
+    L = (args.mib << 20) // 4 // need
+    buf = torch.empty(nobj * total * L, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, 7)
+    lay = D.layout_of(total, L)
+    enc = D.Plan.encode(need, total)
+    enc(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    ref = buf.view(nobj, total, L)[:, need:, :].clone()
+
+    coeff = np.zeros((r, 16), dtype=np.uint32)
+    coeff[:, :need] = enc.coefficients()
+    c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
+    ii = torch.arange(need, dtype=torch.int32, device="cuda")
+    oi = torch.arange(need, total, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+
+    def launch(v, gx, gy):
+        rc = lib.av_launch(v, need, buf.data_ptr(), buf.data_ptr(), total * L, L, total * L, L, c_t.data_ptr(),
+                           ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream))
+        assert rc == 0, rc
+
+    geos = [(t, y) for t, y in itertools.product((512, 1024, 2048), (nobj, 32, 8, 2)) if y <= nobj]
+    times = {(v, g): [] for v in VARIANTS for g in geos}
+    for _ in range(args.rounds):
+        for v in VARIANTS:
+            for t, y in geos:
+                gx = max(1, t // y)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                launch(v, gx, y)
+                b.record(s)
+                torch.cuda.synchronize()
+                times[(v, (t, y))].append(a.elapsed_time(b))
+    # correctness of every variant (last geometry run of each)
+    bad = []
+    for v in VARIANTS:
+        buf.view(nobj, total, L)[:, need:, :].zero_()
+        launch(v, 4, 8)
+        torch.cuda.synchronize()
+        if not torch.equal(buf.view(nobj, total, L)[:, need:, :], ref):
+            bad.append(v)
+    alg = nobj * 4 * L * total
+    rows = []
+    for (v, (t, y)), ts in times.items():
+        med = statistics.median(ts)
+        rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "ms": round(med, 3),
+                     "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
+    rows.sort(key=lambda x: -x["GBps"])
+    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj}", "bad_variants": bad, "top": rows[:12],
+                      "all": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

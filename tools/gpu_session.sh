@@ -39,6 +39,13 @@ has micro && run micro 600 python tools/microbench.py
 has bench && run bench 600 python bench.py
 has prof && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
   python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0
+has ubench && run ubench 600 python tools/ubench.py
+has variants && run variants 600 python tools/apply_variants.py
+if has grid; then
+  for g in 1024 4096 8192; do
+    run bench_grid$g 300 env SLIME_RS_GRID_TARGET=$g python bench.py --steps 5 --cpu-baseline 0
+  done
+fi
 if has pmc; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0

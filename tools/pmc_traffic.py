@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py into HBM bytes per launch.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): counters are in KiB; FETCH_SIZE
+reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
+so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
+
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> > profiles/pmc_traffic.json
+"""
+import csv
+import glob
+import json
+import sys
+
+
+def per_dispatch(d, counter):
+    vals = {}
+    for path in glob.glob(f"{d}/*counter_collection.csv"):
+        for r in csv.DictReader(open(path)):
+            if "rs_apply_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[int(r["Dispatch_Id"])] = float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    fetch_dir, write_dir, config = sys.argv[1:4]
+    f = per_dispatch(fetch_dir, "FETCH_SIZE")
+    w = per_dispatch(write_dir, "WRITE_SIZE")
+    fetch_kib = sum(f.values()) / len(f)
+    write_kib = sum(w.values()) / len(w)
+    read_bytes = 2 * fetch_kib * 1024
+    write_bytes = write_kib * 1024
+    print(json.dumps({
+        "config": config,
+        "kernel": "rs_apply_kernel",
+        "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
+        "fetch_size_kib_avg": fetch_kib,
+        "write_size_kib_avg": write_kib,
+        "read_bytes_per_launch": int(read_bytes),
+        "write_bytes_per_launch": int(write_bytes),
+        "hbm_bytes_per_launch": int(read_bytes + write_bytes),
+        "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream undercount), x1024 (KiB)",
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+// Micro-benchmarks that bound the RS apply kernel on gfx950 (tools only; not
+// part of libslime_rs).  Built into tools/libubench.so by `make ubench`.
+//
+//   copy16       d[i] = s[i], 16 B/lane                     -> HBM copy ceiling
+//   read16       sum of 16 B/lane loads, one store per lane -> HBM read ceiling
+//   write16      16 B/lane stores                           -> HBM write ceiling
+//   pattern      the apply kernel's exact access pattern (K stripes read,
+//                R stripes written, 16 B/lane) with XOR in place of the
+//                field math                                  -> pattern ceiling
+//   compute      the apply kernel's exact math on register-generated symbols
+//                (no loads; one store per lane at the end)  -> VALU ceiling
+//   mad          independent v_mad_u64_u32 chains          -> mad issue rate
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gfp.hpp"
+
+using namespace slime;
+
+namespace {
+constexpr int B = 256;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint4 ld(const uint32_t* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__global__ __launch_bounds__(B) void copy16(const uint4* __restrict__ s, uint4* __restrict__ d, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x; i < n; i += (uint64_t)gridDim.x * B) d[i] = s[i];
+}
+
+__global__ __launch_bounds__(B) void read16(const uint4* __restrict__ s, uint32_t* __restrict__ d, uint64_t n) {
+  uint32_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x; i < n; i += (uint64_t)gridDim.x * B) {
+    const uint4 v = s[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  d[(uint64_t)blockIdx.x * B + threadIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(B) void write16(uint4* __restrict__ d, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * B + threadIdx.x; i < n; i += (uint64_t)gridDim.x * B)
+    d[i] = make_uint4((uint32_t)i, 1, 2, 3);
+}
+
+template <int K>
+__global__ __launch_bounds__(B) void pattern(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                             uint64_t obj, uint64_t shard, uint64_t oobj, uint64_t oshard,
+                                             uint64_t ncols, uint32_t rows) {
+  const uint32_t* ib = in + (uint64_t)blockIdx.y * obj;
+  uint32_t* ob = out + (uint64_t)blockIdx.y * oobj;
+  for (uint64_t g = (uint64_t)blockIdx.x * B + threadIdx.x; g < ncols / 4; g += (uint64_t)gridDim.x * B) {
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld(ib + j * shard + 4 * g);
+    for (uint32_t i = 0; i < rows; ++i) {
+      uint4 r = make_uint4(i, i, i, i);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        r.x ^= x[j].x;
+        r.y ^= x[j].y;
+        r.z ^= x[j].z;
+        r.w ^= x[j].w;
+      }
+      *reinterpret_cast<uint4*>(ob + i * oshard + 4 * g) = r;
+    }
+  }
+}
+
+// Same math as rs_apply_kernel<K, true>, symbols generated in registers.
+template <int K>
+__global__ __launch_bounds__(B) void compute(const uint32_t* __restrict__ coeff, uint32_t* __restrict__ sink,
+                                             uint64_t iters, uint32_t rows) {
+  uint4 x[K];
+  const uint32_t t = blockIdx.x * B + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = make_uint4(t * 2654435761u + j, t ^ (j * 40503u), t + 977u * j, ~t - j);
+  uint32_t acc = 0;
+  for (uint64_t it = 0; it < iters; ++it) {
+    for (uint32_t i = 0; i < rows; ++i) {
+      const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + i * 16);
+      uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
+      uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+      acc += fold96(lo0, hi0) ^ fold96(lo1, hi1) ^ fold96(lo2, hi2) ^ fold96(lo3, hi3);
+    }
+    x[0].x += acc;  // keep iterations dependent on the results
+  }
+  sink[t] = acc;
+}
+
+// Throughput of the MAC primitive itself (mac4: 4 x v_mad_u64_u32 + 4 x
+// v_addc_co_u32 per statement), two independent groups per iteration.
+__global__ __launch_bounds__(B) void mad(uint32_t* __restrict__ sink, uint32_t c, uint64_t iters) {
+  const uint32_t t = blockIdx.x * B + threadIdx.x;
+  uint64_t l0 = t, l1 = t + 1, l2 = t + 2, l3 = t + 3, l4 = t + 4, l5 = t + 5, l6 = t + 6, l7 = t + 7;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0, h7 = 0;
+  const uint32_t x0 = t * 7u + 1u, x1 = t ^ 0x55u, x2 = t + 99u, x3 = ~t;
+  for (uint64_t i = 0; i < iters; ++i) {
+    mac4(l0, l1, l2, l3, h0, h1, h2, h3, x0, x1, x2, x3, c);
+    mac4(l4, l5, l6, l7, h4, h5, h6, h7, x3, x2, x1, x0, c);
+  }
+  sink[t] = (uint32_t)(l0 ^ l1 ^ l2 ^ l3 ^ l4 ^ l5 ^ l6 ^ l7) + h0 + h1 + h2 + h3 + h4 + h5 + h6 + h7;
+}
+
+hipEvent_t e0, e1;
+float time_ms(void (*launch)(void*), void* arg, int reps) {
+  launch(arg);
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < reps; ++i) launch(arg);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms / reps;
+}
+
+struct Args {
+  void *a, *b;
+  uint64_t n, obj, shard, oobj, oshard, ncols, iters;
+  uint32_t nobj, rows, k, grid;
+  const uint32_t* coeff;
+};
+}  // namespace
+
+extern "C" {
+
+int ub_init() {
+  if (hipEventCreate(&e0) != hipSuccess) return -1;
+  return hipEventCreate(&e1) == hipSuccess ? 0 : -1;
+}
+
+float ub_copy(void* s, void* d, uint64_t n16, uint32_t grid, int reps) {
+  Args a{s, d, n16};
+  a.grid = grid;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(copy16, dim3(q->grid), dim3(B), 0, 0, (const uint4*)q->a, (uint4*)q->b, q->n);
+  }, &a, reps);
+}
+
+float ub_read(void* s, void* d, uint64_t n16, uint32_t grid, int reps) {
+  Args a{s, d, n16};
+  a.grid = grid;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(read16, dim3(q->grid), dim3(B), 0, 0, (const uint4*)q->a, (uint32_t*)q->b, q->n);
+  }, &a, reps);
+}
+
+float ub_write(void* d, uint64_t n16, uint32_t grid, int reps) {
+  Args a{nullptr, d, n16};
+  a.grid = grid;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(write16, dim3(q->grid), dim3(B), 0, 0, (uint4*)q->b, q->n);
+  }, &a, reps);
+}
+
+float ub_pattern8(void* in, void* out, uint64_t obj, uint64_t shard, uint64_t oobj, uint64_t oshard, uint64_t ncols,
+                  uint32_t nobj, uint32_t rows, uint32_t gx, int reps) {
+  Args a{in, out, 0, obj, shard, oobj, oshard, ncols};
+  a.nobj = nobj;
+  a.rows = rows;
+  a.grid = gx;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(pattern<8>, dim3(q->grid, q->nobj), dim3(B), 0, 0, (const uint32_t*)q->a, (uint32_t*)q->b,
+                       q->obj, q->shard, q->oobj, q->oshard, q->ncols, q->rows);
+  }, &a, reps);
+}
+
+float ub_compute8(const uint32_t* coeff, void* sink, uint64_t iters, uint32_t rows, uint32_t grid, int reps) {
+  Args a{nullptr, sink};
+  a.iters = iters;
+  a.rows = rows;
+  a.grid = grid;
+  a.coeff = coeff;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(compute<8>, dim3(q->grid), dim3(B), 0, 0, q->coeff, (uint32_t*)q->b, q->iters, q->rows);
+  }, &a, reps);
+}
+
+float ub_mad(void* sink, uint64_t iters, uint32_t grid, int reps) {
+  Args a{nullptr, sink};
+  a.iters = iters;
+  a.grid = grid;
+  return time_ms([](void* p) {
+    Args* q = (Args*)p;
+    hipLaunchKernelGGL(mad, dim3(q->grid), dim3(B), 0, 0, (uint32_t*)q->b, 0x9E3779B9u, q->iters);
+  }, &a, reps);
+}
+}
