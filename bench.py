@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (must precede slime_amd: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
+from slime_amd import batch  # noqa: E402
 from slime_amd import device as D  # noqa: E402
 
 GIB = 1 << 30
@@ -48,18 +49,24 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--need", type=int, default=8)
     ap.add_argument("--total", type=int, default=12)
-    ap.add_argument("--objects", type=int, default=128, help="objects per GPU (C3/C4: 128)")
+    ap.add_argument("--objects", type=int, default=128, help="objects per GPU (C3/C4: 128; weak scaling)")
+    ap.add_argument("--global-objects", type=int, default=0,
+                    help="partition this many objects across ranks instead (strong scaling, e.g. C5: 64)")
     ap.add_argument("--object-mib", type=int, default=256, help="object size in MiB (C3/C4: 256)")
     ap.add_argument("--erase", type=str, default="0,1,2,3", help="erased shards for the decode leg")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle CPU path on rank 0 at N=1")
-    ap.add_argument("--cpu-sample-mib", type=int, default=32, help="object size of the CPU sample")
+    ap.add_argument("--cpu-sample-mib", type=int, default=64, help="object size of the CPU sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall time budget of the CPU sample")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
     return ap.parse_args()
 
 
-def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int) -> dict:
-    """Reference algorithm (oracle C port, %p twice per term, r passes) on host cores."""
+def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, seconds: float) -> dict:
+    """The reference's algorithm on host cores: the oracle's faithful C restatement
+    (uint64 products, `%`p twice per term, r CreateParity passes per object,
+    RecoverData recomputing all need rows), one object per thread as the
+    reference runs it, repeated until ~`seconds` of wall time have elapsed."""
     import threading
 
     import numpy as np
@@ -71,24 +78,30 @@ def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int) -> di
     rng = np.random.default_rng(0x5113E)
     objs = [rng.integers(0, 4294967291, size=(total, L), dtype=np.uint64).astype(np.uint32) for _ in range(threads)]
     have = [i for i in range(total) if i not in erase][:need]
+    reps = [0] * threads
+    deadline = time.perf_counter() + seconds
 
-    def work(o):
-        OC.encode_object(o, need, total)
-        chunks = [o[i] for i in have]
-        rc, _ = OC.recover_data(chunks, have)  # RecoverData recomputes all need rows (vector.go:80-85)
-        assert rc == 0
+    def work(t, o):
+        while True:
+            OC.encode_object(o, need, total)
+            rc, _ = OC.recover_data([o[i] for i in have], have)  # vector.go:80-85: all need rows
+            assert rc == 0
+            reps[t] += 1
+            if time.perf_counter() >= deadline:
+                return
 
     t0 = time.perf_counter()
-    ts = [threading.Thread(target=work, args=(o,)) for o in objs]
+    ts = [threading.Thread(target=work, args=(i, o)) for i, o in enumerate(objs)]
     for t in ts:
         t.start()
     for t in ts:
         t.join()
     dt = time.perf_counter() - t0
-    nbytes = 2 * threads * need * L * 4  # encode + decode of each object
+    nbytes = 2 * sum(reps) * need * L * 4  # encode + decode of each object pass
     return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} objects x {sample_mib} MiB, need={need} total={total}: encode (r CreateParity "
-                      f"passes) + RecoverData(erase {erase}), one object per thread; {dt:.1f} s",
+            "sample": f"{threads} threads x {sample_mib} MiB objects, need={need} total={total}: encode (r "
+                      f"CreateParity passes, multi_store.go:528-531) + RecoverData(erase {erase}); {sum(reps)} "
+                      f"object passes in {dt:.1f} s (oracle/rs_oracle.c, gcc -O2)",
             "seconds": round(dt, 2)}
 
 
@@ -110,7 +123,11 @@ def main():
     have = [i for i in range(total) if i not in erase][:need]
     S = args.object_mib << 20
     L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) symbols (multi_store.go:272)
-    nobj = args.objects
+    if args.global_objects:
+        _, nobj = batch.partition(args.global_objects, world, rank)
+        total_objs, scaling = args.global_objects, "strong"
+    else:
+        nobj, total_objs, scaling = args.objects, args.objects * world, "weak"
     lay = D.layout_of(total, L)
 
     buf = torch.empty(nobj * total * L, dtype=torch.int32, device=f"cuda:{dev}")
@@ -137,15 +154,13 @@ def main():
     torch.cuda.synchronize()
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    batch.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    batch.barrier()
     elapsed = time.perf_counter() - t0
 
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
@@ -156,13 +171,10 @@ def main():
     ok = bool(torch.equal(rec.view(nobj, len(erase), L)[:, [i for i, t in enumerate(erase) if t < need]],
                           v[:, [t for t in erase if t < need]]))
 
-    t = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, enc_ms_max, dec_ms_max, bad = t.tolist()
+    elapsed, enc_ms_max, dec_ms_max, bad = batch.max_over_ranks([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0])
 
     obj_bytes = nobj * S
-    total_bytes = 2 * obj_bytes * world * args.steps
+    total_bytes = 2 * total_objs * S * args.steps
     value = total_bytes / GIB / elapsed
     # Algorithmic HBM bytes per launch: encode 4L(k + r),
     # decode 4L(k + e) per object.
@@ -189,7 +201,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (splitmix64 symbols in [0,p), seeded per rank; MapToGF domain)",
@@ -217,7 +229,7 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib)
+            line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

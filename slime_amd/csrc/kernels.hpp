@@ -25,7 +25,7 @@ struct ApplyLaunch {
   uint32_t nobj;
   uint32_t rows;
   uint32_t k;
-  bool vec_ok;              // every base/stride/offset is 16-byte aligned
+  bool vec_ok;              // 16-byte units per lane (needs 4-byte aligned bases; see rs_capi.cpp)
 };
 
 // Row stride (words) of a device coefficient table: padded to 16 words for the

@@ -27,10 +27,17 @@ namespace {
 using apply::kBlock;
 using apply::rs_apply_kernel;
 
-// Product variant of the vectorised kernel (tuning table).
-constexpr int kUnroll = 1;
+// Product variant of the vectorised kernel (tools/apply_variants.py sweep,
+// DESIGN.md "Tuning"): each wave streams U KiB of every shard per step with
+// non-temporal loads and stores (read-once/write-once streams).  U = 4 up to
+// k = 10 (<= 192 VGPRs, 2 waves/SIMD at the 512-block grid), U = 2 beyond so
+// the k x U x 16 B of symbols stay in registers without dropping below that.
+template <int K>
+constexpr int unroll_for() {
+  return K <= 10 ? 4 : 2;
+}
 constexpr bool kNtLoads = true;
-constexpr bool kNtStores = false;
+constexpr bool kNtStores = true;
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
@@ -45,13 +52,14 @@ struct Geometry {
   uint64_t target, inflight;
 };
 const Geometry& geometry() {
-  static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 1024), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
+  static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 512), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
   return g;
 }
 
 template <int K, bool VEC>
 hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
-  const uint64_t per_block = VEC && K > 0 ? 4ull * kBlock * kUnroll : (uint64_t)kBlock;
+  constexpr int U = unroll_for<K>();
+  const uint64_t per_block = VEC && K > 0 ? 4ull * kBlock * U : (uint64_t)kBlock;
   const Geometry& geo = geometry();
   uint64_t gy = a.nobj < geo.inflight ? a.nobj : geo.inflight;
   if (gy > 65535) gy = 65535;
@@ -59,7 +67,7 @@ hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t need = (a.ncols + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((rs_apply_kernel<K, VEC, kUnroll, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
+  hipLaunchKernelGGL((rs_apply_kernel<K, VEC, U, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
                      dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
                      a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k);
   return hipGetLastError();

@@ -125,7 +125,7 @@ void destroy_plan(slime_rs_plan* plan) {
   delete plan;
 }
 
-bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
 
 int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, uint64_t src_shard, uint32_t* dst,
             uint64_t dst_obj, uint64_t dst_shard, uint64_t L, uint64_t nobj, hipStream_t stream) {
@@ -144,7 +144,13 @@ int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, ui
   a.nobj = (uint32_t)nobj;
   a.rows = plan->rows;
   a.k = plan->k;
-  a.vec_ok = aligned16(src) && aligned16(dst) && ((src_obj | src_shard | dst_obj | dst_shard) & 3u) == 0;
+  // The 16-byte-per-lane kernel needs only 4-byte alignment: gfx9+ runs with
+  // unaligned memory access enabled (SH_MEM_CONFIG alignment_mode =
+  // UNALIGNED), so dwordx4 loads/stores of shards whose stride is not a
+  // multiple of 4 symbols (e.g. 10/14 on 1 GiB objects: L = 26843546) stay
+  // vectorised.  16-byte aligned layouts are faster; pad strides where the
+  // layout is yours to choose.
+  a.vec_ok = aligned4(src) && aligned4(dst);
   DeviceScope ds(plan->device);
   HIP_TRY(launch_apply(a, stream));
   return 0;

@@ -1,0 +1,69 @@
+"""Multi-rank control plane on the CPU (gloo, world size 2).
+
+The data path shards objects across GPUs with no collective; what must be
+right for N > 1 is the partition (every object exactly once) and the
+max-over-ranks timing reduction bench.py reports.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from slime_amd import batch
+
+
+def test_partition_tiles_every_object_once():
+    for nobj in (0, 1, 7, 8, 63, 64, 65, 128, 1000):
+        for world in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(world):
+                s, c = batch.partition(nobj, world, r)
+                seen.extend(range(s, s + c))
+            assert seen == list(range(nobj))
+    assert batch.partition(64, 8, 3) == (24, 8)  # C5: 8 objects per GPU
+
+
+def test_partition_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        batch.partition(10, 2, 2)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        start, count = batch.partition(64, world, rank)
+        batch.barrier()
+        # rank r "took" 1+r seconds and processed `count` objects
+        elapsed, objs = batch.max_over_ranks([1.0 + rank, float(count)])
+        t = torch.tensor([float(count)], dtype=torch.float64)
+        dist.all_reduce(t)
+        q.put((rank, start, count, elapsed, objs, t.item()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_partition_and_max_timing():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 32), (32, 32)]
+    assert all(r[3] == 2.0 for r in res)  # max over ranks
+    assert all(r[5] == 64.0 for r in res)  # every object once

@@ -38,6 +38,9 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
     V(5, 2, false, false)
     V(6, 2, true, true)
     V(7, 2, false, true)
+    V(8, 4, true, true)
+    V(9, 4, true, false)
+    V(10, 3, true, true)
     default:
       return -1;
   }

@@ -26,8 +26,8 @@ import torch  # noqa: E402
 
 from slime_amd import device as D  # noqa: E402
 
-VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain", 6: "U2 ntL ntS",
-            7: "U2 ntS"}
+ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain",
+                6: "U2 ntL ntS", 7: "U2 ntS", 8: "U4 ntL ntS", 9: "U4 ntL", 10: "U3 ntL ntS"}
 
 
 def main():
@@ -37,7 +37,12 @@ def main():
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--nobj", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", type=str, default="0,2,4,6,8,9,10")
+    ap.add_argument("--blocks", type=str, default="256,384,512,768,1024")
+    ap.add_argument("--inflight", type=str, default="0", help="objects in flight (0 = all)")
+    ap.add_argument("--decode", type=int, default=0, help="time reconstruct of data 0..e-1 instead of encode")
     args = ap.parse_args()
+    VARIANTS = {int(v): ALL_VARIANTS[int(v)] for v in args.variants.split(",")}
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
     lib.av_launch.restype = ctypes.c_int
     lib.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
@@ -55,18 +60,31 @@ def main():
     ref = buf.view(nobj, total, L)[:, need:, :].clone()
 
     coeff = np.zeros((r, 16), dtype=np.uint32)
-    coeff[:, :need] = enc.coefficients()
-    c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
-    ii = torch.arange(need, dtype=torch.int32, device="cuda")
-    oi = torch.arange(need, total, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
+    if args.decode:
+        # Rebuild data shards 0..r-1 from shards r..total-1 into a separate buffer.
+        have = list(range(r, total))
+        dec = D.Plan.reconstruct(need, total, have, list(range(r)))
+        coeff[:, :need] = dec.coefficients()
+        ii = torch.tensor(have, dtype=torch.int32, device="cuda")
+        oi = torch.arange(r, dtype=torch.int32, device="cuda")
+        dst = torch.empty(nobj * r * L, dtype=torch.int32, device="cuda")
+        ref = buf.view(nobj, total, L)[:, :r, :].clone()
+        d_ptr, oo, view = dst.data_ptr(), r * L, lambda: dst.view(nobj, r, L)
+    else:
+        coeff[:, :need] = enc.coefficients()
+        ii = torch.arange(need, dtype=torch.int32, device="cuda")
+        oi = torch.arange(need, total, dtype=torch.int32, device="cuda")
+        d_ptr, oo, view = buf.data_ptr(), total * L, lambda: buf.view(nobj, total, L)[:, need:, :]
+    c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
     def launch(v, gx, gy):
-        rc = lib.av_launch(v, need, buf.data_ptr(), buf.data_ptr(), total * L, L, total * L, L, c_t.data_ptr(),
+        rc = lib.av_launch(v, need, buf.data_ptr(), d_ptr, total * L, L, oo, L, c_t.data_ptr(),
                            ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
 
-    geos = [(t, y) for t, y in itertools.product((512, 1024, 2048), (nobj, 32, 8, 2)) if y <= nobj]
+    ys = [nobj if int(y) == 0 else int(y) for y in args.inflight.split(",")]
+    geos = [(int(t), y) for t, y in itertools.product(args.blocks.split(","), ys) if y <= nobj]
     times = {(v, g): [] for v in VARIANTS for g in geos}
     for _ in range(args.rounds):
         for v in VARIANTS:
@@ -81,10 +99,10 @@ def main():
     # correctness of every variant (last geometry run of each)
     bad = []
     for v in VARIANTS:
-        buf.view(nobj, total, L)[:, need:, :].zero_()
+        view().zero_()
         launch(v, 4, 8)
         torch.cuda.synchronize()
-        if not torch.equal(buf.view(nobj, total, L)[:, need:, :], ref):
+        if not torch.equal(view(), ref):
             bad.append(v)
     alg = nobj * 4 * L * total
     rows = []
@@ -93,7 +111,8 @@ def main():
         rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "ms": round(med, 3),
                      "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: -x["GBps"])
-    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj}", "bad_variants": bad, "top": rows[:12],
+    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj}", "decode": bool(args.decode),
+                      "bad_variants": bad, "top": rows[:12],
                       "all": rows}, indent=1))
 
 

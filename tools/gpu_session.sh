@@ -41,6 +41,13 @@ has prof && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o benc
   python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0
 has ubench && run ubench 600 python tools/ubench.py
 has variants && run variants 600 python tools/apply_variants.py
+if has variants2; then
+  run var_enc 300 python tools/apply_variants.py
+  run var_dec 300 python tools/apply_variants.py --decode 1
+  run var_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16
+  run var_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --decode 1
+  run var_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --blocks 256,512,1024,2048
+fi
 if has grid; then
   for g in 1024 4096 8192; do
     run bench_grid$g 300 env SLIME_RS_GRID_TARGET=$g python bench.py --steps 5 --cpu-baseline 0
