@@ -142,6 +142,10 @@ int slime_rs_plan_matrix(int device, const uint32_t *coeff, int rows, int k, con
  * null stream).  Asynchronous; capturable into a hipGraph. */
 int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t *src, slime_rs_layout_t src_layout, uint32_t *dst,
                           slime_rs_layout_t dst_layout, uint64_t L, uint64_t nobj, void *stream);
+/* Write output row i to dst shard out_shards[i] instead of shard i (e.g. a
+ * repair that writes rebuilt shards back into their erased slots of the
+ * source layout, which is also the faster placement on MI355X: DESIGN.md). */
+int slime_rs_plan_set_outputs(slime_rs_plan_t plan, const int *out_shards);
 /* Shape of a plan: rows written and inputs read per column. */
 int slime_rs_plan_shape(slime_rs_plan_t plan, int *rows, int *k);
 /* Host copy of the plan's coefficient rows (rows x k, row-major). */

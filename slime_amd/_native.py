@@ -71,6 +71,7 @@ SIGNATURES = [
     ("slime_rs_plan_execute", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, Layout, ctypes.c_void_p, Layout, ctypes.c_uint64, ctypes.c_uint64,
       ctypes.c_void_p]),
+    ("slime_rs_plan_set_outputs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_plan_shape", ctypes.c_int, [ctypes.c_void_p, c_intp, c_intp]),
     ("slime_rs_plan_coefficients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_plan_destroy", ctypes.c_int, [ctypes.c_void_p]),

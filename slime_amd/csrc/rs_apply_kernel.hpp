@@ -89,7 +89,12 @@ __device__ __forceinline__ void row4(const uint4 (&x)[K], const u32x16& c, uint3
 // and the wave streams U KiB contiguous per shard.  K == 0: generic k.
 // Objects: blockIdx.y strides over objects, so gridDim.y bounds how many
 // objects (x shards) are streamed concurrently.
-template <int K, bool VEC, int U, bool NTL, bool NTS>
+//
+// ROT: each object walks its column tiles starting at a per-object rotation
+// (a bijection of [0, ntiles)), so the ~k x objects-in-flight concurrent
+// streams, whose shard bases share their low address bits when shards are
+// large powers of two, do not all hit the same DRAM channels/banks in step.
+template <int K, bool VEC, int U, bool NTL, bool NTS, bool ROT = false>
 __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
@@ -110,7 +115,10 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
       const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
       const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
       const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
-      for (uint64_t t = wave; t < ntiles; t += nwaves) {
+      const uint64_t rot = ROT && ntiles ? ((uint64_t)obj * 0x9E3779B97F4A7C15ull >> 20) % ntiles : 0;
+      for (uint64_t step = wave; step < ntiles; step += nwaves) {
+        uint64_t t = step + rot;
+        if (t >= ntiles) t -= ntiles;
         const uint64_t g0 = t * (64 * U) + lane;
         uint4 x[U][K];
 #pragma unroll

@@ -27,6 +27,7 @@
 struct slime_rs_plan {
   int device = 0;
   uint32_t rows = 0, k = 0;
+  uint32_t out_max = 0;         // highest destination shard index
   std::vector<uint32_t> coeff;  // rows x k, host copy
   uint32_t* table = nullptr;    // device: coeff (rows x coeff_stride(k)) | in_idx (k) | out_idx (rows)
   const uint32_t* d_coeff = nullptr;
@@ -93,6 +94,7 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   plan->rows = rows;
   plan->k = k;
   plan->coeff.assign(coeff, coeff + (size_t)rows * k);
+  plan->out_max = out_idx.empty() ? 0 : *std::max_element(out_idx.begin(), out_idx.end());
   const uint32_t cs = coeff_stride(k);
   const size_t ncoef = (size_t)rows * cs;
   const size_t n_in = (k + 3) & ~3u, n_out = (rows + 3) & ~3u;
@@ -396,6 +398,20 @@ int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t* src, slime_rs_la
   if (!src || !dst) return fail(Status::InvalidArg, "plan_execute: null buffer");
   return execute(plan, src, src_layout.obj_stride, src_layout.shard_stride, dst, dst_layout.obj_stride,
                  dst_layout.shard_stride, L, nobj, (hipStream_t)stream);
+}
+
+int slime_rs_plan_set_outputs(slime_rs_plan_t plan, const int* out_shards) {
+  if (!plan || !out_shards) return fail(Status::InvalidArg, "plan_set_outputs: bad args");
+  std::vector<uint32_t> idx(plan->rows);
+  for (uint32_t i = 0; i < plan->rows; ++i) {
+    if (out_shards[i] < 0) return fail(Status::InvalidArg, "plan_set_outputs: negative shard index");
+    idx[i] = (uint32_t)out_shards[i];
+  }
+  DeviceScope ds(plan->device);
+  HIP_TRY(hipMemcpy(const_cast<uint32_t*>(plan->d_out_idx), idx.data(), idx.size() * sizeof(uint32_t),
+                    hipMemcpyHostToDevice));
+  plan->out_max = *std::max_element(idx.begin(), idx.end());
+  return 0;
 }
 
 int slime_rs_plan_shape(slime_rs_plan_t plan, int* rows, int* k) {

@@ -42,6 +42,7 @@ class Plan:
         self._h = handle
         self.device = device
         self.in_max = in_max  # highest source shard index a launch reads
+        self.out_max = None   # highest destination shard index (None: rows - 1)
         rows, k = ctypes.c_int(), ctypes.c_int()
         N.check(lib.slime_rs_plan_shape(self._h, ctypes.byref(rows), ctypes.byref(k)))
         self.rows, self.k = rows.value, k.value
@@ -68,6 +69,15 @@ class Plan:
         N.check(lib.slime_rs_plan_matrix(device, c.ctypes.data, c.shape[0], c.shape[1], sv, ctypes.byref(h)))
         return cls(h, device, max(in_shards))
 
+    def set_outputs(self, out_shards: Sequence[int]) -> "Plan":
+        """Write output row i to destination shard out_shards[i] (e.g. repair in place)."""
+        if len(out_shards) != self.rows:
+            raise ValueError("need one destination shard per output row")
+        sv = (ctypes.c_int * len(out_shards))(*out_shards)
+        N.check(lib.slime_rs_plan_set_outputs(self._h, sv))
+        self.out_max = max(out_shards)
+        return self
+
     def coefficients(self) -> np.ndarray:
         out = np.zeros((self.rows, self.k), dtype=np.uint32)
         N.check(lib.slime_rs_plan_coefficients(self._h, out.ctypes.data))
@@ -83,7 +93,8 @@ class Plan:
             if _dev_index(t) != self.device:
                 raise ValueError("tensor is not on the plan's device")
         self._check_extent(src, src_offset, src_layout, L, nobj, self.in_max)
-        self._check_extent(dst, dst_offset, dst_layout, L, nobj, self.rows - 1)
+        self._check_extent(dst, dst_offset, dst_layout, L, nobj,
+                           self.rows - 1 if self.out_max is None else self.out_max)
         N.check(lib.slime_rs_plan_execute(self._h, ctypes.c_void_p(src.data_ptr() + 4 * src_offset), src_layout,
                                           ctypes.c_void_p(dst.data_ptr() + 4 * dst_offset), dst_layout, L, nobj,
                                           _stream_handle(self.device, stream)))

@@ -221,6 +221,26 @@ def test_plan_reconstruct_every_pattern(torch_dev, need, total):
                 assert np.array_equal(got[o, w_i], h[o, t]), (have, t)
 
 
+def test_plan_reconstruct_in_place_repair(torch_dev):
+    """Rebuilt shards written back into their erased slots (slime_rs_plan_set_outputs)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, L, nobj = 8, 12, 5003, 3
+    buf = _objects(torch, nobj, total, L, seed=77)
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    truth = buf.clone()
+    for erase in ([0, 1, 2, 3], [0, 3, 8, 11], [11], [2, 9]):
+        have = [i for i in range(total) if i not in erase][:need]
+        v = buf.view(nobj, total, L)
+        v[:, erase, :] = -1  # destroy the erased shards
+        plan = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+        plan(buf, lay, buf, lay, L, nobj)
+        torch.cuda.synchronize()
+        assert torch.equal(buf, truth), erase
+
+
 def test_plan_matrix_unaligned_layouts_and_noncanonical(torch_dev):
     torch = torch_dev
     from slime_amd import device as D

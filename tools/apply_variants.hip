@@ -9,11 +9,11 @@
 using namespace slime::apply;
 
 namespace {
-template <int K, int U, bool NTL, bool NTS>
+template <int K, int U, bool NTL, bool NTS, bool ROT = false>
 void go(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os, const uint32_t* coeff,
         const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy,
         hipStream_t s) {
-  hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
+  hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS, ROT>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
                      os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K);
 }
 }  // namespace
@@ -22,13 +22,14 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
                          uint64_t oo, uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
                          uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-#define V(id, U, NTL, NTS)                                                                           \
-  case id:                                                                                          \
-    if (k == 8) go<8, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);   \
-    else if (k == 10) go<10, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s); \
-    else if (k == 4) go<4, U, NTL, NTS>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);  \
-    else return -2;                                                                                 \
+#define V2(id, U, NTL, NTS, ROT)                                                                            \
+  case id:                                                                                                 \
+    if (k == 8) go<8, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);     \
+    else if (k == 10) go<10, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s); \
+    else if (k == 4) go<4, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);   \
+    else return -2;                                                                                        \
     break;
+#define V(id, U, NTL, NTS) V2(id, U, NTL, NTS, false)
   switch (variant) {
     V(0, 1, true, false)
     V(1, 1, false, false)
@@ -41,9 +42,12 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
     V(8, 4, true, true)
     V(9, 4, true, false)
     V(10, 3, true, true)
+    V2(11, 4, true, true, true)
+    V2(12, 2, true, true, true)
     default:
       return -1;
   }
 #undef V
+#undef V2
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -27,7 +27,8 @@ import torch  # noqa: E402
 from slime_amd import device as D  # noqa: E402
 
 ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain",
-                6: "U2 ntL ntS", 7: "U2 ntS", 8: "U4 ntL ntS", 9: "U4 ntL", 10: "U3 ntL ntS"}
+                6: "U2 ntL ntS", 7: "U2 ntS", 8: "U4 ntL ntS", 9: "U4 ntL", 10: "U3 ntL ntS",
+                11: "U4 ntL ntS rot", 12: "U2 ntL ntS rot"}
 
 
 def main():
@@ -41,6 +42,9 @@ def main():
     ap.add_argument("--blocks", type=str, default="256,384,512,768,1024")
     ap.add_argument("--inflight", type=str, default="0", help="objects in flight (0 = all)")
     ap.add_argument("--decode", type=int, default=0, help="time reconstruct of data 0..e-1 instead of encode")
+    ap.add_argument("--pad", type=int, default=0, help="shard stride = L + pad symbols")
+    ap.add_argument("--separate", type=int, default=-1,
+                    help="1: write to a separate buffer, 0: in place (default: encode in place, decode separate)")
     args = ap.parse_args()
     VARIANTS = {int(v): ALL_VARIANTS[int(v)] for v in args.variants.split(",")}
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
@@ -51,35 +55,46 @@ def main():
     need, total, nobj = args.need, args.total, args.nobj
     r = total - need
     L = (args.mib << 20) // 4 // need
-    buf = torch.empty(nobj * total * L, dtype=torch.int32, device="cuda")
+    SS = L + args.pad  # shard stride
+    tail = nobj * r * SS if args.separate == 2 else 0  # 2: destination in the same allocation, after the objects
+    whole = torch.empty(nobj * total * SS + tail, dtype=torch.int32, device="cuda")
+    buf = whole[: nobj * total * SS]
     D.fill_symbols(buf, 7)
-    lay = D.layout_of(total, L)
+    lay = D.layout_of(total, L, SS)
     enc = D.Plan.encode(need, total)
-    enc(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    enc(buf, lay, buf, lay, L, nobj, dst_offset=need * SS)
     torch.cuda.synchronize()
-    ref = buf.view(nobj, total, L)[:, need:, :].clone()
+    shards = lambda: buf.view(nobj, total, SS)[:, :, :L]  # noqa: E731
+    ref = shards()[:, need:, :].clone()
 
     coeff = np.zeros((r, 16), dtype=np.uint32)
     s = torch.cuda.current_stream()
+    separate = args.separate if args.separate >= 0 else int(bool(args.decode))
     if args.decode:
-        # Rebuild data shards 0..r-1 from shards r..total-1 into a separate buffer.
+        # Rebuild data shards 0..r-1 from shards r..total-1.
         have = list(range(r, total))
         dec = D.Plan.reconstruct(need, total, have, list(range(r)))
         coeff[:, :need] = dec.coefficients()
         ii = torch.tensor(have, dtype=torch.int32, device="cuda")
-        oi = torch.arange(r, dtype=torch.int32, device="cuda")
-        dst = torch.empty(nobj * r * L, dtype=torch.int32, device="cuda")
-        ref = buf.view(nobj, total, L)[:, :r, :].clone()
-        d_ptr, oo, view = dst.data_ptr(), r * L, lambda: dst.view(nobj, r, L)
+        ref = shards()[:, :r, :].clone()
+        slot0 = 0
     else:
         coeff[:, :need] = enc.coefficients()
         ii = torch.arange(need, dtype=torch.int32, device="cuda")
-        oi = torch.arange(need, total, dtype=torch.int32, device="cuda")
-        d_ptr, oo, view = buf.data_ptr(), total * L, lambda: buf.view(nobj, total, L)[:, need:, :]
+        slot0 = need
+    if separate:
+        dst = whole[nobj * total * SS:] if args.separate == 2 else \
+            torch.empty(nobj * r * SS, dtype=torch.int32, device="cuda")
+        oi = torch.arange(r, dtype=torch.int32, device="cuda")
+        d_ptr, oo, view = dst.data_ptr(), r * SS, lambda: dst.view(nobj, r, SS)[:, :, :L]
+    else:
+        oi = torch.arange(slot0, slot0 + r, dtype=torch.int32, device="cuda")
+        d_ptr, oo = buf.data_ptr(), total * SS
+        view = lambda: shards()[:, slot0:slot0 + r, :]  # noqa: E731
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
     def launch(v, gx, gy):
-        rc = lib.av_launch(v, need, buf.data_ptr(), d_ptr, total * L, L, oo, L, c_t.data_ptr(),
+        rc = lib.av_launch(v, need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                            ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream))
         assert rc == 0, rc
 
@@ -111,7 +126,8 @@ def main():
         rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "ms": round(med, 3),
                      "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: -x["GBps"])
-    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj}", "decode": bool(args.decode),
+    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj} pad {args.pad}", "decode": bool(args.decode),
+                      "separate": int(args.separate if args.separate >= 0 else separate),
                       "bad_variants": bad, "top": rows[:12],
                       "all": rows}, indent=1))
 

@@ -41,6 +41,27 @@ has prof && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o benc
   python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0
 has ubench && run ubench 600 python tools/ubench.py
 has variants && run variants 600 python tools/apply_variants.py
+if has placement; then
+  for d in 0 1; do for sep in 0 1; do
+    run var_d${d}_s${sep} 300 python tools/apply_variants.py --decode $d --separate $sep --variants 8,6 --blocks 256,512,1024
+  done; done
+fi
+if has rot; then
+  for pad in 0 4160; do
+    run rot_enc_inpl_p$pad 300 python tools/apply_variants.py --separate 0 --pad $pad --variants 8,11,6,12 --blocks 256,512,1024
+    run rot_enc_sep_p$pad 300 python tools/apply_variants.py --separate 1 --pad $pad --variants 8,11,6,12 --blocks 256,512,1024
+    run rot_dec_sep_p$pad 300 python tools/apply_variants.py --decode 1 --separate 1 --pad $pad --variants 8,11,6,12 --blocks 256,512,1024
+  done
+  run rot_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --variants 8,11 --blocks 256,512,1024
+  run rot_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --decode 1 --variants 8,11 --blocks 256,512,1024
+fi
+if has sep; then
+  for r in 1 2; do
+  for sep in 0 1 2; do
+    run sep_enc_${sep}_r$r 300 python tools/apply_variants.py --separate $sep --variants 8 --blocks 256,512
+    run sep_dec_${sep}_r$r 300 python tools/apply_variants.py --decode 1 --separate $sep --variants 8 --blocks 256,512
+  done; done
+fi
 if has variants2; then
   run var_enc 300 python tools/apply_variants.py
   run var_dec 300 python tools/apply_variants.py --decode 1
