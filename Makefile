@@ -8,7 +8,7 @@ SRC      := slime_amd/csrc
 OBJ      := build/obj
 LIB      := slime_amd/lib/libslime_rs.so
 
-OBJS := $(OBJ)/rs_apply.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/rs_capi.o
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_bytes.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 all: $(LIB) oracle
@@ -46,3 +46,9 @@ applyvar: tools/libapplyvar.so
 tools/libapplyvar.so: tools/apply_variants.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: applyvar
+
+# Byte-domain kernel variant harness (tools only): make bytesvar
+bytesvar: tools/libbytesvar.so
+tools/libbytesvar.so: tools/bytes_variants.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: bytesvar

@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle CPU path on rank 0 at N=1")
     ap.add_argument("--cpu-sample-mib", type=int, default=64, help="object size of the CPU sample")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall time budget of the CPU sample")
+    ap.add_argument("--bytes-path", type=int, default=1,
+                    help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
     return ap.parse_args()
@@ -105,6 +107,74 @@ def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, secon
                       f"CreateParity passes, multi_store.go:528-531) + RecoverData(erase {erase}); {sum(reps)} "
                       f"object passes in {dt:.1f} s (oracle/rs_oracle.c, gcc -O2)",
             "seconds": round(dt, 2)}
+
+
+def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int) -> dict:
+    """writeChunks / reconstruct on device from object bytes (rs_bytes.hip): one
+    speculative encode pass that also picks gf.MapToGF's mapping, a re-encode
+    pass for objects mapped with 1<<31, and an in-place repair of the erased
+    chunks from chunk bytes.  Objects that would need MapToGF's random
+    fallback are re-drawn before timing and counted."""
+    S = args.object_mib << 20
+    L, chunk, slot = D.slot_geometry(S, need, total)
+    slots = torch.empty(nobj * slot, dtype=torch.uint8, device=f"cuda:{dev}")
+    words = slots.view(torch.int32)
+    D.fill_symbols(words, 0xB17E5 + 7919 * rank)
+    enc = D.Plan.encode(need, total, dev)
+    have = [i for i in range(total) if i not in erase][:need]
+    dec = D.Plan.reconstruct(need, total, have, erase, dev).set_outputs(erase)
+    mapping = torch.empty(nobj, dtype=torch.int32, device=f"cuda:{dev}")
+    status = torch.empty(nobj, dtype=torch.int32, device=f"cuda:{dev}")
+    stream = torch.cuda.current_stream(dev)
+    redraws = 0
+    for attempt in range(64):
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream)
+        bad = status.nonzero().flatten().tolist()
+        if not bad:
+            break
+        for o in bad:  # re-draw the object from another seed
+            D.fill_symbols(words[o * slot // 4:(o * slot + S) // 4], 0xB17E5 + (attempt + 1) * 2**32 + o)
+        redraws += len(bad)
+    truth = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)[:, erase, :].clone()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream)
+        if ev is not None:
+            ev[1].record(stream)
+        D.decode_objects(dec, slots, slot, L, nobj, mapping, stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    batch.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    batch.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    got = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)[:, erase, :]
+    ok = bool(torch.equal(got, truth)) and int(status.sum().item()) == 0
+    ms = mapping.cpu().numpy().view("uint32")
+    elapsed, = batch.max_over_ranks([elapsed])
+    del slots, words, truth
+    torch.cuda.empty_cache()
+    return {"value": round(2 * nobj * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
+            "encode_gibs": round(nobj * S / GIB / (enc_ms * 1e-3), 2),
+            "decode_gibs": round(nobj * S / GIB / (dec_ms * 1e-3), 2),
+            "kernel_ms": {"encode_both_passes": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+            "mappings": {"0": int((ms == 0).sum()), "1<<31": int((ms == 0x80000000).sum()),
+                         "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
+            "fallback_redraws": redraws, "verified": ok,
+            "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative mapping-0 pass + "
+                    "1<<31 re-encode pass) and repair of erased chunks from chunk bytes"}
 
 
 def main():
@@ -204,6 +274,12 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    bytes_path = None
+    if args.bytes_path:
+        del buf, rec  # rec aliases buf for in-place repair
+        torch.cuda.empty_cache()
+        bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj)
+
     if rank == 0:
         line = {
             "metric": "RS encode+decode GiB/s device-resident at need=8/total=12, 1/2/4/8 GPUs",
@@ -241,6 +317,7 @@ def main():
                 "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg},
             },
             "cpu_baseline": None,
+            "object_bytes_path": bytes_path,
         }
         if world == 1 and args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib, args.cpu_seconds)

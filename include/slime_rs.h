@@ -152,6 +152,34 @@ int slime_rs_plan_shape(slime_rs_plan_t plan, int *rows, int *k);
 int slime_rs_plan_coefficients(slime_rs_plan_t plan, uint32_t *out);
 int slime_rs_plan_destroy(slime_rs_plan_t plan);
 
+/* ==== fused byte-domain object pipeline (writeChunks / reconstruct on device) ====
+ * Object slots: object o's slot starts at slots + o*slot_stride bytes and holds
+ * its `total` chunks of 4L bytes (chunk c at slot + c*4L, L = ceil(ceil(S/4)/need),
+ * multi_store.go:272).  The object's S bytes are the first S bytes of its slot,
+ * so the data chunks are in place: after encoding, chunk c of the slot is
+ * exactly MapFromGF(mapping, part c) (multi_store.go:526-554).  need <= 16. */
+
+/* Encode nobj objects of S bytes: mapping[o] receives gf.MapToGF's choice
+ * (map.go:35-62) and status[o] = 1 marks an object that needs MapToGF's random
+ * fallback (map.go:64-66; its chunks are not final until
+ * slime_rs_resolve_fallbacks).  mapping/status are device arrays of nobj
+ * words.  Speculative single pass (mapping 0) plus a re-encode pass only for
+ * objects whose mapping is 1<<31.  Asynchronous. */
+int slime_rs_encode_objects(slime_rs_plan_t encode_plan, uint8_t *slots, uint64_t slot_stride, uint64_t object_size,
+                            uint64_t nobj, uint32_t *mapping, uint32_t *status, void *stream);
+/* Synchronous: for each object with status 1, draw random mapping candidates
+ * (64 per device pass) until one fits, store it in mapping[o], clear status[o]
+ * and re-encode the object.  *resolved (optional) = objects fixed. */
+int slime_rs_resolve_fallbacks(slime_rs_plan_t encode_plan, uint8_t *slots, uint64_t slot_stride,
+                               uint64_t object_size, uint64_t nobj, uint32_t *mapping, uint32_t *status, void *stream,
+                               int *resolved);
+/* Rebuild chunks from `need` surviving chunks of each slot: a reconstruct plan
+ * whose inputs are the survivors' chunk indices and whose outputs
+ * (slime_rs_plan_set_outputs) are the chunk slots to write.  mapping[o] is the
+ * object's mapping value (meta.File.MappingValue).  Asynchronous. */
+int slime_rs_decode_objects(slime_rs_plan_t reconstruct_plan, uint8_t *slots, uint64_t slot_stride, uint64_t L,
+                            uint64_t nobj, const uint32_t *mapping, void *stream);
+
 /* Device codec (internal/rs/gf/map.go) over device buffers, asynchronous on
  * `stream`.  pack: words[i] = BE(bytes[4i..4i+3]) ^ mapping (zero low bytes
  * in a partial last word); if flags != NULL it is OR-ed with bit0 = some

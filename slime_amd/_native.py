@@ -75,6 +75,15 @@ SIGNATURES = [
     ("slime_rs_plan_shape", ctypes.c_int, [ctypes.c_void_p, c_intp, c_intp]),
     ("slime_rs_plan_coefficients", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_plan_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("slime_rs_encode_objects", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_resolve_fallbacks", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_void_p, c_intp]),
+    ("slime_rs_decode_objects", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+      ctypes.c_void_p]),
     ("slime_gf_pack_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_gf_unpack_device", ctypes.c_int,

@@ -37,6 +37,29 @@ hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 // out[i] = in[i] mod p  (RecoverData's unit rows for surviving data shards).
 hipError_t launch_canon_copy(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t stream);
 
+// --- fused byte-domain encode/decode over object slots (rs_bytes.hip) --------
+// Slot o at slots + o*slot_stride bytes; chunk c at slot + c*4L.  coeff /
+// in_idx / out_idx are a plan's device tables.  Encode: phase 0 = speculative
+// (mapping 0, OR MapToGF flag bits into flags[obj]); select_mapping turns the
+// flags into mapping[] and a fallback status in place; phase 1 re-encodes the
+// objects with mapping != 0 and status == 0.  Decode uses mapping[obj].
+struct BytesLaunch {
+  uint8_t* slots;
+  uint64_t slot_stride;
+  uint64_t L;
+  uint64_t S;  // object size in bytes (encode)
+  uint32_t nobj, rows, k;
+  int phase;
+  const uint32_t* coeff;
+  const uint32_t* in_idx;
+  const uint32_t* out_idx;
+  uint32_t* flags;  // encode: the caller's status array (flags, then fallback status)
+  const uint32_t* mapping;
+};
+hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
+hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t stream);
+hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t stream);
+
 // --- byte <-> symbol codec (internal/rs/gf/map.go) -------------------------
 // Pack len bytes big-endian into ceil(len/4) words (zero low bytes in a partial
 // last word), XOR with `mapping`; words_out must hold ceil(len/4) words.

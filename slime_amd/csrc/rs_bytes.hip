@@ -1,0 +1,96 @@
+// Fused byte-domain encode/decode launchers (kernels: rs_bytes_kernel.hpp).
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+#include "rs_bytes_kernel.hpp"
+
+namespace slime {
+namespace {
+
+using apply::kBlock;
+using bytes::decode_bytes_kernel;
+using bytes::encode_bytes_kernel;
+using bytes::select_mapping_kernel;
+
+template <int K>
+constexpr int bytes_unroll() {
+  return K <= 8 ? 4 : (K <= 12 ? 2 : 1);
+}
+
+dim3 grid_for(uint64_t L, uint32_t objects_in_flight) {
+  uint64_t gy = objects_in_flight < 65535u ? objects_in_flight : 65535u;
+  if (gy < 1) gy = 1;
+  uint64_t gx = (512 + gy - 1) / gy;
+  const uint64_t need = (L + 4ull * kBlock - 1) / (4ull * kBlock);
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  return dim3((uint32_t)gx, (uint32_t)gy);
+}
+
+template <int K>
+hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
+  constexpr int U = bytes_unroll<K>();
+  // Phase 0 streams every object at once; phase 1 re-encodes the few objects
+  // MapToGF maps with 1<<31 (~7.5% of 256 MiB random objects), so the whole
+  // grid sweeps them one after another instead of 512/nobj blocks each.
+  const dim3 g = grid_for(a.L, a.phase == 0 ? a.nobj : 1);
+  if (a.phase == 0) {
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.S,
+                       a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+  } else {
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.S,
+                       a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
+  constexpr int U = bytes_unroll<K>();
+  hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(a.L, a.nobj), dim3(kBlock), 0, s, a.slots,
+                     a.slot_stride, a.L, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping);
+  return hipGetLastError();
+}
+
+#define SLIME_K_SWITCH(fn)                   \
+  switch (a.k) {                             \
+    case 1: return fn<1>(a, s);              \
+    case 2: return fn<2>(a, s);              \
+    case 3: return fn<3>(a, s);              \
+    case 4: return fn<4>(a, s);              \
+    case 5: return fn<5>(a, s);              \
+    case 6: return fn<6>(a, s);              \
+    case 7: return fn<7>(a, s);              \
+    case 8: return fn<8>(a, s);              \
+    case 9: return fn<9>(a, s);              \
+    case 10: return fn<10>(a, s);            \
+    case 11: return fn<11>(a, s);            \
+    case 12: return fn<12>(a, s);            \
+    case 13: return fn<13>(a, s);            \
+    case 14: return fn<14>(a, s);            \
+    case 15: return fn<15>(a, s);            \
+    case 16: return fn<16>(a, s);            \
+    default: return hipErrorInvalidValue;    \
+  }
+
+}  // namespace
+
+hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t s) {
+  if (a.nobj == 0 || a.L == 0) return hipSuccess;
+  SLIME_K_SWITCH(enc_k)
+}
+
+hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t s) {
+  if (a.nobj == 0 || a.L == 0 || a.rows == 0) return hipSuccess;
+  SLIME_K_SWITCH(dec_k)
+}
+
+hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t s) {
+  if (nobj == 0) return hipSuccess;
+  hipLaunchKernelGGL(select_mapping_kernel, dim3((nobj + 255) / 256), dim3(256), 0, s, mapping, status, nobj);
+  return hipGetLastError();
+}
+
+#undef SLIME_K_SWITCH
+
+}  // namespace slime

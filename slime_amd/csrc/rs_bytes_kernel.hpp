@@ -1,0 +1,333 @@
+// Fused byte-domain encode/decode kernels (device code) for CDNA4, shared by
+// rs_bytes.hip (product) and tools/bytes_variants.hip (tuning): slime's writeChunks and
+// reconstruct data paths (internal/store/multi/multi_store.go:516-557 and
+// :215-242) on device, without materialising the symbol domain.
+//
+// Object slot layout (bytes): slot o starts at base + o*slot_stride; chunk c
+// of object o is the 4L bytes at slot + c*4L, L = ceil(ceil(S/4)/need)
+// (splitVector, multi_store.go:272).  The object's S bytes occupy the start
+// of its slot, so data chunk j IS bytes [4jL, 4(j+1)L) of the slot once the
+// encoder has written the tail past S with what MapFromGF produces there.
+//
+// Encode (one object, mapping m chosen as gf.MapToGF does, map.go:15-67):
+//   word w < nw = ceil(S/4): packed = BE(bytes[4w..4w+3]) (a partial last
+//   word keeps its high bytes, low bytes zero, map.go:25-32); symbol =
+//   packed ^ m.  Words nw..kL-1 are splitVector's zero padding (symbol 0,
+//   NOT xor-ed).  Chunk word = BE(symbol ^ m) (MapFromGF, map.go:103-113):
+//   parity chunks from the code rows, data-chunk tail = BE(packed) for the
+//   partial word and BE(m) for padding words.
+//   Speculative: pass 0 assumes m = 0 and reduces the two MapToGF flag bits
+//   per object; a tiny kernel turns flags into m (0, 1<<31, or "fallback");
+//   pass 1 re-encodes only objects whose m != 0 (other blocks exit at once).
+// Decode: symbol = BE(chunk word) ^ m for the survivors, rebuilt chunk word =
+//   BE(symbol ^ m) (MapToGFWith + RecoverData + MapFromGF).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gfp.hpp"
+#include "rs_apply_kernel.hpp"
+
+namespace slime {
+namespace bytes {
+
+using apply::kBlock;
+using apply::kCoeffStride;
+using apply::kWaves;
+using apply::u32x16;
+using apply::u32x4;
+
+__device__ __forceinline__ uint32_t be(uint32_t w) { return __builtin_bswap32(w); }
+
+__device__ __forceinline__ uint32_t flag_bits(uint32_t w) {
+  return (w >= kP ? 1u : 0u) | ((w ^ 0x80000000u) >= kP ? 2u : 0u);
+}
+
+struct ObjWords {
+  uint64_t nw;        // ceil(S/4): words carrying object bytes
+  uint32_t tailmask;  // mask of the valid high bytes of word nw-1 (0xFFFFFFFF if S%4 == 0)
+};
+
+// Symbol-domain word w of an object from the slot bytes loaded as `raw`.
+// Returns the packed (pre-mapping) word; *pad says "splitVector padding".
+__device__ __forceinline__ uint32_t packed_word(uint32_t raw, uint64_t w, const ObjWords& ow, bool* pad) {
+  *pad = w >= ow.nw;
+  const uint32_t p = be(raw);
+  return *pad ? 0u : (w + 1 == ow.nw ? p & ow.tailmask : p);
+}
+
+template <int K>
+__device__ __forceinline__ void rows_out(const uint32_t (&x)[K][4], uint32_t rows, const uint32_t* __restrict__ coeff,
+                                         const uint32_t* __restrict__ out_idx, uint8_t* out_slot, uint64_t chunk,
+                                         uint64_t byte_off, uint32_t m, int ncol) {
+  for (uint32_t i = 0; i < rows; ++i) {
+    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
+    uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j][0], x[j][1], x[j][2], x[j][3], c[j]);
+    uint8_t* dst = out_slot + (uint64_t)out_idx[i] * chunk + byte_off;
+    if (ncol == 4) {
+      const u32x4 v = {be(fold96(lo0, hi0) ^ m), be(fold96(lo1, hi1) ^ m), be(fold96(lo2, hi2) ^ m),
+                       be(fold96(lo3, hi3) ^ m)};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+    } else {
+      reinterpret_cast<uint32_t*>(dst)[0] = be(fold96(lo0, hi0) ^ m);
+    }
+  }
+}
+
+// All output rows for U units of 4 columns: rows outer (one s_load_dwordx16
+// of coefficients per row), units inner, so the units' independent MAC chains
+// interleave.  valid_units: units [0, n) are inside the chunk.
+template <int K, int U>
+__device__ __forceinline__ void rows_out_units(const uint32_t (&x)[U][K][4], int n, uint32_t rows,
+                                               const uint32_t* __restrict__ coeff,
+                                               const uint32_t* __restrict__ out_idx, uint8_t* out_slot,
+                                               uint64_t chunk, uint64_t g0, uint32_t m) {
+  for (uint32_t i = 0; i < rows; ++i) {
+    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    uint8_t* const orow = out_slot + (uint64_t)out_idx[i] * chunk;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= n) break;
+      uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
+      uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[u][j][0], x[u][j][1], x[u][j][2], x[u][j][3], c[j]);
+      const u32x4 v = {be(fold96(lo0, hi0) ^ m), be(fold96(lo1, hi1) ^ m), be(fold96(lo2, hi2) ^ m),
+                       be(fold96(lo3, hi3) ^ m)};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(orow + (((g0 + 64 * u) << 2) << 2)));
+    }
+  }
+}
+
+// MapToGF's two flag bits (map.go:35-62) as running maxima:
+// bit0 <=> max(word) >= p, bit1 <=> max(word ^ 1<<31) >= p.  One accumulator
+// pair per column lane c keeps four independent max chains instead of one
+// serial chain through every word of a step.
+struct Flags {
+  uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  __device__ __forceinline__ void add(int c, uint32_t w) {
+    a[c] = a[c] > w ? a[c] : w;
+    const uint32_t h = w ^ 0x80000000u;
+    b[c] = b[c] > h ? b[c] : h;
+  }
+  __device__ __forceinline__ uint32_t bits() const {
+    uint32_t ma = 0, mb = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      ma = ma > a[c] ? ma : a[c];
+      mb = mb > b[c] ? mb : b[c];
+    }
+    return (ma >= kP ? 1u : 0u) | (mb >= kP ? 2u : 0u);
+  }
+};
+
+// Load the K data-chunk words of columns [b, b+ncol) as symbols (mapping m,
+// splitVector padding), folding the packed words into MapToGF's flags.
+// INTERIOR: every word of the unit is a full object word (the bulk of every
+// object) -- no padding/partial-word checks.
+template <int K, bool INTERIOR, bool FLAGS>
+__device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t b,
+                                                  int ncol, const ObjWords& ow, uint32_t m, uint32_t (&x)[K][4],
+                                                  Flags* fl) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint8_t* src = slot + (uint64_t)j * chunk + 4 * b;
+    uint32_t raw[4] = {0, 0, 0, 0};
+    if (ncol == 4) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+      raw[0] = v.x, raw[1] = v.y, raw[2] = v.z, raw[3] = v.w;
+    } else {
+      raw[0] = *reinterpret_cast<const uint32_t*>(src);
+    }
+    if constexpr (INTERIOR) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t p = be(raw[c]);
+        if (FLAGS) fl->add(c, p);
+        x[j][c] = p ^ m;
+      }
+    } else {
+      const uint64_t w0 = (uint64_t)j * L + b;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bool pad;
+        const uint32_t p = packed_word(raw[c], w0 + c, ow, &pad);
+        if (FLAGS && !pad && c < ncol) fl->add(c, p);
+        x[j][c] = pad ? 0u : p ^ m;
+      }
+    }
+  }
+}
+
+// Data-chunk bytes from the last object word on (only units that reach it):
+// BE(packed) for the partial word, BE(m) for splitVector padding words.
+template <int K>
+__device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t b, int ncol,
+                                              const ObjWords& ow, uint32_t m, const uint32_t (&x)[K][4]) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint64_t w0 = (uint64_t)j * L + b;
+    if (w0 + ncol < ow.nw) continue;
+    uint32_t fix[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fix[c] = be(w0 + c >= ow.nw ? m : x[j][c] ^ m);
+    uint8_t* d = slot + (uint64_t)j * chunk + 4 * b;
+    if (ncol == 4) {
+      const u32x4 v = {fix[0], fix[1], fix[2], fix[3]};
+      *reinterpret_cast<u32x4*>(d) = v;
+    } else {
+      *reinterpret_cast<uint32_t*>(d) = fix[0];
+    }
+  }
+}
+
+// MODE 0: speculative encode with m = 0, OR-ing MapToGF's flag bits into
+//         flags[obj] (the caller's status array, zeroed first).
+// MODE 1: re-encode objects with mapping[obj] != 0 and status[obj] == 0.
+// Lanes own 4 columns (16 B per chunk) per unit; a wave issues the loads of
+// U units (U KiB of every data chunk) before any math or store; columns past
+// the last multiple of 4 go one per lane.
+template <int K, int U, int MODE, bool FAST = true, bool FLAGS_ON = true>
+__global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows,
+    const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ mapping) {
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t nvec = L >> 2;
+  const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  // Units whose columns reach the object's last word (or padding) need the
+  // data-chunk tail fix; every other unit skips that branch.
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+    uint32_t m = 0;
+    if constexpr (MODE == 1) {
+      m = mapping[obj];
+      if (m == 0 || flags[obj] != 0) continue;  // nothing to redo / random fallback pending (uniform per block)
+    }
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride;
+    uint8_t* const par = slot + (uint64_t)K * chunk;  // parity chunk i at par + out_idx[i]*chunk
+    constexpr bool F = MODE == 0 && FLAGS_ON;
+    Flags fl;
+    for (uint64_t step = wave; step < ntiles; step += nwaves) {
+      const uint64_t g0 = step * (64 * U) + lane;
+      // Interior step: the highest word the wave's units touch (last data
+      // chunk, last unit) is below the object's last word: no checks needed.
+      const uint64_t top = (uint64_t)(K - 1) * L + ((step * (64 * U) + 64 * U) << 2);
+      uint32_t x[U][K][4];
+      if (FAST && top < first_tail_word && (step + 1) * (64 * U) <= nvec) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          load_data_symbols<K, true, F>(slot, chunk, L, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
+        rows_out_units<K, U>(x, U, rows, coeff, out_idx, par, chunk, g0, m);
+        continue;
+      }
+      // Edge step: units past the chunk end are skipped; units reaching the
+      // object's last word also rewrite the data-chunk tail.  Units inside
+      // the chunk always form a prefix [0, n) of the step's units.
+      int n = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (g0 + 64 * u < nvec) {
+          load_data_symbols<K, false, F>(slot, chunk, L, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
+          n = u + 1;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u >= n) break;
+        const uint64_t b = (g0 + 64 * u) << 2;
+        if ((uint64_t)(K - 1) * L + b + 4 > first_tail_word) fix_data_tail<K>(slot, chunk, L, b, 4, ow, m, x[u]);
+      }
+      rows_out_units<K, U>(x, n, rows, coeff, out_idx, par, chunk, g0, m);
+    }
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < L; b += nwaves * 64) {
+      uint32_t x[K][4];
+      load_data_symbols<K, false, F>(slot, chunk, L, b, 1, ow, m, x, &fl);
+      fix_data_tail<K>(slot, chunk, L, b, 1, ow, m, x);
+      rows_out<K>(x, rows, coeff, out_idx, par, chunk, 4 * b, m, 1);
+    }
+    if constexpr (F) {
+      const uint32_t f = fl.bits();
+      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+      if (wf && lane == 0) atomicOr(&flags[obj], wf);
+    }
+  }
+}
+
+// flags -> MapToGF's choice (map.go:35-62): 0 if no word >= p, else 1<<31 if
+// that fits, else the random fallback: status 1, resolved on the host.
+// `status` holds the flags on entry (in place: each lane owns one object).
+__global__ void select_mapping_kernel(uint32_t* __restrict__ mapping, uint32_t* __restrict__ status, uint32_t nobj) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= nobj) return;
+  const uint32_t f = status[o];
+  const bool zero_ok = !(f & 1u), high_ok = !(f & 2u);
+  mapping[o] = zero_ok ? 0u : (high_ok ? 0x80000000u : 0u);
+  status[o] = (!zero_ok && !high_ok) ? 1u : 0u;
+}
+
+// Decode: rebuild `rows` chunks (out_idx slots) from need survivors (in_idx).
+template <int K>
+__device__ __forceinline__ void load_chunk_symbols(const uint8_t* slot, const uint64_t (&ioff)[K], uint64_t b,
+                                                   int ncol, uint32_t m, uint32_t (&x)[K][4]) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint8_t* src = slot + ioff[j] + 4 * b;
+    if (ncol == 4) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+      x[j][0] = be(v.x) ^ m, x[j][1] = be(v.y) ^ m, x[j][2] = be(v.z) ^ m, x[j][3] = be(v.w) ^ m;
+    } else {
+      x[j][0] = be(*reinterpret_cast<const uint32_t*>(src)) ^ m;
+      x[j][1] = x[j][2] = x[j][3] = 0;
+    }
+  }
+}
+
+template <int K, int U>
+__global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
+                                                              uint64_t L, uint32_t nobj, uint32_t rows,
+                                                              const uint32_t* __restrict__ coeff,
+                                                              const uint32_t* __restrict__ in_idx,
+                                                              const uint32_t* __restrict__ out_idx,
+                                                              const uint32_t* __restrict__ mapping) {
+  const uint64_t chunk = 4 * L;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t nvec = L >> 2;
+  const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+    const uint32_t m = mapping[obj];
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride;
+    uint64_t ioff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * chunk;
+    for (uint64_t step = wave; step < ntiles; step += nwaves) {
+      const uint64_t g0 = step * (64 * U) + lane;
+      uint32_t x[U][K][4];
+      int n = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (g0 + 64 * u < nvec) {
+          load_chunk_symbols<K>(slot, ioff, (g0 + 64 * u) << 2, 4, m, x[u]);
+          n = u + 1;
+        }
+      rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot, chunk, g0, m);
+    }
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < L; b += nwaves * 64) {
+      uint32_t x[K][4];
+      load_chunk_symbols<K>(slot, ioff, b, 1, m, x);
+      rows_out<K>(x, rows, coeff, out_idx, slot, chunk, 4 * b, m, 1);
+    }
+  }
+}
+
+}  // namespace bytes
+}  // namespace slime

@@ -28,6 +28,7 @@ struct slime_rs_plan {
   int device = 0;
   uint32_t rows = 0, k = 0;
   uint32_t out_max = 0;         // highest destination shard index
+  std::vector<uint32_t> in_idx_host;  // input shard indices (host copy, bounds checks)
   std::vector<uint32_t> coeff;  // rows x k, host copy
   uint32_t* table = nullptr;    // device: coeff (rows x coeff_stride(k)) | in_idx (k) | out_idx (rows)
   const uint32_t* d_coeff = nullptr;
@@ -95,6 +96,7 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   plan->k = k;
   plan->coeff.assign(coeff, coeff + (size_t)rows * k);
   plan->out_max = out_idx.empty() ? 0 : *std::max_element(out_idx.begin(), out_idx.end());
+  plan->in_idx_host = in_idx;
   const uint32_t cs = coeff_stride(k);
   const size_t ncoef = (size_t)rows * cs;
   const size_t n_in = (k + 3) & ~3u, n_out = (rows + 3) & ~3u;
@@ -429,6 +431,132 @@ int slime_rs_plan_coefficients(slime_rs_plan_t plan, uint32_t* out) {
 
 int slime_rs_plan_destroy(slime_rs_plan_t plan) {
   destroy_plan(plan);
+  return 0;
+}
+
+// ---- fused byte-domain object pipeline ------------------------------------------------
+
+static uint64_t slot_L(uint64_t S, uint32_t need) { return ((S + 3) / 4 + need - 1) / need; }
+
+static int check_slots(const slime_rs_plan* plan, const uint8_t* slots, uint64_t slot_stride, uint64_t L,
+                       uint32_t first_out, const char* what) {
+  if (!plan || !slots) return fail(Status::InvalidArg, std::string(what) + ": null plan or slots");
+  if (plan->k == 0 || plan->k > 16) return fail(Status::InvalidArg, std::string(what) + ": need must be 1..16");
+  const uint64_t chunk = 4 * L;
+  uint64_t hi = first_out + plan->out_max;
+  for (uint32_t j = 0; j < plan->k; ++j) hi = std::max<uint64_t>(hi, plan->in_idx_host[j]);
+  if ((hi + 1) * chunk > slot_stride)
+    return fail(Status::InvalidArg, std::string(what) + ": slot_stride smaller than the chunks it must hold");
+  return 0;
+}
+
+static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
+                                uint64_t S, uint64_t nobj, int phase, uint32_t* flags, const uint32_t* mapping) {
+  BytesLaunch a;
+  a.slots = slots;
+  a.slot_stride = slot_stride;
+  a.L = L;
+  a.S = S;
+  a.nobj = (uint32_t)nobj;
+  a.rows = plan->rows;
+  a.k = plan->k;
+  a.phase = phase;
+  a.coeff = plan->d_coeff;
+  a.in_idx = plan->d_in_idx;
+  a.out_idx = plan->d_out_idx;
+  a.flags = flags;
+  a.mapping = mapping;
+  return a;
+}
+
+extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                       uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
+                                       void* stream) {
+  if (nobj == 0) return 0;
+  if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "encode_objects: nobj exceeds 2^32-1");
+  if (!mapping || !status) return fail(Status::InvalidArg, "encode_objects: null mapping/status");
+  const uint64_t L = slot_L(object_size, plan ? plan->k : 1);
+  // parity row i goes to chunk need + out_idx[i]
+  if (int rc = check_slots(plan, slots, slot_stride, L, plan ? plan->k : 0, "encode_objects")) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  DeviceScope ds(plan->device);
+  HIP_TRY(hipMemsetAsync(status, 0, nobj * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(mapping, 0, nobj * sizeof(uint32_t), s));
+  if (L == 0) return 0;
+  HIP_TRY(launch_encode_bytes(bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 0, status, mapping), s));
+  HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
+  HIP_TRY(launch_encode_bytes(bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 1, status, mapping), s));
+  return 0;
+}
+
+extern "C" int slime_rs_resolve_fallbacks(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                          uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
+                                          void* stream, int* resolved) {
+  if (resolved) *resolved = 0;
+  if (nobj == 0) return 0;
+  if (!mapping || !status) return fail(Status::InvalidArg, "resolve_fallbacks: null mapping/status");
+  const uint64_t L = slot_L(object_size, plan ? plan->k : 1);
+  if (int rc = check_slots(plan, slots, slot_stride, L, plan ? plan->k : 0, "resolve_fallbacks")) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  DeviceScope ds(plan->device);
+  std::vector<uint32_t> st(nobj);
+  HIP_TRY(hipMemcpyAsync(st.data(), status, nobj * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint64_t nw = (object_size + 3) / 4;
+  constexpr uint32_t kCand = 64;
+  WsLease lease;
+  bool have_ws = false;
+  for (uint64_t o = 0; o < nobj; ++o) {
+    if (st[o] != 1) continue;
+    if (!have_ws) {
+      if (int rc = acquire_ws(plan->device, &lease.ws)) return rc;
+      if (int rc = lease.ws->reserve(round16(nw * 4) + 2 * kCand * 4)) return rc;
+      have_ws = true;
+    }
+    uint32_t* d_words = (uint32_t*)lease.ws->dbuf;
+    uint32_t* d_cand = (uint32_t*)(lease.ws->dbuf + round16(nw * 4));
+    uint32_t* d_bad = d_cand + kCand;
+    uint8_t* slot = slots + o * slot_stride;
+    HIP_TRY(launch_map_pack(slot, object_size, 0, d_words, nullptr, s));
+    uint32_t m = 0;
+    bool found = false;
+    for (int round = 0; round < (1 << 16) && !found; ++round) {
+      uint32_t cand[kCand], bad[kCand];
+      {
+        std::lock_guard<std::mutex> lk(g_rng_mu);
+        for (uint32_t c = 0; c < kCand; ++c) cand[c] = (uint32_t)(g_rng() >> 32);
+      }
+      HIP_TRY(hipMemcpyAsync(d_cand, cand, sizeof(cand), hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(bad), s));
+      HIP_TRY(launch_mapping_probe(d_words, nw, d_cand, kCand, d_bad, s));
+      HIP_TRY(hipMemcpyAsync(bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      for (uint32_t c = 0; c < kCand && !found; ++c)
+        if (!bad[c] && cand[c] != 0) {
+          m = cand[c];
+          found = true;
+        }
+    }
+    if (!found) return status_of(Status::MappingFallback, "resolve_fallbacks");
+    const uint32_t zero = 0;
+    HIP_TRY(hipMemcpyAsync(mapping + o, &m, 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(status + o, &zero, 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, slot_stride, L, object_size, 1, 1, status + o, mapping + o), s));
+    HIP_TRY(hipStreamSynchronize(s));  // m and zero live on this frame
+    if (resolved) ++*resolved;
+  }
+  return 0;
+}
+
+extern "C" int slime_rs_decode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
+                                       uint64_t nobj, const uint32_t* mapping, void* stream) {
+  if (nobj == 0 || L == 0) return 0;
+  if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "decode_objects: nobj exceeds 2^32-1");
+  if (!mapping) return fail(Status::InvalidArg, "decode_objects: null mapping");
+  if (int rc = check_slots(plan, slots, slot_stride, L, 0, "decode_objects")) return rc;
+  DeviceScope ds(plan->device);
+  HIP_TRY(launch_decode_bytes(bytes_launch(plan, slots, slot_stride, L, 0, nobj, 0, nullptr, mapping),
+                              (hipStream_t)stream));
   return 0;
 }
 

@@ -146,3 +146,55 @@ def unpack_words(words: torch.Tensor, mapping: int, dst: torch.Tensor,
         raise ValueError("byte tensor too small")
     N.check(lib.slime_gf_unpack_device(ctypes.c_void_p(words.data_ptr()), words.numel(), mapping & 0xFFFFFFFF,
                                        ctypes.c_void_p(dst.data_ptr()), _stream_handle(dev, stream)))
+
+
+# ---- fused byte-domain object pipeline (writeChunks / reconstruct on device) ----
+
+def slot_geometry(object_size: int, need: int, total: int) -> tuple[int, int, int]:
+    """(L symbols per chunk, chunk bytes, minimal slot bytes) for objects of object_size bytes."""
+    L = -(-(-(-object_size // 4)) // need)
+    return L, 4 * L, 4 * L * total
+
+
+def _check_slots(slots: torch.Tensor, slot_stride: int, nobj: int, slot_bytes: int) -> int:
+    if slots.dtype != torch.uint8 or not slots.is_contiguous():
+        raise TypeError("slots must be a contiguous uint8 tensor")
+    if nobj and (slot_stride < slot_bytes or (nobj - 1) * slot_stride + slot_bytes > slots.numel()):
+        raise ValueError("slot layout exceeds the slots tensor")
+    return _dev_index(slots)
+
+
+def encode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,
+                   mapping: torch.Tensor, status: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Device writeChunks: chunks of every object slot, gf.MapToGF's mapping per object."""
+    _, _, need_bytes = slot_geometry(object_size, plan.k, plan.k + plan.rows)
+    dev = _check_slots(slots, slot_stride, nobj, need_bytes)
+    for t in (mapping, status):
+        if t.numel() < nobj or t.dtype not in (torch.int32, torch.uint32):
+            raise ValueError("mapping/status need nobj int32 words")
+    N.check(lib.slime_rs_encode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, object_size, nobj,
+                                        ctypes.c_void_p(mapping.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                                        _stream_handle(dev, stream)))
+
+
+def resolve_fallbacks(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,
+                      mapping: torch.Tensor, status: torch.Tensor,
+                      stream: Optional[torch.cuda.Stream] = None) -> int:
+    """Finish objects that need MapToGF's random mapping; returns how many were fixed."""
+    _, _, need_bytes = slot_geometry(object_size, plan.k, plan.k + plan.rows)
+    dev = _check_slots(slots, slot_stride, nobj, need_bytes)
+    n = ctypes.c_int(0)
+    N.check(lib.slime_rs_resolve_fallbacks(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, object_size,
+                                           nobj, ctypes.c_void_p(mapping.data_ptr()),
+                                           ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream),
+                                           ctypes.byref(n)))
+    return n.value
+
+
+def decode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, L: int, nobj: int, mapping: torch.Tensor,
+                   stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Device reconstruct: rebuild the plan's output chunks from its input chunks in every slot."""
+    hi = max(plan.in_max, plan.rows - 1 if plan.out_max is None else plan.out_max)
+    dev = _check_slots(slots, slot_stride, nobj, 4 * L * (hi + 1))
+    N.check(lib.slime_rs_decode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, L, nobj,
+                                        ctypes.c_void_p(mapping.data_ptr()), _stream_handle(dev, stream)))

@@ -326,3 +326,113 @@ def test_fill_symbols_deterministic_and_canonical(torch_dev):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert int(a.cpu().numpy().view(np.uint32).max()) < P
+
+
+# ------------------------------------------- fused byte-domain object pipeline
+
+def _oracle_chunks(obj: bytes, need: int, total: int, cands=()):
+    """The reference's writeChunks framing (multi_store.go:526-554) via the oracle."""
+    rc, m, words = OC.map_to_gf(obj, list(cands))
+    assert rc == 0
+    parts = OP.split_vector(words, need)
+    parity = [OC.create_parity(parts, need + i)[1] for i in range(total - need)]
+    return m, [OC.map_from_gf(m, p) for p in parts + parity]
+
+
+def _make_slots(torch, objs, need, total, extra=0):
+    from slime_amd import device as D
+    S = len(objs[0])
+    L, chunk, slot = D.slot_geometry(S, need, total)
+    stride = slot + extra
+    host = np.zeros(len(objs) * stride, dtype=np.uint8)
+    for o, b in enumerate(objs):
+        host[o * stride: o * stride + S] = np.frombuffer(b, dtype=np.uint8)
+        host[o * stride + S: (o + 1) * stride] = 0xA5  # garbage past the object
+    return torch.from_numpy(host).cuda(), L, chunk, stride
+
+
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20)])
+@pytest.mark.parametrize("S", [1, 3, 4, 5, 31, 32, 33, 1000, 4096, 65537, 1 << 20])
+def test_encode_objects_matches_write_chunks(torch_dev, need, total, S):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(S * 31 + need)
+    objs = [rng.integers(0, 256, size=S, dtype=np.uint8).tobytes() for _ in range(3)]
+    # object 1 forces mapping 1<<31 (a word >= p, no word in 0x7FFFFFFB..0x7FFFFFFF)
+    if S >= 4:
+        b = bytearray(objs[1]); b[0:4] = b"\xff\xff\xff\xfd"; objs[1] = bytes(b)
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total, extra=12)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(3, dtype=torch.int32, device="cuda")
+    status = torch.empty(3, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 3, mapping, status)
+    torch.cuda.synchronize()
+    h = slots.cpu().numpy()
+    ms = mapping.cpu().numpy().view(np.uint32)
+    assert status.cpu().numpy().tolist() == [0, 0, 0]
+    for o, obj in enumerate(objs):
+        m, chunks = _oracle_chunks(obj, need, total)
+        assert ms[o] == m
+        for c in range(total):
+            got = h[o * stride + c * chunk: o * stride + (c + 1) * chunk].tobytes()
+            assert got == chunks[c], (o, c)
+    if S >= 4:
+        assert ms[1] == 1 << 31
+
+
+def test_encode_objects_random_fallback(torch_dev):
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, S = 4, 6, 4096
+    rng = np.random.default_rng(9)
+    b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+    b[0:8] = b"\xff\xff\xff\xff\x7f\xff\xff\xff"  # neither 0 nor 1<<31 fits (map_test.go TestMapTricky)
+    objs = [bytes(b), rng.integers(0, 256, size=S, dtype=np.uint8).tobytes()]
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(2, dtype=torch.int32, device="cuda")
+    status = torch.empty(2, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 2, mapping, status)
+    torch.cuda.synchronize()
+    assert status.cpu().numpy().tolist() == [1, 0]
+    assert D.resolve_fallbacks(plan, slots, stride, S, 2, mapping, status) == 1
+    m = int(mapping.cpu().numpy().view(np.uint32)[0])
+    assert status.cpu().numpy().tolist() == [0, 0]
+    # the chosen mapping is valid and the chunks are the reference's for that mapping
+    rc, m2, _ = OC.map_to_gf(objs[0], [m])
+    assert rc == 0 and m2 == m
+    _, chunks = _oracle_chunks(objs[0], need, total, [m])
+    h = slots.cpu().numpy()
+    for c in range(total):
+        assert h[c * chunk:(c + 1) * chunk].tobytes() == chunks[c]
+
+
+@pytest.mark.parametrize("need,total,S", [(4, 6, 5000), (8, 12, 1 << 20), (8, 12, 999999), (10, 14, 77777),
+                                          (2, 3, 3)])
+def test_decode_objects_repairs_chunks(torch_dev, need, total, S):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(S)
+    objs = [rng.integers(0, 256, size=S, dtype=np.uint8).tobytes() for _ in range(4)]
+    if S >= 4:
+        b = bytearray(objs[2]); b[0:4] = b"\xff\xff\xff\xfe"; objs[2] = bytes(b)  # mapping 1<<31
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(4, dtype=torch.int32, device="cuda")
+    status = torch.empty(4, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 4, mapping, status)
+    torch.cuda.synchronize()
+    truth = slots.clone()
+    r = total - need
+    for erase in (list(range(min(r, need))), [0, total - 1][:r], [need - 1]):
+        have = [i for i in range(total) if i not in erase][:need]
+        rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+        v = slots.view(4, stride)[:, : total * chunk].view(4, total, chunk)
+        v[:, erase, :] = 0x5A
+        D.decode_objects(rec, slots, stride, L, 4, mapping)
+        torch.cuda.synchronize()
+        assert torch.equal(slots, truth), erase
+    # the object bytes are the first S bytes of each slot (reconstruct's data[:Size])
+    h = slots.cpu().numpy()
+    for o, obj in enumerate(objs):
+        assert h[o * stride: o * stride + S].tobytes() == obj

@@ -42,7 +42,9 @@ def main():
     ap.add_argument("--blocks", type=str, default="256,384,512,768,1024")
     ap.add_argument("--inflight", type=str, default="0", help="objects in flight (0 = all)")
     ap.add_argument("--decode", type=int, default=0, help="time reconstruct of data 0..e-1 instead of encode")
-    ap.add_argument("--pad", type=int, default=0, help="shard stride = L + pad symbols")
+    ap.add_argument("--pad", type=str, default="0", help="shard stride = L + pad symbols (comma list)")
+    ap.add_argument("--hunt", choices=["any", "slow", "fast"], default="any",
+                    help="re-allocate until the product encode runs in the given placement mode")
     ap.add_argument("--separate", type=int, default=-1,
                     help="1: write to a separate buffer, 0: in place (default: encode in place, decode separate)")
     args = ap.parse_args()
@@ -55,13 +57,45 @@ def main():
     need, total, nobj = args.need, args.total, args.nobj
     r = total - need
     L = (args.mib << 20) // 4 // need
-    SS = L + args.pad  # shard stride
-    tail = nobj * r * SS if args.separate == 2 else 0  # 2: destination in the same allocation, after the objects
-    whole = torch.empty(nobj * total * SS + tail, dtype=torch.int32, device="cuda")
+    pads = [int(p) for p in args.pad.split(",")]
+    maxss = L + max(pads)
+    tail = nobj * r * maxss if args.separate == 2 else 0  # 2: destination in the same allocation, after the objects
+    enc = D.Plan.encode(need, total)
+    hunt_ms, keep = [], []
+    for attempt in range(24):
+        whole = torch.empty(nobj * total * maxss + tail, dtype=torch.int32, device="cuda")
+        if args.hunt == "any":
+            break
+        lay0 = D.layout_of(total, L)
+        probe = whole[: nobj * total * L]
+        D.fill_symbols(probe, 7)
+        t = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            enc(probe, lay0, probe, lay0, L, nobj, dst_offset=need * L)
+            b.record()
+            torch.cuda.synchronize()
+            t.append(a.elapsed_time(b))
+        hunt_ms.append(round(min(t[1:]), 3))
+        slow = min(t[1:]) > 9.2 * (nobj / 128) * (args.mib / 256)
+        if (args.hunt == "slow") == slow:
+            break
+        keep = (keep + [whole])[-2:]  # hold the last two so the next allocation lands elsewhere
+        torch.cuda.empty_cache()
+    del keep
+    torch.cuda.empty_cache()
+    results_by_pad = {}
+    for pad in pads:
+        results_by_pad[pad] = run_pad(args, lib, whole, enc, need, total, r, nobj, L, L + pad, VARIANTS)
+    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj}", "decode": bool(args.decode),
+                      "hunt": args.hunt, "hunt_probe_ms": hunt_ms, "by_pad": results_by_pad}, indent=1))
+
+
+def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     buf = whole[: nobj * total * SS]
     D.fill_symbols(buf, 7)
     lay = D.layout_of(total, L, SS)
-    enc = D.Plan.encode(need, total)
     enc(buf, lay, buf, lay, L, nobj, dst_offset=need * SS)
     torch.cuda.synchronize()
     shards = lambda: buf.view(nobj, total, SS)[:, :, :L]  # noqa: E731
@@ -83,7 +117,7 @@ def main():
         ii = torch.arange(need, dtype=torch.int32, device="cuda")
         slot0 = need
     if separate:
-        dst = whole[nobj * total * SS:] if args.separate == 2 else \
+        dst = whole[whole.numel() - nobj * r * SS:] if args.separate == 2 else \
             torch.empty(nobj * r * SS, dtype=torch.int32, device="cuda")
         oi = torch.arange(r, dtype=torch.int32, device="cuda")
         d_ptr, oo, view = dst.data_ptr(), r * SS, lambda: dst.view(nobj, r, SS)[:, :, :L]
@@ -126,10 +160,8 @@ def main():
         rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "ms": round(med, 3),
                      "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: -x["GBps"])
-    print(json.dumps({"shape": f"{need}/{total} {args.mib} MiB x {nobj} pad {args.pad}", "decode": bool(args.decode),
-                      "separate": int(args.separate if args.separate >= 0 else separate),
-                      "bad_variants": bad, "top": rows[:12],
-                      "all": rows}, indent=1))
+    return {"separate": int(args.separate if args.separate >= 0 else separate), "bad_variants": bad,
+            "top": rows[:12], "all": rows}
 
 
 if __name__ == "__main__":

@@ -37,6 +37,9 @@ has tests && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
 has smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has micro && run micro 600 python tools/microbench.py
 has bench && run bench 600 python bench.py
+if has bench3; then
+  for i in 1 2 3; do run bench_rep$i 300 python bench.py --cpu-baseline 0; done
+fi
 has prof && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
   python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0
 has ubench && run ubench 600 python tools/ubench.py
@@ -73,6 +76,35 @@ if has grid; then
   for g in 1024 4096 8192; do
     run bench_grid$g 300 env SLIME_RS_GRID_TARGET=$g python bench.py --steps 5 --cpu-baseline 0
   done
+fi
+has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
+has contig && run contig 600 python tools/alloc_contig.py --rounds 6
+has hbmmap && run hbmmap 600 python tools/hbm_map.py
+has bytesvar && run bytesvar 600 python tools/bytes_variants.py
+if has bvs; then
+  for i in 1 2 3; do run bvs$i 300 python tools/bytes_vs_symbols.py; done
+fi
+if has bvspmc; then
+  run bvs_pmc1 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d "$OUT/bvs_pmc1" -o p --output-format csv -- python3 tools/bytes_vs_symbols.py
+  run bvs_pmc2 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d "$OUT/bvs_pmc2" -o p --output-format csv -- python3 tools/bytes_vs_symbols.py
+fi
+if has hunt3; then
+  P="0,65536,262144,524288,1048576,2097152,4194304"
+  run hunt3_slow 600 python tools/apply_variants.py --hunt slow --variants 8 --blocks 512 --inflight 0 --pad $P
+  run hunt3_fast 600 python tools/apply_variants.py --hunt fast --variants 8 --blocks 512 --inflight 0 --pad $P
+fi
+if has hunt2; then
+  run hunt2_slow 600 python tools/apply_variants.py --hunt slow --variants 8 --blocks 256,512,1024 --inflight 1,2,4,8,128 --pad 0
+  run hunt2_fast 600 python tools/apply_variants.py --hunt fast --variants 8 --blocks 256,512,1024 --inflight 1,2,4,8,128 --pad 0
+fi
+if has hunt; then
+  run hunt_slow 600 python tools/apply_variants.py --hunt slow --variants 0,1,2,4,8,11 --blocks 256,512,1024 --inflight 0,16 --pad 0,64,4160
+  run hunt_fast 600 python tools/apply_variants.py --hunt fast --variants 0,1,2,4,8,11 --blocks 256,512,1024 --inflight 0,16 --pad 0,64,4160
+fi
+if has sustained; then
+  run sustained1 300 python tools/sustained.py --seconds 8 --idle 2
+  run smi 60 rocm-smi --showclocks --showperflevel --showpower
+  run sustained2 300 python tools/sustained.py --seconds 8 --idle 0
 fi
 if has pmc; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- \
