@@ -8,7 +8,7 @@ SRC      := slime_amd/csrc
 OBJ      := build/obj
 LIB      := slime_amd/lib/libslime_rs.so
 
-OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_bytes.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/rs_capi.o
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_bytes.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 all: $(LIB) oracle
@@ -21,7 +21,7 @@ $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS) | $(OBJ)
 
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libslime_rs.so -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libslime_rs.so -Wl,--no-undefined -lpthread
 
 $(OBJ):
 	@mkdir -p $@

@@ -58,6 +58,19 @@ const char *slime_rs_version(void);
 int slime_rs_device_count(void);
 /* Device the calling thread's Go-API entry points run on (default 0). */
 int slime_rs_select_device(int device);
+/* How the Go-API entry points (CreateParity/CreateParities/RecoverData) move
+ * host rows to the GPU and back (process-wide; env SLIME_RS_HOST_PIPE sets
+ * the initial value):
+ *   0 staged   - column-chunked 3-stage ring through pinned staging buffers,
+ *                H2D / kernel / D2H of one chunk overlapping the host copies
+ *                of the others (default);
+ *   1 register - page-lock the caller's rows for the call and DMA directly
+ *                (falls back to staged when registration is refused);
+ *   2 direct   - one-shot pageable hipMemcpy (measurement reference).
+ * mode < 0 queries: returns the current mode.  Otherwise returns 0, or
+ * SLIME_RS_ERR_INVALID_ARG for an unknown mode.  No reference counterpart:
+ * the Go implementation computes in place on host memory. */
+int slime_rs_host_pipeline(int mode);
 
 /* ==== internal/rs/gf ===================================================== */
 

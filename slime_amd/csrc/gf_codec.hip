@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint32_t* __restrict__ dst
 
 hipError_t launch_map_pack(const uint8_t* bytes, uint64_t len, uint32_t mapping, uint32_t* words_out,
                            uint32_t* flags, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   const uint64_t nwords = (len + 3) / 4;
   if (nwords == 0) return hipSuccess;
   uint64_t done_words = 0;
@@ -165,6 +166,7 @@ hipError_t launch_map_pack(const uint8_t* bytes, uint64_t len, uint32_t mapping,
 }
 
 hipError_t launch_xor_words(uint32_t* words, uint64_t n, uint32_t mapping, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (n == 0 || mapping == 0) return hipSuccess;
   hipLaunchKernelGGL(xor_kernel, dim3((uint32_t)grid_for(n)), dim3(kBlock), 0, s, words, n, mapping);
   return hipGetLastError();
@@ -172,6 +174,7 @@ hipError_t launch_xor_words(uint32_t* words, uint64_t n, uint32_t mapping, hipSt
 
 hipError_t launch_mapping_probe(const uint32_t* words, uint64_t n, const uint32_t* cand, uint32_t ncand,
                                 uint32_t* bad, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (n == 0 || ncand == 0) return hipSuccess;
   if (ncand > 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(probe_kernel, dim3((uint32_t)grid_for(n)), dim3(kBlock), 0, s, words, n, cand, ncand, bad);
@@ -179,6 +182,7 @@ hipError_t launch_mapping_probe(const uint32_t* words, uint64_t n, const uint32_
 }
 
 hipError_t launch_map_unpack(const uint32_t* words, uint64_t n, uint32_t mapping, uint8_t* bytes_out, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (n == 0) return hipSuccess;
   uint64_t done = 0;
   const bool aligned = (((uintptr_t)words | (uintptr_t)bytes_out) & 15u) == 0;
@@ -195,6 +199,7 @@ hipError_t launch_map_unpack(const uint32_t* words, uint64_t n, uint32_t mapping
 }
 
 hipError_t launch_fill_symbols(uint32_t* dst, uint64_t n, uint64_t seed, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(fill_kernel, dim3((uint32_t)grid_for(n)), dim3(kBlock), 0, s, dst, n, seed);
   return hipGetLastError();

@@ -1,0 +1,175 @@
+// Persistent host copy pool (host_copy.hpp).
+#include "host_copy.hpp"
+
+#include <emmintrin.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace slime {
+namespace {
+
+constexpr size_t kPiece = 512u << 10;  // bytes per work piece
+constexpr size_t kSerialBelow = 2u << 20;  // small copies: not worth a wake-up
+
+struct Job {
+  const CopyItem* pieces = nullptr;
+  size_t n = 0;
+  std::atomic<size_t> next{0};
+  size_t done = 0;  // guarded by Pool::mu
+  int active = 0;   // workers holding a pointer to this job (guarded)
+};
+
+// Streaming (non-temporal) copy: the staged rows are written once and not
+// read again by this core, so bypassing the cache saves the read-for-ownership
+// of every destination line.
+void stream_copy(void* dst, const void* src, size_t n) {
+  char* d = (char*)dst;
+  const char* s = (const char*)src;
+  const size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+  if (n < 256 || head > n) {
+    memcpy(d, s, n);
+    return;
+  }
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128((const __m128i*)(s + i));
+    const __m128i b = _mm_loadu_si128((const __m128i*)(s + i + 16));
+    const __m128i c = _mm_loadu_si128((const __m128i*)(s + i + 32));
+    const __m128i e = _mm_loadu_si128((const __m128i*)(s + i + 48));
+    _mm_stream_si128((__m128i*)(d + i), a);
+    _mm_stream_si128((__m128i*)(d + i + 16), b);
+    _mm_stream_si128((__m128i*)(d + i + 32), c);
+    _mm_stream_si128((__m128i*)(d + i + 48), e);
+  }
+  memcpy(d + i, s + i, n - i);
+  _mm_sfence();
+}
+
+bool use_nt() {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_COPY_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+void copy_piece(const CopyItem& it) {
+  if (use_nt())
+    stream_copy(it.dst, it.src, it.bytes);
+  else
+    memcpy(it.dst, it.src, it.bytes);
+}
+
+size_t drain(Job* j) {
+  size_t did = 0;
+  for (size_t i; (i = j->next.fetch_add(1, std::memory_order_relaxed)) < j->n; ++did) copy_piece(j->pieces[i]);
+  return did;
+}
+
+class Pool {
+ public:
+  explicit Pool(int nthreads) {
+    for (int t = 0; t < nthreads; ++t) th_.emplace_back([this] { worker(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int threads() const { return (int)th_.size(); }
+
+  void run(const CopyItem* pieces, size_t n) {
+    std::unique_lock<std::mutex> owner(run_mu_, std::try_to_lock);
+    if (!owner.owns_lock() || th_.empty()) {  // busy or no workers: copy here
+      for (size_t i = 0; i < n; ++i) copy_piece(pieces[i]);
+      return;
+    }
+    Job j;
+    j.pieces = pieces;
+    j.n = n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      cur_ = &j;
+    }
+    cv_.notify_all();
+    const size_t did = drain(&j);
+    std::unique_lock<std::mutex> lk(mu_);
+    j.done += did;
+    done_cv_.wait(lk, [&] { return j.done == j.n && j.active == 0; });
+    cur_ = nullptr;
+  }
+
+ private:
+  void worker() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || (cur_ && cur_->next.load(std::memory_order_relaxed) < cur_->n); });
+      if (stop_) return;
+      Job* j = cur_;
+      ++j->active;
+      lk.unlock();
+      const size_t did = drain(j);
+      lk.lock();
+      j->done += did;
+      --j->active;
+      if (j->done == j->n && j->active == 0) done_cv_.notify_all();
+    }
+  }
+
+  std::mutex run_mu_;  // one job at a time
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  Job* cur_ = nullptr;
+  bool stop_ = false;
+  std::vector<std::thread> th_;
+};
+
+int env_threads() {
+  const char* s = getenv("SLIME_RS_COPY_THREADS");
+  if (!s || !*s) return 4;
+  const int v = atoi(s);
+  return v < 0 ? 0 : (v > 64 ? 64 : v);
+}
+
+Pool& pool() {
+  static Pool* p = new Pool(env_threads());  // intentionally leaked: workers outlive static destructors
+  return *p;
+}
+
+}  // namespace
+
+int copy_pool_threads() { return pool().threads(); }
+
+void parallel_copy(const CopyItem* items, size_t n) {
+  size_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += items[i].bytes;
+  if (total < kSerialBelow) {
+    for (size_t i = 0; i < n; ++i)
+      if (items[i].bytes) memcpy(items[i].dst, items[i].src, items[i].bytes);
+    return;
+  }
+  std::vector<CopyItem> pieces;
+  pieces.reserve(total / kPiece + n);
+  for (size_t i = 0; i < n; ++i) {
+    char* d = (char*)items[i].dst;
+    const char* s = (const char*)items[i].src;
+    for (size_t off = 0; off < items[i].bytes; off += kPiece)
+      pieces.push_back({d + off, s + off, std::min(kPiece, items[i].bytes - off)});
+  }
+  pool().run(pieces.data(), pieces.size());
+}
+
+}  // namespace slime

@@ -1,0 +1,25 @@
+// Parallel host memcpy for the pinned staging pipeline of the Go-API entry
+// points (rs_capi.cpp).  A single host thread copies at ~10-20 GB/s, below
+// what one PCIe/xGMI host link moves; the staging copies are split into
+// pieces and run on a small persistent pool so the host side keeps pace with
+// the DMA engines.
+#pragma once
+#include <stddef.h>
+
+namespace slime {
+
+struct CopyItem {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+
+// Copy every item (non-overlapping ranges).  Large items are split into
+// pieces spread over the pool; the caller works too.  Concurrent callers are
+// safe: a caller that finds the pool busy copies on its own thread.
+void parallel_copy(const CopyItem* items, size_t n);
+
+// Threads the pool runs besides the caller (env SLIME_RS_COPY_THREADS, default 4).
+int copy_pool_threads();
+
+}  // namespace slime

@@ -34,9 +34,6 @@ inline uint32_t coeff_stride(uint32_t k) { return k <= 16 ? 16u : k; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 
-// out[i] = in[i] mod p  (RecoverData's unit rows for surviving data shards).
-hipError_t launch_canon_copy(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t stream);
-
 // --- fused byte-domain encode/decode over object slots (rs_bytes.hip) --------
 // Slot o at slots + o*slot_stride bytes; chunk c at slot + c*4L.  coeff /
 // in_idx / out_idx are a plan's device tables.  Encode: phase 0 = speculative

@@ -78,15 +78,10 @@ hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   return a.vec_ok ? launch_k<K, true>(a, s) : launch_k<K, false>(a, s);
 }
 
-__global__ __launch_bounds__(kBlock) void canon_copy_kernel(const uint32_t* __restrict__ in,
-                                                            uint32_t* __restrict__ out, uint64_t n) {
-  const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) out[i] = canon(in[i]);
-}
-
 }  // namespace
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.ncols == 0 || a.rows == 0) return hipSuccess;
   switch (a.k) {
     case 1: return dispatch_vec<1>(a, s);
@@ -107,14 +102,6 @@ hipError_t launch_apply(const ApplyLaunch& a, hipStream_t s) {
     case 16: return dispatch_vec<16>(a, s);
     default: return launch_k<0, false>(a, s);
   }
-}
-
-hipError_t launch_canon_copy(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(canon_copy_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, s, in, out, n);
-  return hipGetLastError();
 }
 
 }  // namespace slime

@@ -76,16 +76,19 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0) return hipSuccess;
   SLIME_K_SWITCH(enc_k)
 }
 
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0 || a.rows == 0) return hipSuccess;
   SLIME_K_SWITCH(dec_k)
 }
 
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t s) {
+  (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (nobj == 0) return hipSuccess;
   hipLaunchKernelGGL(select_mapping_kernel, dim3((nobj + 255) / 256), dim3(256), 0, s, mapping, status, nobj);
   return hipGetLastError();

@@ -8,10 +8,12 @@
 #include "slime_rs.h"
 
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -21,6 +23,7 @@
 #include <vector>
 
 #include "gfp_host.hpp"
+#include "host_copy.hpp"
 #include "kernels.hpp"
 #include "rs_matrix.hpp"
 
@@ -183,19 +186,48 @@ int cached_plan(const PlanKey& key, slime_rs_plan** out,
 // ---- per-call device workspaces (host entry points) ----------------------------
 
 struct Workspace {
+  static constexpr int kStages = 3;  // host pipeline depth (host_apply)
   int device = -1;
   hipStream_t stream = nullptr;
   uint8_t* dbuf = nullptr;
   size_t dcap = 0;
+  hipStream_t sst[kStages] = {};  // one stream per pipeline stage
+  hipEvent_t sev[kStages] = {};   // stage's D2H done
+  uint8_t* pin = nullptr;         // pinned staging, kStages x (in rows | out rows)
+  size_t pcap = 0;
   int reserve(size_t bytes) {
     if (bytes <= dcap) return 0;
     DeviceScope ds(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (hipStream_t st : sst)
+      if (st) (void)hipStreamSynchronize(st);
     if (dbuf) (void)hipFree(dbuf);
     dbuf = nullptr;
     dcap = 0;
     size_t want = std::max<size_t>(bytes, 1u << 20);
     HIP_TRY(hipMalloc((void**)&dbuf, want));
     dcap = want;
+    return 0;
+  }
+  int reserve_pinned(size_t bytes) {
+    if (bytes <= pcap) return 0;
+    DeviceScope ds(device);
+    for (hipStream_t st : sst)
+      if (st) (void)hipStreamSynchronize(st);
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pcap = 0;
+    HIP_TRY(hipHostMalloc((void**)&pin, bytes, hipHostMallocDefault));
+    pcap = bytes;
+    return 0;
+  }
+  int ensure_stages() {
+    if (sst[0]) return 0;
+    DeviceScope ds(device);
+    for (int i = 0; i < kStages; ++i) {
+      HIP_TRY(hipStreamCreateWithFlags(&sst[i], hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming));
+    }
     return 0;
   }
 };
@@ -235,6 +267,181 @@ struct WsLease {
 };
 
 size_t round16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+// ---- host <-> device pipeline for the Go-API entry points ----------------------
+//
+// Column-chunked and kStages deep: chunk c's H2D / kernel / D2H run on stage
+// stream c % S while the host thread copies chunk c-S's results out of pinned
+// memory and chunk c's inputs into it (host_copy.cpp spreads those memcpys
+// over a small pool).  The caller's buffers stay pageable; only the staging
+// ring is pinned, so nothing is registered per call.
+
+constexpr size_t kStageBytes = 8u << 20;  // in + out bytes one stage moves
+
+enum class HostPipe : int { Staged = 0, Register = 1, Direct = 2 };
+
+std::atomic<int> g_host_pipe{[] {
+  const char* e = getenv("SLIME_RS_HOST_PIPE");
+  if (e && strcmp(e, "direct") == 0) return (int)HostPipe::Direct;      // one-shot pageable copies
+  if (e && strcmp(e, "register") == 0) return (int)HostPipe::Register;  // pin caller rows per call
+  return (int)HostPipe::Staged;
+}()};
+
+HostPipe host_pipe_mode() { return (HostPipe)g_host_pipe.load(std::memory_order_relaxed); }
+
+int host_apply_direct(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
+                      uint64_t L) {
+  const size_t shard = round16(L * 4) / 4;  // keep every shard 16-byte aligned
+  if (int rc = ws->reserve(shard * 4 * ((size_t)plan->k + plan->rows))) return rc;
+  uint32_t* d_in = (uint32_t*)ws->dbuf;
+  uint32_t* d_out = d_in + shard * plan->k;
+  for (uint32_t j = 0; j < plan->k; ++j)
+    HIP_TRY(hipMemcpyAsync(d_in + shard * j, in[j], L * 4, hipMemcpyHostToDevice, ws->stream));
+  if (int rc = execute(plan, d_in, 0, shard, d_out, 0, shard, L, 1, ws->stream)) return rc;
+  for (uint32_t i = 0; i < plan->rows; ++i)
+    HIP_TRY(hipMemcpyAsync(out[i], d_out + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
+  HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
+                      uint64_t L) {
+  const uint64_t nin = plan->k, nout = plan->rows;
+  uint64_t cl = std::max<uint64_t>(kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
+  if (cl >= L) cl = (L + 3) & ~3ull;  // one chunk; rows stay 16-byte aligned
+  const uint64_t nch = (L + cl - 1) / cl;
+  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
+  const size_t stage_words = (size_t)(nin + nout) * cl;
+  if (int rc = ws->reserve(stage_words * 4 * S)) return rc;
+  if (int rc = ws->reserve_pinned(stage_words * 4 * S)) return rc;
+  if (int rc = ws->ensure_stages()) return rc;
+  uint32_t* const pin = (uint32_t*)ws->pin;
+  uint32_t* const dev = (uint32_t*)ws->dbuf;
+  std::vector<CopyItem> items;
+  items.reserve(std::max(nin, nout));
+  // SLIME_RS_PIPE_TRACE=1: per-call split of host time (copy in / wait / copy out).
+  static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  double t_in = 0, t_wait = 0, t_out = 0;
+  const auto t_start = clk::now();
+  auto since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+
+  auto copy_out = [&](uint64_t c) -> int {
+    const int s = (int)(c % S);
+    const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
+    auto t0 = clk::now();
+    HIP_TRY(hipEventSynchronize(ws->sev[s]));
+    t_wait += since(t0);
+    t0 = clk::now();
+    const uint32_t* po = pin + s * stage_words + nin * cl;
+    items.clear();
+    for (uint64_t i = 0; i < nout; ++i) items.push_back({out[i] + c0, po + i * cl, n * 4});
+    parallel_copy(items.data(), items.size());
+    t_out += since(t0);
+    return 0;
+  };
+  auto body = [&]() -> int {
+    for (uint64_t c = 0; c < nch; ++c) {
+      const int s = (int)(c % S);
+      if (c >= (uint64_t)S)
+        if (int rc = copy_out(c - S)) return rc;
+      const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
+      uint32_t* pi = pin + s * stage_words;
+      uint32_t* di = dev + s * stage_words;
+      auto t0 = clk::now();
+      items.clear();
+      for (uint64_t j = 0; j < nin; ++j) items.push_back({pi + j * cl, in[j] + c0, n * 4});
+      parallel_copy(items.data(), items.size());
+      t_in += since(t0);
+      hipStream_t st = ws->sst[s];
+      HIP_TRY(hipMemcpyAsync(di, pi, ((nin - 1) * cl + n) * 4, hipMemcpyHostToDevice, st));
+      if (int rc = execute(plan, di, 0, cl, di + nin * cl, 0, cl, n, 1, st)) return rc;
+      HIP_TRY(hipMemcpyAsync(pi + nin * cl, di + nin * cl, ((nout - 1) * cl + n) * 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipEventRecord(ws->sev[s], st));
+    }
+    for (uint64_t c = nch > (uint64_t)S ? nch - S : 0; c < nch; ++c)
+      if (int rc = copy_out(c)) return rc;
+    return 0;
+  };
+  const int rc = body();
+  if (rc)  // drain what was queued before the failure: the ring is reused by the next call
+    for (int s = 0; s < S; ++s) (void)hipStreamSynchronize(ws->sst[s]);
+  if (trace)
+    fprintf(stderr, "slime_rs staged L=%llu chunks=%llu in=%.3f wait=%.3f out=%.3f total=%.3f ms\n",
+            (unsigned long long)L, (unsigned long long)nch, t_in, t_wait, t_out, since(t_start));
+  return rc;
+}
+
+// Register mode: page-lock the caller's rows for the duration of the call
+// and DMA straight from / to them (no host memcpy at all).  Returns -1 when
+// registration is refused (read-only or already-registered pages) so the
+// caller can stage instead.
+int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
+                          uint64_t L) {
+  const uint64_t nin = plan->k, nout = plan->rows;
+  std::vector<void*> reg;
+  reg.reserve(nin + nout);
+  auto unregister = [&] {
+    for (void* p : reg) (void)hipHostUnregister(p);
+  };
+  auto pin_row = [&](const void* p) -> bool {
+    if (hipHostRegister(const_cast<void*>(p), L * 4, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    reg.push_back(const_cast<void*>(p));
+    return true;
+  };
+  for (uint64_t j = 0; j < nin; ++j)
+    if (!pin_row(in[j])) return unregister(), -1;
+  for (uint64_t i = 0; i < nout; ++i)
+    if (!pin_row(out[i])) return unregister(), -1;
+  uint64_t cl = std::max<uint64_t>(4 * kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
+  if (cl >= L) cl = (L + 3) & ~3ull;
+  const uint64_t nch = (L + cl - 1) / cl;
+  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
+  const size_t stage_words = (size_t)(nin + nout) * cl;
+  int rc = ws->reserve(stage_words * 4 * S);
+  if (!rc) rc = ws->ensure_stages();
+  auto body = [&]() -> int {
+    uint32_t* const dev = (uint32_t*)ws->dbuf;
+    for (uint64_t c = 0; c < nch; ++c) {
+      const int s = (int)(c % S);
+      const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
+      uint32_t* di = dev + s * stage_words;
+      hipStream_t st = ws->sst[s];
+      for (uint64_t j = 0; j < nin; ++j)
+        HIP_TRY(hipMemcpyAsync(di + j * cl, in[j] + c0, n * 4, hipMemcpyHostToDevice, st));
+      if (int e = execute(plan, di, 0, cl, di + nin * cl, 0, cl, n, 1, st)) return e;
+      for (uint64_t i = 0; i < nout; ++i)
+        HIP_TRY(hipMemcpyAsync(out[i] + c0, di + (nin + i) * cl, n * 4, hipMemcpyDeviceToHost, st));
+    }
+    return 0;
+  };
+  if (!rc) rc = body();
+  for (int s = 0; s < S; ++s)
+    if (ws->sst[s] && hipStreamSynchronize(ws->sst[s]) != hipSuccess && !rc) rc = fail_hip(hipGetLastError(), "stage sync");
+  unregister();
+  return rc;
+}
+
+// out[i][0:L] = sum_j coeff[i][j] * in[j][0:L] for a plan whose inputs are
+// 0..k-1 and outputs 0..rows-1 (host memory on both sides).
+int host_apply(const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out, uint64_t L) {
+  WsLease lease;
+  if (int rc = acquire_ws(plan->device, &lease.ws)) return rc;
+  DeviceScope ds(plan->device);
+  switch (host_pipe_mode()) {
+    case HostPipe::Direct:
+      return host_apply_direct(lease.ws, plan, in, out, L);
+    case HostPipe::Register:
+      if (int rc = host_apply_registered(lease.ws, plan, in, out, L); rc != -1) return rc;
+      [[fallthrough]];
+    case HostPipe::Staged:
+    default:
+      return host_apply_staged(lease.ws, plan, in, out, L);
+  }
+}
 
 // ---- MapToGF fallback candidates (the reference's rand.Uint32() stream) ------
 
@@ -276,6 +483,13 @@ const char* slime_rs_status_string(int status) { return status_text(status); }
 const char* slime_rs_last_error(void) { return t_error.c_str(); }
 const char* slime_rs_version(void) { return "slime_rs 0.1 (gfx950, GF(2^32-5))"; }
 int slime_rs_device_count(void) { return visible_devices(); }
+
+int slime_rs_host_pipeline(int mode) {
+  if (mode < 0) return g_host_pipe.load();
+  if (mode > 2) return fail(Status::InvalidArg, "host_pipeline: mode must be 0 (staged), 1 (register) or 2 (direct)");
+  g_host_pipe.store(mode);
+  return 0;
+}
 
 int slime_rs_select_device(int device) {
   if (int rc = check_device(device)) return rc;
@@ -611,21 +825,7 @@ static int run_rows(int need, const std::vector<int>& rows, const uint32_t* cons
   if (int rc = check_device(dev)) return rc;
   slime_rs_plan* plan = nullptr;
   if (int rc = cached_plan(PlanKey{dev, 'P', need, 0, rows}, &plan, make_rows_plan)) return rc;
-  WsLease lease;
-  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
-  Workspace* ws = lease.ws;
-  DeviceScope ds(dev);
-  const size_t shard = round16(L * 4) / 4;  // keep every shard 16-byte aligned
-  if (int rc = ws->reserve(shard * 4 * ((size_t)need + rows.size()))) return rc;
-  uint32_t* d_in = (uint32_t*)ws->dbuf;
-  uint32_t* d_out = d_in + shard * need;
-  for (int j = 0; j < need; ++j)
-    HIP_TRY(hipMemcpyAsync(d_in + shard * j, data[j], L * 4, hipMemcpyHostToDevice, ws->stream));
-  if (int rc = execute(plan, d_in, 0, shard, d_out, 0, shard, L, 1, ws->stream)) return rc;
-  for (size_t i = 0; i < rows.size(); ++i)
-    HIP_TRY(hipMemcpyAsync(out[i], d_out + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
-  return 0;
+  return host_apply(plan, data, out, L);
 }
 
 int slime_rs_create_parity(const uint32_t* const* data, const uint64_t* lens, int ndata, int index, uint32_t* out) {
@@ -661,29 +861,20 @@ int slime_rs_create_parities(const uint32_t* const* data, const uint64_t* lens, 
 }
 
 static int make_recover_plan(const PlanKey& key, slime_rs_plan** out) {
-  // kind 'R': erased data rows of a need-row recovery from survivors `have`.
+  // kind 'R': all need data rows of the inverse of the survivors' code rows
+  // (vector.go RecoverData applies the whole inverse; surviving data rows are
+  // its unit rows, i.e. x mod p).  The staged chunks sit at inputs 0..need-1.
   const int dev = std::get<0>(key), need = std::get<2>(key);
   const std::vector<int>& have = std::get<4>(key);
-  std::vector<char> present(need, 0);
-  for (int h : have)
-    if (h < need) present[h] = 1;
-  std::vector<int> want;
-  for (int t = 0; t < need; ++t)
-    if (!present[t]) want.push_back(t);
-  if (want.empty()) {
-    *out = nullptr;  // nothing to compute: every data row survived
-    return 0;
-  }
-  // `have` indexes code rows; the staged chunk buffer holds them at 0..need-1.
   const int total = std::max(need, *std::max_element(have.begin(), have.end()) + 1);
+  std::vector<int> want(need);
+  for (int t = 0; t < need; ++t) want[t] = t;
   slime_rs_plan* tmp = nullptr;
-  if (int rc = slime_rs_plan_reconstruct(dev, need, total, have.data(), want.data(), (int)want.size(), &tmp))
-    return rc;
-  // Re-point inputs at the staged positions 0..need-1 (plan tables are ours).
+  if (int rc = slime_rs_plan_reconstruct(dev, need, total, have.data(), want.data(), need, &tmp)) return rc;
   std::vector<int> pos(need);
   for (int q = 0; q < need; ++q) pos[q] = q;
   slime_rs_plan* staged = nullptr;
-  const int rc = slime_rs_plan_matrix(dev, tmp->coeff.data(), (int)tmp->rows, need, pos.data(), &staged);
+  const int rc = slime_rs_plan_matrix(dev, tmp->coeff.data(), need, need, pos.data(), &staged);
   destroy_plan(tmp);
   if (rc) return rc;
   *out = staged;
@@ -729,38 +920,7 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   std::vector<int> have(indices, indices + nindices);
   slime_rs_plan* plan = nullptr;
   if (int rc = cached_plan(PlanKey{dev, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
-
-  // Surviving data rows are unit rows of the inverse (x mod p); the erased
-  // ones come from the plan, in ascending row order.
-  std::vector<int> slot_of(need, -1);
-  for (int q = 0; q < need; ++q)
-    if (indices[q] < need) slot_of[indices[q]] = q;
-  std::vector<int> erased;
-  for (int t = 0; t < need; ++t)
-    if (slot_of[t] < 0) erased.push_back(t);
-
-  WsLease lease;
-  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
-  Workspace* ws = lease.ws;
-  DeviceScope ds(dev);
-  const size_t shard = round16(L * 4) / 4;  // every staged shard 16-byte aligned
-  if (int rc = ws->reserve(shard * 4 * ((size_t)need * 2 + erased.size()))) return rc;
-  uint32_t* d_in = (uint32_t*)ws->dbuf;      // need staged chunks
-  uint32_t* d_copy = d_in + shard * need;    // canonical copies of surviving data rows
-  uint32_t* d_rec = d_copy + shard * need;   // recovered rows, erased order
-  for (int q = 0; q < need; ++q)
-    HIP_TRY(hipMemcpyAsync(d_in + shard * q, chunks[q], L * 4, hipMemcpyHostToDevice, ws->stream));
-  for (int t = 0; t < need; ++t)
-    if (slot_of[t] >= 0) HIP_TRY(launch_canon_copy(d_in + shard * slot_of[t], d_copy + shard * t, L, ws->stream));
-  if (plan && (int)plan->rows != (int)erased.size()) return fail(Status::InvalidArg, "RecoverData: plan mismatch");
-  if (plan)
-    if (int rc = execute(plan, d_in, 0, shard, d_rec, 0, shard, L, 1, ws->stream)) return rc;
-  for (size_t i = 0; i < erased.size(); ++i)
-    HIP_TRY(hipMemcpyAsync(out[erased[i]], d_rec + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
-  for (int t = 0; t < need; ++t)
-    if (slot_of[t] >= 0) HIP_TRY(hipMemcpyAsync(out[t], d_copy + shard * t, L * 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
-  return 0;
+  return host_apply(plan, chunks, out, L);
 }
 
 // ---- gf codec (host memory) -----------------------------------------------------------

@@ -103,20 +103,37 @@ def CreateParity(data: Sequence, index: int, out=None) -> np.ndarray:
     return res
 
 
-def CreateParities(data: Sequence, total: int) -> list[np.ndarray]:
+def _outs(outs, n: int, L: int) -> list[np.ndarray]:
+    """Caller-supplied result rows (uint32, contiguous, >= L symbols) are
+    written in place and returned as [:L] views; otherwise fresh rows."""
+    if outs is None:
+        return [np.zeros(L, dtype=np.uint32) for _ in range(n)]
+    if len(outs) != n:
+        raise ValueError(f"expected {n} output rows, got {len(outs)}")
+    res = []
+    for o in outs:
+        if not (isinstance(o, np.ndarray) and o.dtype == np.uint32 and o.flags.c_contiguous
+                and o.flags.writeable and o.size >= L):
+            raise ValueError("output rows must be writeable contiguous uint32 arrays of at least L symbols")
+        res.append(o[:L])
+    return res
+
+
+def CreateParities(data: Sequence, total: int, outs: Sequence[np.ndarray] | None = None) -> list[np.ndarray]:
     """All total-len(data) parity rows in one GPU pass (batched multi_store.go:528-531)."""
     arrays = [_vec(d) for d in data]
     L = arrays[0].size if arrays else 0
-    outs = [np.zeros(L, dtype=np.uint32) for _ in range(max(total - len(arrays), 0))]
+    outs = _outs(outs, max(total - len(arrays), 0), L)
     N.check(lib.slime_rs_create_parities(_ptrs(arrays), _lens(arrays), len(arrays), total, _ptrs(outs)))
     return outs
 
 
-def RecoverData(chunks: Sequence, indices: Sequence[int]) -> list[np.ndarray]:
+def RecoverData(chunks: Sequence, indices: Sequence[int],
+                outs: Sequence[np.ndarray] | None = None) -> list[np.ndarray]:
     """internal/rs/vector.go:50 — all len(chunks) data rows from any len(chunks) code rows."""
     arrays = [_vec(c) for c in chunks]
     idx = (ctypes.c_int * max(len(indices), 1))(*[int(i) for i in indices])
     L = arrays[0].size if arrays else 0
-    outs = [np.zeros(L, dtype=np.uint32) for _ in arrays]
+    outs = _outs(outs, len(arrays), L)
     N.check(lib.slime_rs_recover_data(_ptrs(arrays), _lens(arrays), len(arrays), idx, len(indices), _ptrs(outs)))
     return outs

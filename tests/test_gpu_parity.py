@@ -124,6 +124,66 @@ def test_recover_data_ragged_longer_chunks():
     assert all(g.size == 8 for g in got)
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["staged", "register", "direct"])
+def host_mode(request):
+    prev = N.lib.slime_rs_host_pipeline(-1)
+    N.check(N.lib.slime_rs_host_pipeline(request.param))
+    yield request.param
+    N.check(N.lib.slime_rs_host_pipeline(prev))
+
+
+@pytest.mark.parametrize("need,total,L", [(8, 12, 700001), (4, 6, 3 * 262144 + 5), (16, 20, 500003), (8, 12, 4099)])
+def test_host_pipeline_multi_chunk(host_mode, need, total, L):
+    # The Go-API entry points stream host buffers through a 3-deep ring of
+    # ~8 MiB stages: these sizes span >3 chunks with a ragged last chunk.
+    rng = np.random.default_rng(L)
+    data = rand_vecs(rng, need, L)
+    par = rs.CreateParities(data, total)
+    for i, row in enumerate(par):
+        assert np.array_equal(row, OC.create_parity(data, need + i)[1]), i
+    code = [OC.create_parity(data, t)[1] for t in range(total)]  # canonical data rows via identity rows
+    have = list(range(total - need, total))[::-1]
+    got = rs.RecoverData([code[i] for i in have], have)
+    rc, want = OC.recover_data([code[i] for i in have], have)
+    assert rc == 0
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+
+
+def test_host_pipeline_read_only_and_shared_inputs(host_mode):
+    # Read-only rows (np.frombuffer of bytes) and one row passed twice: page
+    # registration may be refused; the result must not change.
+    need, total, L = 4, 7, 300007
+    rng = np.random.default_rng(5)
+    base = rand_vecs(rng, need, L)
+    data = [np.frombuffer(base[0].tobytes(), dtype=np.uint32), base[1], base[1], base[3]]
+    assert not data[0].flags.writeable
+    par = rs.CreateParities(data, total)
+    for i, row in enumerate(par):
+        assert np.array_equal(row, OC.create_parity([np.array(d) for d in data], need + i)[1])
+
+
+def test_host_pipeline_mode_knob():
+    prev = N.lib.slime_rs_host_pipeline(-1)
+    assert prev in (0, 1, 2)
+    with pytest.raises(N.NativeError):
+        N.check(N.lib.slime_rs_host_pipeline(3))
+    assert N.lib.slime_rs_host_pipeline(-1) == prev
+
+
+def test_host_pipeline_concurrent_callers(host_mode):
+    # Several host threads share the workspace pool and the copy pool.
+    import concurrent.futures as cf
+    need, total, L = 8, 12, 400009
+    rng = np.random.default_rng(9)
+    jobs = [rand_vecs(rng, need, L) for _ in range(6)]
+    with cf.ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(lambda d: rs.CreateParities(d, total), jobs))
+    for d, par in zip(jobs, outs):
+        for i, row in enumerate(par):
+            assert np.array_equal(row, OC.create_parity(d, need + i)[1])
+
+
 def test_map_kats_on_gpu(kats):
     for case in kats["map_trivial"]:
         data = bytes(case["in"])

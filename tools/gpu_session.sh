@@ -106,6 +106,8 @@ if has sustained; then
   run smi 60 rocm-smi --showclocks --showperflevel --showpower
   run sustained2 300 python tools/sustained.py --seconds 8 --idle 0
 fi
+has hostpipe && run hostpipe 900 python tools/host_pipe.py
+has counters && run counters 120 rocprofv3 -L
 if has pmc; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0
