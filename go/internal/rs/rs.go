@@ -236,3 +236,74 @@ func invertMatrix(m [][]uint32) [][]uint32 {
 	raise(C.slime_rs_invert_matrix((*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(d), &inv[0]))
 	return matrixFromC(&inv[0], d, d)
 }
+
+// WriteChunks is the data path of Multi.writeChunks
+// (internal/store/multi/multi_store.go:526-531 and :554) in one GPU pass:
+// gf.MapToGF, splitVector, CreateParity for every parity row, gf.MapFromGF per
+// part.  It returns MappingValue and the total chunks as written to stores.
+// Not part of the reference's rs API: it lets writeChunks replace its
+// per-row CreateParity loop and per-part MapFromGF calls (see INTEGRATION.md).
+func WriteChunks(data []byte, need, total int) (uint32, [][]byte) {
+	cb := int(C.slime_rs_chunk_size(C.uint64_t(len(data)), C.int(need)))
+	chunks := make([][]byte, total)
+	ptrs := (**C.uint8_t)(C.calloc(C.size_t(total+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
+	defer C.free(unsafe.Pointer(ptrs))
+	ps := unsafe.Slice(ptrs, total+1)
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for i := range chunks {
+		chunks[i] = make([]byte, cb)
+		if cb > 0 {
+			pinner.Pin(&chunks[i][0])
+			ps[i] = (*C.uint8_t)(unsafe.Pointer(&chunks[i][0]))
+		}
+	}
+	var in *C.uint8_t
+	if len(data) > 0 {
+		pinner.Pin(&data[0])
+		in = (*C.uint8_t)(unsafe.Pointer(&data[0]))
+	}
+	var mapping C.uint32_t
+	raise(C.slime_rs_write_chunks(in, C.uint64_t(len(data)), C.int(need), C.int(total), ptrs, &mapping))
+	return uint32(mapping), chunks
+}
+
+// ReconstructObject is the slow path of Multi.reconstruct
+// (multi_store.go:215-241): from exactly need surviving chunks (equal length)
+// and their indices, gf.MapToGFWith + RecoverData + gf.MapFromGF, truncated to
+// size.  Panics as RecoverData does for bad indices.
+func ReconstructObject(chunks [][]byte, indices []int, mapping uint32, size int) []byte {
+	n := len(chunks)
+	if n != len(indices) {
+		panic("RecoverData: len(chunks) != len(indices)")
+	}
+	cb := 0
+	if n > 0 {
+		cb = len(chunks[0])
+	}
+	ptrs := (**C.uint8_t)(C.calloc(C.size_t(n+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
+	defer C.free(unsafe.Pointer(ptrs))
+	idx := (*C.int)(C.calloc(C.size_t(n+1), C.size_t(unsafe.Sizeof(C.int(0)))))
+	defer C.free(unsafe.Pointer(idx))
+	ps, is := unsafe.Slice(ptrs, n+1), unsafe.Slice(idx, n+1)
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for i, c := range chunks {
+		if len(c) < cb {
+			panic(fmt.Sprintf("runtime error: index out of range [%d] with length %d", len(c), len(c)))
+		}
+		if cb > 0 {
+			pinner.Pin(&c[0])
+			ps[i] = (*C.uint8_t)(unsafe.Pointer(&c[0]))
+		}
+		is[i] = C.int(indices[i])
+	}
+	out := make([]byte, size, size+16)
+	var op *C.uint8_t
+	if size > 0 {
+		pinner.Pin(&out[0])
+		op = (*C.uint8_t)(unsafe.Pointer(&out[0]))
+	}
+	raise(C.slime_rs_reconstruct(ptrs, idx, C.int(n), C.uint64_t(cb), C.uint32_t(mapping), C.uint64_t(size), op))
+	return out
+}

@@ -193,6 +193,33 @@ int slime_rs_resolve_fallbacks(slime_rs_plan_t encode_plan, uint8_t *slots, uint
 int slime_rs_decode_objects(slime_rs_plan_t reconstruct_plan, uint8_t *slots, uint64_t slot_stride, uint64_t L,
                             uint64_t nobj, const uint32_t *mapping, void *stream);
 
+/* ---- Object entry points over host memory (the callers' data paths) ----
+ *
+ * Byte length of every chunk of a `size`-byte object split `need` ways:
+ * 4 * ceil(ceil(size/4) / need)  (splitVector, multi_store.go:271-278). */
+uint64_t slime_rs_chunk_size(uint64_t size, int need);
+
+/* The data path of Multi.writeChunks (multi_store.go:526-531 and :554):
+ *   mapping, all := gf.MapToGF(data); parts := splitVector(all, need);
+ *   parity i := rs.CreateParity(parts, need+i, nil); chunk i := gf.MapFromGF(mapping, part i)
+ * in one device pass (fused byte kernels) with pinned, overlapped transfers.
+ * chunks[0..total-1] each receive slime_rs_chunk_size(size, need) bytes;
+ * *mapping receives MappingValue.  The random-mapping fallback draws from the
+ * library's stream (slime_gf_seed).  need must be 1..16 and total > need;
+ * size 0 gives mapping 0 and empty chunks.  Synchronous; thread-safe. */
+int slime_rs_write_chunks(const uint8_t *data, uint64_t size, int need, int total, uint8_t *const *chunks,
+                          uint32_t *mapping);
+
+/* The slow path of Multi.reconstruct (multi_store.go:215-241): the first
+ * `need` available chunks (chunk_bytes each, a multiple of 4) with their
+ * chunk indices, and the file's MappingValue -> the object's `size` bytes in
+ * out:  chunk := MapToGFWith(data, mapping); RecoverData(chunks, indices);
+ * MapFromGF each data row; data[:size].  Same panics as RecoverData for bad
+ * indices; need must be <= 16.  Bytes past need*chunk_bytes are zero, as
+ * in the reference's data[:Size] of a zeroed buffer.  Synchronous. */
+int slime_rs_reconstruct(const uint8_t *const *chunks, const int *indices, int need, uint64_t chunk_bytes,
+                         uint32_t mapping, uint64_t size, uint8_t *out);
+
 /* Device codec (internal/rs/gf/map.go) over device buffers, asynchronous on
  * `stream`.  pack: words[i] = BE(bytes[4i..4i+3]) ^ mapping (zero low bytes
  * in a partial last word); if flags != NULL it is OR-ed with bit0 = some

@@ -85,6 +85,12 @@ SIGNATURES = [
     ("slime_rs_decode_objects", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
       ctypes.c_void_p]),
+    ("slime_rs_chunk_size", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int]),
+    ("slime_rs_write_chunks", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, c_u32p]),
+    ("slime_rs_reconstruct", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+      ctypes.c_void_p]),
     ("slime_gf_pack_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_gf_unpack_device", ctypes.c_int,

@@ -193,6 +193,7 @@ struct Workspace {
   size_t dcap = 0;
   hipStream_t sst[kStages] = {};  // one stream per pipeline stage
   hipEvent_t sev[kStages] = {};   // stage's D2H done
+  hipEvent_t cev = nullptr;       // compute stream reached a point (staged_d2h)
   uint8_t* pin = nullptr;         // pinned staging, kStages x (in rows | out rows)
   size_t pcap = 0;
   int reserve(size_t bytes) {
@@ -228,6 +229,7 @@ struct Workspace {
       HIP_TRY(hipStreamCreateWithFlags(&sst[i], hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming));
     }
+    HIP_TRY(hipEventCreateWithFlags(&cev, hipEventDisableTiming));
     return 0;
   }
 };
@@ -423,6 +425,83 @@ int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32
     if (ws->sst[s] && hipStreamSynchronize(ws->sst[s]) != hipSuccess && !rc) rc = fail_hip(hipGetLastError(), "stage sync");
   unregister();
   return rc;
+}
+
+// ---- staged whole-buffer transfers (object entry points) -------------------------
+//
+// A span is a host range and its device offset.  Spans are cut into pieces
+// of at most kStageBytes; piece p goes through pinned stage p % S, so the host
+// memcpy of one piece overlaps the DMA of the previous ones.
+
+struct Span {
+  uint8_t* host;
+  uint64_t dev_off;
+  uint64_t bytes;
+};
+
+std::vector<Span> pieces_of(const Span* sp, size_t n) {
+  std::vector<Span> out;
+  for (size_t i = 0; i < n; ++i)
+    for (uint64_t off = 0; off < sp[i].bytes; off += kStageBytes)
+      out.push_back({sp[i].host + off, sp[i].dev_off + off, std::min<uint64_t>(kStageBytes, sp[i].bytes - off)});
+  return out;
+}
+
+int stage_ring(Workspace* ws) {
+  if (int rc = ws->reserve_pinned(kStageBytes * Workspace::kStages)) return rc;
+  return ws->ensure_stages();
+}
+
+// Host spans -> dev; ws->stream waits for every piece before its next launch.
+int staged_h2d(Workspace* ws, uint8_t* dev, const Span* sp, size_t n) {
+  if (int rc = stage_ring(ws)) return rc;
+  const std::vector<Span> pcs = pieces_of(sp, n);
+  const int S = Workspace::kStages;
+  for (size_t p = 0; p < pcs.size(); ++p) {
+    const int s = (int)(p % S);
+    uint8_t* pin = ws->pin + (size_t)s * kStageBytes;
+    if (p >= (size_t)S) HIP_TRY(hipEventSynchronize(ws->sev[s]));  // stage buffer free again
+    const CopyItem it{pin, pcs[p].host, pcs[p].bytes};
+    parallel_copy(&it, 1);
+    HIP_TRY(hipMemcpyAsync(dev + pcs[p].dev_off, pin, pcs[p].bytes, hipMemcpyHostToDevice, ws->sst[s]));
+    HIP_TRY(hipEventRecord(ws->sev[s], ws->sst[s]));
+  }
+  for (int s = 0; s < S && (size_t)s < pcs.size(); ++s) HIP_TRY(hipStreamWaitEvent(ws->stream, ws->sev[s], 0));
+  return 0;
+}
+
+// dev -> host spans after everything queued on ws->stream so far; returns
+// when the host copies are complete.
+int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
+  if (int rc = stage_ring(ws)) return rc;
+  const std::vector<Span> pcs = pieces_of(sp, n);
+  const int S = Workspace::kStages;
+  HIP_TRY(hipEventRecord(ws->cev, ws->stream));
+  for (int s = 0; s < S; ++s) HIP_TRY(hipStreamWaitEvent(ws->sst[s], ws->cev, 0));
+  auto land = [&](size_t p) -> int {
+    const int s = (int)(p % S);
+    HIP_TRY(hipEventSynchronize(ws->sev[s]));
+    const CopyItem it{pcs[p].host, ws->pin + (size_t)s * kStageBytes, pcs[p].bytes};
+    parallel_copy(&it, 1);
+    return 0;
+  };
+  for (size_t p = 0; p < pcs.size(); ++p) {
+    const int s = (int)(p % S);
+    if (p >= (size_t)S)
+      if (int rc = land(p - S)) return rc;
+    HIP_TRY(hipMemcpyAsync(ws->pin + (size_t)s * kStageBytes, dev + pcs[p].dev_off, pcs[p].bytes,
+                           hipMemcpyDeviceToHost, ws->sst[s]));
+    HIP_TRY(hipEventRecord(ws->sev[s], ws->sst[s]));
+  }
+  for (size_t p = pcs.size() > (size_t)S ? pcs.size() - S : 0; p < pcs.size(); ++p)
+    if (int rc = land(p)) return rc;
+  return 0;
+}
+
+void drain_stages(Workspace* ws) {
+  if (ws->stream) (void)hipStreamSynchronize(ws->stream);
+  for (hipStream_t st : ws->sst)
+    if (st) (void)hipStreamSynchronize(st);
 }
 
 // out[i][0:L] = sum_j coeff[i][j] * in[j][0:L] for a plan whose inputs are
@@ -881,30 +960,34 @@ static int make_recover_plan(const PlanKey& key, slime_rs_plan** out) {
   return 0;
 }
 
+// RecoverData's index checks (vector.go:65-77): no non-negative index ->
+// "No indices given"; a negative index -> Go's index-out-of-range; duplicate
+// or otherwise dependent rows -> invertMatrix's panic.
+static int check_survivors(int need, const int* indices) {
+  int max_index = -1;
+  for (int i = 0; i < need; ++i) max_index = std::max(max_index, indices[i]);
+  if (max_index == -1) return status_of(Status::NoIndices, "RecoverData");
+  for (int i = 0; i < need; ++i)
+    if (indices[i] < 0)
+      return fail(Status::IndexRange, "runtime error: index out of range [" + std::to_string(indices[i]) + "]");
+  Matrix hv((size_t)need, (size_t)need), inv;
+  std::vector<uint32_t> row;
+  for (int i = 0; i < need; ++i) {
+    if (Status st = code_row(need, indices[i], &row); st != Status::Ok) return status_of(st, "ParityMatrixCached");
+    std::copy(row.begin(), row.end(), hv.v.begin() + (size_t)i * need);
+  }
+  if (Status st = invert(hv, &inv); st != Status::Ok) return status_of(st, "RecoverData");
+  return 0;
+}
+
 int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, int nchunks, const int* indices,
                           int nindices, uint32_t* const* out) {
   if (nchunks < 0 || nindices < 0) return fail(Status::InvalidArg, "RecoverData: negative count");
   if (nchunks != nindices) return status_of(Status::LenMismatch, "RecoverData");
   if (nchunks == 0) return status_of(Status::Empty, "RecoverData");
   if (!chunks || !lens || !indices) return fail(Status::InvalidArg, "RecoverData: bad args");
-  int max_index = -1;
-  for (int i = 0; i < nindices; ++i) max_index = std::max(max_index, indices[i]);
-  if (max_index == -1) return status_of(Status::NoIndices, "RecoverData");
+  if (int rc = check_survivors(nchunks, indices)) return rc;
   const int need = nchunks;
-  for (int i = 0; i < nindices; ++i)
-    if (indices[i] < 0)
-      return fail(Status::IndexRange, "runtime error: index out of range [" + std::to_string(indices[i]) + "]");
-  // ParityMatrixCached(len(chunks), maxIndex) + invertMatrix(have): same
-  // failure conditions as the reference (duplicate rows -> singular).
-  {
-    Matrix hv((size_t)need, (size_t)need), inv;
-    std::vector<uint32_t> row;
-    for (int i = 0; i < need; ++i) {
-      if (Status st = code_row(need, indices[i], &row); st != Status::Ok) return status_of(st, "ParityMatrixCached");
-      std::copy(row.begin(), row.end(), hv.v.begin() + (size_t)i * need);
-    }
-    if (Status st = invert(hv, &inv); st != Status::Ok) return status_of(st, "RecoverData");
-  }
   const uint64_t L = lens[0];
   for (int i = 1; i < need; ++i)
     if (lens[i] < L)
@@ -921,6 +1004,133 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   slime_rs_plan* plan = nullptr;
   if (int rc = cached_plan(PlanKey{dev, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
   return host_apply(plan, chunks, out, L);
+}
+
+// ---- object entry points (host memory): writeChunks / reconstruct ------------------
+
+static int make_encode_plan(const PlanKey& key, slime_rs_plan** out) {
+  return slime_rs_plan_encode(std::get<0>(key), std::get<2>(key), std::get<3>(key), out);
+}
+
+static int make_object_recover_plan(const PlanKey& key, slime_rs_plan** out) {
+  // All need data rows of the inverse, inputs = staged survivors 0..need-1,
+  // outputs = chunk positions need..2need-1 (the rebuilt object, in order).
+  if (int rc = make_recover_plan(key, out)) return rc;
+  const int need = std::get<2>(key);
+  std::vector<int> pos(need);
+  for (int t = 0; t < need; ++t) pos[t] = need + t;
+  if (int rc = slime_rs_plan_set_outputs(*out, pos.data())) {
+    destroy_plan(*out);
+    *out = nullptr;
+    return rc;
+  }
+  return 0;
+}
+
+uint64_t slime_rs_chunk_size(uint64_t size, int need) { return need > 0 ? 4 * slot_L(size, (uint32_t)need) : 0; }
+
+int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
+                          uint32_t* mapping) {
+  if (!mapping) return fail(Status::InvalidArg, "write_chunks: null mapping");
+  *mapping = 0;
+  if (need < 1 || need > 16 || total <= need)
+    return fail(Status::InvalidArg, "write_chunks: need must be 1..16 and total > need");
+  const uint64_t L = slot_L(size, (uint32_t)need);
+  if (L == 0) return 0;  // MapToGF(empty) = (0, []): every chunk is empty
+  if (!data || !chunks) return fail(Status::InvalidArg, "write_chunks: null buffer");
+  for (int i = 0; i < total; ++i)
+    if (!chunks[i]) return fail(Status::InvalidArg, "write_chunks: null chunk buffer");
+  const int dev = t_device;
+  if (int rc = check_device(dev)) return rc;
+  slime_rs_plan* plan = nullptr;
+  if (int rc = cached_plan(PlanKey{dev, 'E', need, total, {}}, &plan, make_encode_plan)) return rc;
+  WsLease lease;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  Workspace* ws = lease.ws;
+  DeviceScope ds(dev);
+  const uint64_t chunk = 4 * L, stride = (uint64_t)total * chunk;
+  if (int rc = ws->reserve(round16(stride) + 16)) return rc;
+  uint8_t* const slot = ws->dbuf;
+  uint32_t* const d_map = (uint32_t*)(ws->dbuf + round16(stride));
+  uint32_t* const d_status = d_map + 1;
+  auto body = [&]() -> int {
+    const Span in{const_cast<uint8_t*>(data), 0, size};
+    if (int rc = staged_h2d(ws, slot, &in, 1)) return rc;
+    if (int rc = slime_rs_encode_objects(plan, slot, stride, size, 1, d_map, d_status, ws->stream)) return rc;
+    // Below the object's last word a data chunk is the object's own bytes
+    // (MapFromGF(m, MapToGF(x)) = x, map.go:15-33,103-113): place them while
+    // the device encodes; the tail (partial word, padding) comes back from it.
+    std::vector<CopyItem> items;
+    for (int j = 0; j < need; ++j) {
+      const uint64_t lo = (uint64_t)j * chunk;
+      if (lo < size) items.push_back({chunks[j], data + lo, std::min(size, lo + chunk) - lo});
+    }
+    parallel_copy(items.data(), items.size());
+    uint32_t ms[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    if (ms[1] != 0) {  // MapToGF's random fallback (map.go:64-66)
+      if (int rc = slime_rs_resolve_fallbacks(plan, slot, stride, size, 1, d_map, d_status, ws->stream, nullptr))
+        return rc;
+      HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
+      HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    std::vector<Span> out;
+    for (int j = 0; j < need; ++j) {
+      const uint64_t lo = (uint64_t)j * chunk, start = std::max(size, lo);
+      if (start < lo + chunk) out.push_back({chunks[j] + (start - lo), start, lo + chunk - start});
+    }
+    for (int i = need; i < total; ++i) out.push_back({chunks[i], (uint64_t)i * chunk, chunk});
+    if (int rc = staged_d2h(ws, slot, out.data(), out.size())) return rc;
+    *mapping = ms[0];
+    return 0;
+  };
+  const int rc = body();
+  if (rc) drain_stages(ws);
+  return rc;
+}
+
+int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int need, uint64_t chunk_bytes,
+                         uint32_t mapping, uint64_t size, uint8_t* out) {
+  if (need < 0) return fail(Status::InvalidArg, "reconstruct: negative count");
+  if (need == 0) return status_of(Status::Empty, "RecoverData");
+  if (!chunks || !indices) return fail(Status::InvalidArg, "reconstruct: bad args");
+  if (int rc = check_survivors(need, indices)) return rc;
+  if (need > 16) return fail(Status::InvalidArg, "reconstruct: need must be <= 16");
+  if (chunk_bytes % 4) return fail(Status::InvalidArg, "reconstruct: chunk_bytes must be a multiple of 4");
+  if (size && !out) return fail(Status::InvalidArg, "reconstruct: null out");
+  const uint64_t L = chunk_bytes / 4, body_bytes = (uint64_t)need * chunk_bytes, got = std::min(size, body_bytes);
+  // data[:f.Size] of a make([]byte, 0, Size+16) buffer (multi_store.go:203,241):
+  // bytes past the recovered ones are the zeroed capacity.
+  if (size > got) memset(out + got, 0, size - got);
+  if (got == 0) return 0;
+  for (int q = 0; q < need; ++q)
+    if (!chunks[q]) return fail(Status::InvalidArg, "reconstruct: null chunk");
+  const int dev = t_device;
+  if (int rc = check_device(dev)) return rc;
+  std::vector<int> have(indices, indices + need);
+  slime_rs_plan* plan = nullptr;
+  if (int rc = cached_plan(PlanKey{dev, 'O', need, 0, have}, &plan, make_object_recover_plan)) return rc;
+  WsLease lease;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  Workspace* ws = lease.ws;
+  DeviceScope ds(dev);
+  const uint64_t stride = 2 * body_bytes;
+  if (int rc = ws->reserve(round16(stride) + 16)) return rc;
+  uint8_t* const slot = ws->dbuf;
+  uint32_t* const d_map = (uint32_t*)(ws->dbuf + round16(stride));
+  auto body = [&]() -> int {
+    HIP_TRY(hipMemcpyAsync(d_map, &mapping, 4, hipMemcpyHostToDevice, ws->stream));
+    std::vector<Span> in;
+    for (int q = 0; q < need; ++q) in.push_back({const_cast<uint8_t*>(chunks[q]), (uint64_t)q * chunk_bytes, chunk_bytes});
+    if (int rc = staged_h2d(ws, slot, in.data(), in.size())) return rc;
+    if (int rc = slime_rs_decode_objects(plan, slot, stride, L, 1, d_map, ws->stream)) return rc;
+    const Span o{out, body_bytes, got};
+    return staged_d2h(ws, slot, &o, 1);
+  };
+  const int rc = body();
+  if (rc) drain_stages(ws);
+  return rc;
 }
 
 // ---- gf codec (host memory) -----------------------------------------------------------

@@ -1,0 +1,74 @@
+"""Object-level data paths of slime's multi store over the MI355X C-ABI.
+
+``write_chunks`` is the data path of ``Multi.writeChunks``
+(internal/store/multi/multi_store.go:526-531, :554): MapToGF, splitVector,
+one CreateParity per parity row, MapFromGF per part.  ``reconstruct`` is the
+slow path of ``Multi.reconstruct`` (multi_store.go:215-241): MapToGFWith per
+surviving chunk, RecoverData, MapFromGF, truncation to the object size.  Both
+run on the GPU in one fused pass; storage, metadata and hashing stay with the
+caller, as in the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from . import _native as N
+
+lib = N.lib
+
+
+def chunk_size(size: int, need: int) -> int:
+    """Bytes per chunk: 4 * ceil(ceil(size/4) / need) (splitVector, multi_store.go:271-278)."""
+    return int(lib.slime_rs_chunk_size(size, need))
+
+
+def _bytes_view(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(data), dtype=np.uint8)
+
+
+def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None = None
+                 ) -> tuple[int, list[np.ndarray]]:
+    """(MappingValue, [total chunk byte arrays]) for an object, as writeChunks
+    stores them.  `out`: caller-owned uint8 chunk buffers (>= chunk_size bytes
+    each) written in place and returned as views."""
+    buf = _bytes_view(data)
+    cb = chunk_size(buf.size, need) if need > 0 else 0
+    if out is None:
+        chunks = [np.empty(cb, dtype=np.uint8) for _ in range(max(total, 0))]
+    else:
+        if len(out) != total or any(o.dtype != np.uint8 or not o.flags.c_contiguous or not o.flags.writeable
+                                    or o.size < cb for o in out):
+            raise ValueError("write_chunks: out must be `total` writeable contiguous uint8 arrays of chunk_size bytes")
+        chunks = [o[:cb] for o in out]
+    ptrs = (ctypes.c_void_p * max(len(chunks), 1))(*[c.ctypes.data for c in chunks])
+    m = ctypes.c_uint32(0)
+    N.check(lib.slime_rs_write_chunks(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
+                                      ctypes.byref(m)))
+    return int(m.value), chunks
+
+
+def reconstruct(chunks: Sequence, indices: Sequence[int], mapping: int, size: int,
+                out: np.ndarray | None = None) -> np.ndarray:
+    """The object's bytes (uint8 array) from `need` surviving chunks
+    (reconstruct's slow path).  `out`: caller-owned uint8 buffer of >= size bytes."""
+    arrs = [_bytes_view(c) for c in chunks]
+    cb = arrs[0].size if arrs else 0
+    if any(a.size != cb for a in arrs):
+        raise ValueError("reconstruct: chunks must have equal length")
+    ptrs = (ctypes.c_void_p * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+    idx = (ctypes.c_int * max(len(indices), 1))(*[int(i) for i in indices])
+    if len(indices) != len(arrs):
+        raise ValueError("reconstruct: one index per chunk")
+    if out is None:
+        out = np.empty(size, dtype=np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or not out.flags.writeable or out.size < size:
+        raise ValueError("reconstruct: out must be a writeable contiguous uint8 array of >= size bytes")
+    out = out[:size]
+    N.check(lib.slime_rs_reconstruct(ptrs, idx, len(arrs), cb, mapping & 0xFFFFFFFF, size,
+                                     out.ctypes.data if size else None))
+    return out

@@ -496,3 +496,96 @@ def test_decode_objects_repairs_chunks(torch_dev, need, total, S):
     h = slots.cpu().numpy()
     for o, obj in enumerate(objs):
         assert h[o * stride: o * stride + S].tobytes() == obj
+
+
+# ------------------------------------------------- object entry points (host memory)
+
+def _obj_bytes(rng, S, kind):
+    b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+    if kind == "high" and S >= 4:
+        b[0:4] = b"\xff\xff\xff\xff"  # mapping 1<<31 (map.go:47)
+    if kind == "fallback" and S >= 8:
+        b[0:8] = b"\xff\xff\xff\xff\x7f\xff\xff\xff"  # neither 0 nor 1<<31 (TestMapTricky)
+    return bytes(b)
+
+
+def _oracle_reconstruct(chunks, have, mapping, need, size):
+    """multi_store.go:215-241 via the oracle: MapToGFWith, RecoverData, MapFromGF, [:Size]."""
+    vecs = [OC.map_to_gf_with(bytes(c), mapping) for c in chunks]
+    rc, data = OC.recover_data(vecs, have)
+    assert rc == 0
+    out = b"".join(OC.map_from_gf(mapping, v) for v in data)
+    return (out + bytes(max(0, size - len(out))))[:size]
+
+
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (16, 20)])
+@pytest.mark.parametrize("S", [1, 3, 4, 5, 33, 4096, 100003, 3 * (8 << 20) + 13])
+@pytest.mark.parametrize("kind", ["plain", "high", "fallback"])
+def test_write_chunks_and_reconstruct_vs_oracle(need, total, S, kind):
+    # Objects of 3 x 8 MiB + 13 span several pinned ring stages each way.
+    from slime_amd import objects
+    rng = np.random.default_rng(S * 31 + need)
+    obj = _obj_bytes(rng, S, kind)
+    m, chunks = objects.write_chunks(obj, need, total)
+    if kind == "plain":
+        assert m in (0, 1 << 31)
+    if kind == "high" and S >= 4:
+        assert m == 1 << 31
+    # the reference's chunks for the mapping it would pick (the random draw is the library's)
+    m_ref, want = _oracle_chunks(obj, need, total, [m] if kind == "fallback" and S >= 8 else [])
+    assert m == m_ref
+    assert [c.tobytes() for c in chunks] == want
+    # reconstruct from the last `need` chunks, and from a mixed set
+    for have in (list(range(total - need, total)), sorted(rng.choice(total, size=need, replace=False).tolist())):
+        got = objects.reconstruct([chunks[i] for i in have], have, m, S)
+        assert got.tobytes() == obj
+    assert objects.reconstruct([chunks[i] for i in have], have, m, S).tobytes() == \
+        _oracle_reconstruct([chunks[i] for i in have], have, m, need, S)
+
+
+def test_reconstruct_every_pattern_4_6():
+    from slime_amd import objects
+    rng = np.random.default_rng(46)
+    S = 77777
+    obj = _obj_bytes(rng, S, "high")
+    m, chunks = objects.write_chunks(obj, 4, 6)
+    for have in itertools.combinations(range(6), 4):
+        assert objects.reconstruct([chunks[i] for i in have], list(have), m, S).tobytes() == obj
+
+
+def test_reconstruct_corrupt_noncanonical_survivor_matches_reference():
+    # A surviving data chunk whose words unmap to values >= p: the reference
+    # reduces them mod p (RecoverData applies unit rows); so must we.
+    from slime_amd import objects
+    need, total, S = 4, 6, 4000
+    rng = np.random.default_rng(7)
+    obj = _obj_bytes(rng, S, "plain")
+    m, chunks = objects.write_chunks(obj, need, total)
+    bad = chunks[1].copy()
+    bad[0:8] = np.frombuffer(b"\xff\xff\xff\xff\xff\xff\xff\xfb", dtype=np.uint8)
+    assert m == 0  # so the corrupt words unmap to 0xFFFFFFFF and 0xFFFFFFFB, both >= p
+    have = [0, 1, 4, 5]
+    surv = [chunks[0], bad, chunks[4], chunks[5]]
+    assert objects.reconstruct(surv, have, m, S).tobytes() == _oracle_reconstruct(surv, have, m, need, S)
+
+
+def test_reconstruct_size_past_chunks_is_zero_padded():
+    from slime_amd import objects
+    m, chunks = objects.write_chunks(b"abcdefgh" * 3, 2, 3)
+    got = objects.reconstruct([chunks[1], chunks[2]], [1, 2], m, 40).tobytes()
+    assert got[:24] == b"abcdefgh" * 3 and got[24:] == bytes(16)
+
+
+def test_object_entry_points_reuse_caller_buffers():
+    from slime_amd import objects
+    rng = np.random.default_rng(3)
+    obj = rng.integers(0, 256, size=123457, dtype=np.uint8).tobytes()
+    cb = objects.chunk_size(len(obj), 4)
+    bufs = [np.full(cb + 9, 0xAB, dtype=np.uint8) for _ in range(6)]
+    m, chunks = objects.write_chunks(obj, 4, 6, out=bufs)
+    assert all(c.ctypes.data == b.ctypes.data for c, b in zip(chunks, bufs))
+    assert all((b[cb:] == 0xAB).all() for b in bufs)
+    assert [c.tobytes() for c in chunks] == _oracle_chunks(obj, 4, 6)[1]
+    dst = np.full(len(obj) + 5, 0xCD, dtype=np.uint8)
+    got = objects.reconstruct([chunks[i] for i in (1, 3, 4, 5)], [1, 3, 4, 5], m, len(obj), out=dst)
+    assert got.ctypes.data == dst.ctypes.data and got.tobytes() == obj and (dst[len(obj):] == 0xCD).all()

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import slime_amd
+from slime_amd import objects
 from slime_amd import _native as N
 from slime_amd import gf, rs
 from oracle import oracle_c as OC
@@ -135,6 +136,32 @@ def test_compute_without_device_fails_loudly():
         gf.MapToGF(b"abcd")
     h = ctypes.c_void_p()
     assert N.lib.slime_rs_plan_encode(0, 8, 12, ctypes.byref(h)) == N.ERR_NO_DEVICE
+    with pytest.raises(slime_amd.NativeError) as e:
+        objects.write_chunks(b"x" * 100, 4, 6)
+    assert e.value.code == N.ERR_NO_DEVICE
+    with pytest.raises(slime_amd.NativeError) as e:
+        objects.reconstruct([b"\0" * 8, b"\0" * 8], [0, 2], 0, 16)
+    assert e.value.code == N.ERR_NO_DEVICE
+
+
+def test_object_chunk_size_is_split_vector_length():
+    # splitVector: L = ceil(len(all)/count), len(all) = ceil(S/4) (multi_store.go:272, map.go:16)
+    for S in [0, 1, 3, 4, 5, 31, 32, 33, 1000, 1 << 20, (256 << 20) + 7]:
+        for need in [1, 2, 3, 8, 10, 16]:
+            assert objects.chunk_size(S, need) == 4 * (-(-(-(-S // 4)) // need))
+
+
+def test_object_entry_points_validate_like_reference():
+    with pytest.raises(slime_amd.Panic) as e:  # RecoverData(chunks[:0], ...)
+        objects.reconstruct([], [], 0, 10)
+    assert "len(chunks) == 0" in str(e.value)
+    with pytest.raises(slime_amd.Panic) as e:  # duplicate survivors -> singular
+        objects.reconstruct([b"\0" * 8, b"\0" * 8], [1, 1], 0, 16)
+    assert "Couldn't ensure" in str(e.value)
+    with pytest.raises(slime_amd.NativeError):
+        objects.write_chunks(b"abc", 4, 4)  # total must exceed need
+    m, chunks = objects.write_chunks(b"", 4, 6)
+    assert m == 0 and all(c.size == 0 for c in chunks)
 
 
 def test_status_strings_are_reference_panics():

@@ -108,6 +108,21 @@ if has sustained; then
 fi
 has hostpipe && run hostpipe 900 python tools/host_pipe.py
 has counters && run counters 120 rocprofv3 -L
+if has pmcplace; then  # counters that may separate the fast/slow placement modes
+  run place_plain 300 python tools/placement_pmc.py
+  i=0
+  for set in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum" \
+             "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum" \
+             "TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum" \
+             "TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_WRREQ_sum" \
+             "TCC_EA0_WRREQ_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum" \
+             "TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum" \
+             "TCC_EA0_RDREQ_GMI_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum"; do
+    i=$((i+1))
+    run place_pmc$i 300 rocprofv3 --pmc $set --kernel-trace -d "$OUT/place_pmc$i" -o run --output-format csv -- \
+      python3 tools/placement_pmc.py
+  done
+fi
 if has pmc; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o bench --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0

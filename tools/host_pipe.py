@@ -80,6 +80,23 @@ def one(sizes_mib, reps):
         res[f"{mib}MiB"] = {"encode_GiBps": round(obj / enc / GIB, 2),
                             "encode_fresh_out_GiBps": round(obj / enc_fresh / GIB, 2),
                             "recover_GiBps": round(obj / dec / GIB, 2)}
+        # object entry points: writeChunks / reconstruct data paths (bytes in, bytes out)
+        from slime_amd import objects
+        raw = rng.integers(0, 256, size=mib << 20, dtype=np.uint8).tobytes()
+        box = {}
+
+        cbufs = [np.zeros(objects.chunk_size(len(raw), need), dtype=np.uint8) for _ in range(total)]
+        obuf = np.zeros(len(raw), dtype=np.uint8)
+
+        def wc():
+            box["w"] = objects.write_chunks(raw, need, total, out=cbufs)
+        wct = med(wc)  # caller-reused chunk buffers (steady state of a store's buffer pool)
+        m, chunks = box["w"]
+        surv = [chunks[i] for i in have]
+        rct = med(lambda: objects.reconstruct(surv, have, m, len(raw), out=obuf))
+        assert obuf.tobytes() == raw
+        res[f"{mib}MiB"].update({"write_chunks_GiBps": round(len(raw) / wct / GIB, 2),
+                                 "reconstruct_GiBps": round(len(raw) / rct / GIB, 2), "mapping": m})
     return res
 
 
