@@ -52,3 +52,9 @@ bytesvar: tools/libbytesvar.so
 tools/libbytesvar.so: tools/bytes_variants.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: bytesvar
+
+# Hash throughput probe for §8(f3) (tools only): make hashprobe
+hashprobe: tools/libhashprobe.so
+tools/libhashprobe.so: tools/hash_probe.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: hashprobe

@@ -108,6 +108,7 @@ if has sustained; then
 fi
 has hostpipe && run hostpipe 900 python tools/host_pipe.py
 has counters && run counters 120 rocprofv3 -L
+has hashprobe && run hashprobe 600 bash -c "make hashprobe >/dev/null && python tools/hash_probe.py"
 if has pmcplace; then  # counters that may separate the fast/slow placement modes
   run place_plain 300 python tools/placement_pmc.py
   i=0
