@@ -20,7 +20,8 @@ import torch  # noqa: E402  (owns the HIP runtime; load before our .so)
 lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libubench.so"))
 V, U64, U32, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
 for name, args in {
-    "ub_copy": [V, V, U64, U32, I], "ub_read": [V, V, U64, U32, I], "ub_write": [V, U64, U32, I],
+    "ub_copy": [V, V, U64, U32, I], "ub_read": [V, V, U64, U32, I], "ub_read_nt": [V, V, U64, U32, I],
+    "ub_read_glds": [V, V, U64, U32, I, I], "ub_write": [V, U64, U32, I],
     "ub_pattern8": [V, V, U64, U64, U64, U64, U64, U32, U32, U32, I],
     "ub_compute8": [V, V, U64, U32, U32, I], "ub_mad": [V, U64, U32, I],
 }.items():
@@ -46,6 +47,9 @@ def main():
     for grid in (2048, 8192, 32768):
         out[f"copy_grid{grid}"] = gbps(2 * n * 16, lib.ub_copy(a.data_ptr(), b.data_ptr(), n, grid, 5))
         out[f"read_grid{grid}"] = gbps(n * 16, lib.ub_read(a.data_ptr(), b.data_ptr(), n, grid, 5))
+        out[f"read_nt_grid{grid}"] = gbps(n * 16, lib.ub_read_nt(a.data_ptr(), b.data_ptr(), n, grid, 5))
+        out[f"read_glds_grid{grid}"] = gbps(n * 16, lib.ub_read_glds(a.data_ptr(), b.data_ptr(), n, grid, 0, 5))
+        out[f"read_glds_nt_grid{grid}"] = gbps(n * 16, lib.ub_read_glds(a.data_ptr(), b.data_ptr(), n, grid, 1, 5))
         out[f"write_grid{grid}"] = gbps(n * 16, lib.ub_write(b.data_ptr(), n, grid, 5))
     del a, b
     torch.cuda.empty_cache()
