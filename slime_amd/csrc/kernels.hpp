@@ -52,6 +52,8 @@ struct BytesLaunch {
   const uint32_t* out_idx;
   uint32_t* flags;  // encode: the caller's status array (flags, then fallback status)
   const uint32_t* mapping;
+  uint64_t col0 = 0;   // column window [col0, col0 + ncols) of every chunk; col0 % 4 == 0
+  uint64_t ncols = 0;  // 0: the whole chunk (L columns)
 };
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t stream);

@@ -33,13 +33,14 @@ hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
   // Phase 0 streams every object at once; phase 1 re-encodes the few objects
   // MapToGF maps with 1<<31 (~7.5% of 256 MiB random objects), so the whole
   // grid sweeps them one after another instead of 512/nobj blocks each.
-  const dim3 g = grid_for(a.L, a.phase == 0 ? a.nobj : 1);
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const dim3 g = grid_for(ncols, a.phase == 0 ? a.nobj : 1);
   if (a.phase == 0) {
-    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.S,
-                       a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                       ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
   } else {
-    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.S,
-                       a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                       ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
   }
   return hipGetLastError();
 }
@@ -47,8 +48,9 @@ hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
 template <int K>
 hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = bytes_unroll<K>();
-  hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(a.L, a.nobj), dim3(kBlock), 0, s, a.slots,
-                     a.slot_stride, a.L, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping);
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s, a.slots,
+                     a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping);
   return hipGetLastError();
 }
 
@@ -78,12 +80,14 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0) return hipSuccess;
+  if (a.col0 % 4 || a.col0 + a.ncols > a.L) return hipErrorInvalidValue;
   SLIME_K_SWITCH(enc_k)
 }
 
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0 || a.rows == 0) return hipSuccess;
+  if (a.col0 % 4 || a.col0 + a.ncols > a.L) return hipErrorInvalidValue;
   SLIME_K_SWITCH(dec_k)
 }
 

@@ -124,14 +124,16 @@ struct Flags {
   }
 };
 
-// Load the K data-chunk words of columns [b, b+ncol) as symbols (mapping m,
-// splitVector padding), folding the packed words into MapToGF's flags.
+// Load the K data-chunk words of window columns [b, b+ncol) as symbols
+// (mapping m, splitVector padding), folding the packed words into MapToGF's
+// flags.  `slot` points at the window (object slot + 4*col0); the object word
+// index of chunk j, window column b is j*L + col0 + b.
 // INTERIOR: every word of the unit is a full object word (the bulk of every
 // object) -- no padding/partial-word checks.
 template <int K, bool INTERIOR, bool FLAGS>
-__device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t b,
-                                                  int ncol, const ObjWords& ow, uint32_t m, uint32_t (&x)[K][4],
-                                                  Flags* fl) {
+__device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0,
+                                                  uint64_t b, int ncol, const ObjWords& ow, uint32_t m,
+                                                  uint32_t (&x)[K][4], Flags* fl) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const uint8_t* src = slot + (uint64_t)j * chunk + 4 * b;
@@ -150,7 +152,7 @@ __device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t 
         x[j][c] = p ^ m;
       }
     } else {
-      const uint64_t w0 = (uint64_t)j * L + b;
+      const uint64_t w0 = (uint64_t)j * L + col0 + b;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         bool pad;
@@ -165,11 +167,11 @@ __device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t 
 // Data-chunk bytes from the last object word on (only units that reach it):
 // BE(packed) for the partial word, BE(m) for splitVector padding words.
 template <int K>
-__device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t b, int ncol,
-                                              const ObjWords& ow, uint32_t m, const uint32_t (&x)[K][4]) {
+__device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0, uint64_t b,
+                                              int ncol, const ObjWords& ow, uint32_t m, const uint32_t (&x)[K][4]) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    const uint64_t w0 = (uint64_t)j * L + b;
+    const uint64_t w0 = (uint64_t)j * L + col0 + b;
     if (w0 + ncol < ow.nw) continue;
     uint32_t fix[4];
 #pragma unroll
@@ -190,17 +192,20 @@ __device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uin
 // Lanes own 4 columns (16 B per chunk) per unit; a wave issues the loads of
 // U units (U KiB of every data chunk) before any math or store; columns past
 // the last multiple of 4 go one per lane.
+// Column window: columns [col0, col0 + ncols) of every chunk (col0 a
+// multiple of 4; the whole object is col0 = 0, ncols = L).  Chunks stay 4L
+// bytes apart; the host pipeline streams an object window by window.
 template <int K, int U, int MODE, bool FAST = true, bool FLAGS_ON = true>
 __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows,
-    const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ mapping) {
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping) {
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t nvec = L >> 2;
+  const uint64_t nvec = ncols >> 2;
   const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
   // Units whose columns reach the object's last word (or padding) need the
   // data-chunk tail fix; every other unit skips that branch.
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
       m = mapping[obj];
       if (m == 0 || flags[obj] != 0) continue;  // nothing to redo / random fallback pending (uniform per block)
     }
-    uint8_t* const slot = slots + (uint64_t)obj * slot_stride;
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
     uint8_t* const par = slot + (uint64_t)K * chunk;  // parity chunk i at par + out_idx[i]*chunk
     constexpr bool F = MODE == 0 && FLAGS_ON;
     Flags fl;
@@ -219,12 +224,12 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
       const uint64_t g0 = step * (64 * U) + lane;
       // Interior step: the highest word the wave's units touch (last data
       // chunk, last unit) is below the object's last word: no checks needed.
-      const uint64_t top = (uint64_t)(K - 1) * L + ((step * (64 * U) + 64 * U) << 2);
+      const uint64_t top = (uint64_t)(K - 1) * L + col0 + ((step * (64 * U) + 64 * U) << 2);
       uint32_t x[U][K][4];
       if (FAST && top < first_tail_word && (step + 1) * (64 * U) <= nvec) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          load_data_symbols<K, true, F>(slot, chunk, L, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
+          load_data_symbols<K, true, F>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
         rows_out_units<K, U>(x, U, rows, coeff, out_idx, par, chunk, g0, m);
         continue;
       }
@@ -235,21 +240,22 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (g0 + 64 * u < nvec) {
-          load_data_symbols<K, false, F>(slot, chunk, L, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
+          load_data_symbols<K, false, F>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
           n = u + 1;
         }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u >= n) break;
         const uint64_t b = (g0 + 64 * u) << 2;
-        if ((uint64_t)(K - 1) * L + b + 4 > first_tail_word) fix_data_tail<K>(slot, chunk, L, b, 4, ow, m, x[u]);
+        if ((uint64_t)(K - 1) * L + col0 + b + 4 > first_tail_word)
+          fix_data_tail<K>(slot, chunk, L, col0, b, 4, ow, m, x[u]);
       }
       rows_out_units<K, U>(x, n, rows, coeff, out_idx, par, chunk, g0, m);
     }
-    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < L; b += nwaves * 64) {
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < ncols; b += nwaves * 64) {
       uint32_t x[K][4];
-      load_data_symbols<K, false, F>(slot, chunk, L, b, 1, ow, m, x, &fl);
-      fix_data_tail<K>(slot, chunk, L, b, 1, ow, m, x);
+      load_data_symbols<K, false, F>(slot, chunk, L, col0, b, 1, ow, m, x, &fl);
+      fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
       rows_out<K>(x, rows, coeff, out_idx, par, chunk, 4 * b, m, 1);
     }
     if constexpr (F) {
@@ -290,9 +296,11 @@ __device__ __forceinline__ void load_chunk_symbols(const uint8_t* slot, const ui
   }
 }
 
+// Column window [col0, col0 + ncols) as in encode_bytes_kernel.
 template <int K, int U>
 __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
-                                                              uint64_t L, uint32_t nobj, uint32_t rows,
+                                                              uint64_t L, uint64_t col0, uint64_t ncols,
+                                                              uint32_t nobj, uint32_t rows,
                                                               const uint32_t* __restrict__ coeff,
                                                               const uint32_t* __restrict__ in_idx,
                                                               const uint32_t* __restrict__ out_idx,
@@ -301,11 +309,11 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t nvec = L >> 2;
+  const uint64_t nvec = ncols >> 2;
   const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
   for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
     const uint32_t m = mapping[obj];
-    uint8_t* const slot = slots + (uint64_t)obj * slot_stride;
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
     uint64_t ioff[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * chunk;
@@ -321,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
         }
       rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot, chunk, g0, m);
     }
-    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < L; b += nwaves * 64) {
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < ncols; b += nwaves * 64) {
       uint32_t x[K][4];
       load_chunk_symbols<K>(slot, ioff, b, 1, m, x);
       rows_out<K>(x, rows, coeff, out_idx, slot, chunk, 4 * b, m, 1);

@@ -278,7 +278,8 @@ size_t round16(size_t n) { return (n + 15) & ~(size_t)15; }
 // over a small pool).  The caller's buffers stay pageable; only the staging
 // ring is pinned, so nothing is registered per call.
 
-constexpr size_t kStageBytes = 8u << 20;  // in + out bytes one stage moves
+constexpr size_t kStageBytes = 8u << 20;      // in + out bytes one stage moves (Go-API rows)
+constexpr size_t kObjStageBytes = 16u << 20;  // per window of the object entry points
 
 enum class HostPipe : int { Staged = 0, Register = 1, Direct = 2 };
 
@@ -304,127 +305,6 @@ int host_apply_direct(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
     HIP_TRY(hipMemcpyAsync(out[i], d_out + shard * i, L * 4, hipMemcpyDeviceToHost, ws->stream));
   HIP_TRY(hipStreamSynchronize(ws->stream));
   return 0;
-}
-
-int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
-                      uint64_t L) {
-  const uint64_t nin = plan->k, nout = plan->rows;
-  uint64_t cl = std::max<uint64_t>(kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
-  if (cl >= L) cl = (L + 3) & ~3ull;  // one chunk; rows stay 16-byte aligned
-  const uint64_t nch = (L + cl - 1) / cl;
-  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
-  const size_t stage_words = (size_t)(nin + nout) * cl;
-  if (int rc = ws->reserve(stage_words * 4 * S)) return rc;
-  if (int rc = ws->reserve_pinned(stage_words * 4 * S)) return rc;
-  if (int rc = ws->ensure_stages()) return rc;
-  uint32_t* const pin = (uint32_t*)ws->pin;
-  uint32_t* const dev = (uint32_t*)ws->dbuf;
-  std::vector<CopyItem> items;
-  items.reserve(std::max(nin, nout));
-  // SLIME_RS_PIPE_TRACE=1: per-call split of host time (copy in / wait / copy out).
-  static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
-  using clk = std::chrono::steady_clock;
-  double t_in = 0, t_wait = 0, t_out = 0;
-  const auto t_start = clk::now();
-  auto since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
-
-  auto copy_out = [&](uint64_t c) -> int {
-    const int s = (int)(c % S);
-    const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
-    auto t0 = clk::now();
-    HIP_TRY(hipEventSynchronize(ws->sev[s]));
-    t_wait += since(t0);
-    t0 = clk::now();
-    const uint32_t* po = pin + s * stage_words + nin * cl;
-    items.clear();
-    for (uint64_t i = 0; i < nout; ++i) items.push_back({out[i] + c0, po + i * cl, n * 4});
-    parallel_copy(items.data(), items.size());
-    t_out += since(t0);
-    return 0;
-  };
-  auto body = [&]() -> int {
-    for (uint64_t c = 0; c < nch; ++c) {
-      const int s = (int)(c % S);
-      if (c >= (uint64_t)S)
-        if (int rc = copy_out(c - S)) return rc;
-      const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
-      uint32_t* pi = pin + s * stage_words;
-      uint32_t* di = dev + s * stage_words;
-      auto t0 = clk::now();
-      items.clear();
-      for (uint64_t j = 0; j < nin; ++j) items.push_back({pi + j * cl, in[j] + c0, n * 4});
-      parallel_copy(items.data(), items.size());
-      t_in += since(t0);
-      hipStream_t st = ws->sst[s];
-      HIP_TRY(hipMemcpyAsync(di, pi, ((nin - 1) * cl + n) * 4, hipMemcpyHostToDevice, st));
-      if (int rc = execute(plan, di, 0, cl, di + nin * cl, 0, cl, n, 1, st)) return rc;
-      HIP_TRY(hipMemcpyAsync(pi + nin * cl, di + nin * cl, ((nout - 1) * cl + n) * 4, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipEventRecord(ws->sev[s], st));
-    }
-    for (uint64_t c = nch > (uint64_t)S ? nch - S : 0; c < nch; ++c)
-      if (int rc = copy_out(c)) return rc;
-    return 0;
-  };
-  const int rc = body();
-  if (rc)  // drain what was queued before the failure: the ring is reused by the next call
-    for (int s = 0; s < S; ++s) (void)hipStreamSynchronize(ws->sst[s]);
-  if (trace)
-    fprintf(stderr, "slime_rs staged L=%llu chunks=%llu in=%.3f wait=%.3f out=%.3f total=%.3f ms\n",
-            (unsigned long long)L, (unsigned long long)nch, t_in, t_wait, t_out, since(t_start));
-  return rc;
-}
-
-// Register mode: page-lock the caller's rows for the duration of the call
-// and DMA straight from / to them (no host memcpy at all).  Returns -1 when
-// registration is refused (read-only or already-registered pages) so the
-// caller can stage instead.
-int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
-                          uint64_t L) {
-  const uint64_t nin = plan->k, nout = plan->rows;
-  std::vector<void*> reg;
-  reg.reserve(nin + nout);
-  auto unregister = [&] {
-    for (void* p : reg) (void)hipHostUnregister(p);
-  };
-  auto pin_row = [&](const void* p) -> bool {
-    if (hipHostRegister(const_cast<void*>(p), L * 4, hipHostRegisterDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    reg.push_back(const_cast<void*>(p));
-    return true;
-  };
-  for (uint64_t j = 0; j < nin; ++j)
-    if (!pin_row(in[j])) return unregister(), -1;
-  for (uint64_t i = 0; i < nout; ++i)
-    if (!pin_row(out[i])) return unregister(), -1;
-  uint64_t cl = std::max<uint64_t>(4 * kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
-  if (cl >= L) cl = (L + 3) & ~3ull;
-  const uint64_t nch = (L + cl - 1) / cl;
-  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
-  const size_t stage_words = (size_t)(nin + nout) * cl;
-  int rc = ws->reserve(stage_words * 4 * S);
-  if (!rc) rc = ws->ensure_stages();
-  auto body = [&]() -> int {
-    uint32_t* const dev = (uint32_t*)ws->dbuf;
-    for (uint64_t c = 0; c < nch; ++c) {
-      const int s = (int)(c % S);
-      const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
-      uint32_t* di = dev + s * stage_words;
-      hipStream_t st = ws->sst[s];
-      for (uint64_t j = 0; j < nin; ++j)
-        HIP_TRY(hipMemcpyAsync(di + j * cl, in[j] + c0, n * 4, hipMemcpyHostToDevice, st));
-      if (int e = execute(plan, di, 0, cl, di + nin * cl, 0, cl, n, 1, st)) return e;
-      for (uint64_t i = 0; i < nout; ++i)
-        HIP_TRY(hipMemcpyAsync(out[i] + c0, di + (nin + i) * cl, n * 4, hipMemcpyDeviceToHost, st));
-    }
-    return 0;
-  };
-  if (!rc) rc = body();
-  for (int s = 0; s < S; ++s)
-    if (ws->sst[s] && hipStreamSynchronize(ws->sst[s]) != hipSuccess && !rc) rc = fail_hip(hipGetLastError(), "stage sync");
-  unregister();
-  return rc;
 }
 
 // ---- staged whole-buffer transfers (object entry points) -------------------------
@@ -503,6 +383,191 @@ void drain_stages(Workspace* ws) {
   for (hipStream_t st : ws->sst)
     if (st) (void)hipStreamSynchronize(st);
 }
+
+// ---- windowed pipeline ------------------------------------------------------------
+//
+// A host call is cut into column windows.  Window c runs on stage s = c % S:
+// its input spans are memcpy'd (copy pool) into stage s's pinned buffer and
+// DMA'd on stage stream s, then the window's launch, then the DMA of its
+// output spans back into the same pinned buffer.  The outputs reach the
+// caller when stage s is needed again (or at the end), so the host copies of
+// one window overlap the DMA and kernels of the others, and the H2D of one
+// window overlaps the D2H of another.  Windows may also carry host-to-host
+// copies (write_chunks' data-chunk bodies), done with the window's inputs.
+
+struct Window {
+  std::vector<Span> in, out;
+  std::vector<CopyItem> host;
+  std::vector<size_t> in_off, out_off;  // offsets in the stage's pinned buffer
+};
+
+size_t round64(size_t n) { return (n + 63) & ~(size_t)63; }
+
+// DMA spans one by one, merging neighbours contiguous on both sides.
+int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
+              hipStream_t st) {
+  for (size_t i = 0; i < sp.size();) {
+    size_t j = i + 1, bytes = sp[i].bytes;
+    while (j < sp.size() && sp[j].dev_off == sp[i].dev_off + bytes && off[j] == off[i] + bytes) bytes += sp[j++].bytes;
+    if (h2d)
+      HIP_TRY(hipMemcpyAsync(dev + sp[i].dev_off, pin + off[i], bytes, hipMemcpyHostToDevice, st));
+    else
+      HIP_TRY(hipMemcpyAsync(pin + off[i], dev + sp[i].dev_off, bytes, hipMemcpyDeviceToHost, st));
+    i = j;
+  }
+  return 0;
+}
+
+// io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its kernels.
+template <class Io, class Launch>
+int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io, Launch&& launch) {
+  if (n == 0) return 0;
+  const int S = (int)std::min<uint64_t>(Workspace::kStages, n);
+  if (int rc = ws->reserve_pinned(stage_bytes * S)) return rc;
+  if (int rc = ws->ensure_stages()) return rc;
+  std::vector<Window> win(S);
+  std::vector<CopyItem> items;
+  auto pin_of = [&](int s) { return ws->pin + (size_t)s * stage_bytes; };
+  auto land = [&](int s) -> int {
+    HIP_TRY(hipEventSynchronize(ws->sev[s]));
+    const Window& w = win[s];
+    items.clear();
+    for (size_t i = 0; i < w.out.size(); ++i) items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
+    parallel_copy(items.data(), items.size());
+    return 0;
+  };
+  auto body = [&]() -> int {
+    for (uint64_t c = 0; c < n; ++c) {
+      const int s = (int)(c % S);
+      if (c >= (uint64_t)S)
+        if (int rc = land(s)) return rc;
+      Window& w = win[s];
+      w.in.clear(), w.out.clear(), w.host.clear();
+      io(c, s, w);
+      uint8_t* const pin = pin_of(s);
+      size_t off = 0;
+      items.clear();
+      w.in_off.resize(w.in.size());
+      for (size_t i = 0; i < w.in.size(); ++i) {
+        w.in_off[i] = off;
+        items.push_back({pin + off, w.in[i].host, w.in[i].bytes});
+        off = round64(off + w.in[i].bytes);
+      }
+      w.out_off.resize(w.out.size());
+      for (size_t i = 0; i < w.out.size(); ++i) {
+        w.out_off[i] = off;
+        off = round64(off + w.out[i].bytes);
+      }
+      if (off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
+      items.insert(items.end(), w.host.begin(), w.host.end());
+      parallel_copy(items.data(), items.size());
+      hipStream_t st = ws->sst[s];
+      if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;
+      if (int rc = launch(c, s, st)) return rc;
+      if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) return rc;
+      HIP_TRY(hipEventRecord(ws->sev[s], st));
+    }
+    for (uint64_t c = n > (uint64_t)S ? n - S : 0; c < n; ++c)
+      if (int rc = land((int)(c % S))) return rc;
+    return 0;
+  };
+  const int rc = body();
+  if (rc) drain_stages(ws);
+  return rc;
+}
+
+// Columns per window so that one window moves about `stage` bytes over
+// `rows` rows of 4-byte symbols; a multiple of 4096 (16 KiB per row), or the
+// whole length in one window.
+uint64_t window_cols(uint64_t L, uint64_t rows, size_t stage) {
+  const uint64_t cl = std::max<uint64_t>(stage / (rows * 4), 4096) & ~4095ull;
+  return cl >= L ? L : cl;
+}
+
+int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
+                      uint64_t L) {
+  const uint64_t nin = plan->k, nout = plan->rows;
+  const uint64_t cl = window_cols(L, nin + nout, kStageBytes);
+  const uint64_t n = (L + cl - 1) / cl;
+  const uint64_t rs = (cl + 3) & ~3ull;  // device row stride: 16-byte aligned rows
+  const size_t stage_dev = (size_t)(nin + nout) * rs * 4;
+  if (int rc = ws->reserve(stage_dev * std::min<uint64_t>(Workspace::kStages, n))) return rc;
+  uint8_t* const dev = ws->dbuf;
+  static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = run_windows(
+      ws, dev, n, (size_t)(nin + nout) * round64(rs * 4),
+      [&](uint64_t c, int s, Window& w) {
+        const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
+        const uint64_t base = (uint64_t)s * stage_dev;
+        for (uint64_t j = 0; j < nin; ++j) w.in.push_back({(uint8_t*)(in[j] + c0), base + j * rs * 4, nc * 4});
+        for (uint64_t i = 0; i < nout; ++i) w.out.push_back({(uint8_t*)(out[i] + c0), base + (nin + i) * rs * 4, nc * 4});
+      },
+      [&](uint64_t c, int s, hipStream_t st) -> int {
+        const uint64_t nc = std::min(cl, L - c * cl);
+        const uint32_t* di = (const uint32_t*)(dev + (size_t)s * stage_dev);
+        return execute(plan, di, 0, rs, (uint32_t*)di + nin * rs, 0, rs, nc, 1, st);
+      });
+  if (trace)
+    fprintf(stderr, "slime_rs staged L=%llu windows=%llu total=%.3f ms\n", (unsigned long long)L,
+            (unsigned long long)n,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return rc;
+}
+
+// Register mode: page-lock the caller's rows for the duration of the call
+// and DMA straight from / to them (no host memcpy at all).  Returns -1 when
+// registration is refused (read-only or already-registered pages) so the
+// caller can stage instead.
+int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
+                          uint64_t L) {
+  const uint64_t nin = plan->k, nout = plan->rows;
+  std::vector<void*> reg;
+  reg.reserve(nin + nout);
+  auto unregister = [&] {
+    for (void* p : reg) (void)hipHostUnregister(p);
+  };
+  auto pin_row = [&](const void* p) -> bool {
+    if (hipHostRegister(const_cast<void*>(p), L * 4, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    reg.push_back(const_cast<void*>(p));
+    return true;
+  };
+  for (uint64_t j = 0; j < nin; ++j)
+    if (!pin_row(in[j])) return unregister(), -1;
+  for (uint64_t i = 0; i < nout; ++i)
+    if (!pin_row(out[i])) return unregister(), -1;
+  uint64_t cl = std::max<uint64_t>(4 * kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
+  if (cl >= L) cl = (L + 3) & ~3ull;
+  const uint64_t nch = (L + cl - 1) / cl;
+  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
+  const size_t stage_words = (size_t)(nin + nout) * cl;
+  int rc = ws->reserve(stage_words * 4 * S);
+  if (!rc) rc = ws->ensure_stages();
+  auto body = [&]() -> int {
+    uint32_t* const dev = (uint32_t*)ws->dbuf;
+    for (uint64_t c = 0; c < nch; ++c) {
+      const int s = (int)(c % S);
+      const uint64_t c0 = c * cl, n = std::min(cl, L - c0);
+      uint32_t* di = dev + s * stage_words;
+      hipStream_t st = ws->sst[s];
+      for (uint64_t j = 0; j < nin; ++j)
+        HIP_TRY(hipMemcpyAsync(di + j * cl, in[j] + c0, n * 4, hipMemcpyHostToDevice, st));
+      if (int e = execute(plan, di, 0, cl, di + nin * cl, 0, cl, n, 1, st)) return e;
+      for (uint64_t i = 0; i < nout; ++i)
+        HIP_TRY(hipMemcpyAsync(out[i] + c0, di + (nin + i) * cl, n * 4, hipMemcpyDeviceToHost, st));
+    }
+    return 0;
+  };
+  if (!rc) rc = body();
+  for (int s = 0; s < S; ++s)
+    if (ws->sst[s] && hipStreamSynchronize(ws->sst[s]) != hipSuccess && !rc) rc = fail_hip(hipGetLastError(), "stage sync");
+  unregister();
+  return rc;
+}
+
 
 // out[i][0:L] = sum_j coeff[i][j] * in[j][0:L] for a plan whose inputs are
 // 0..k-1 and outputs 0..rows-1 (host memory on both sides).
@@ -1053,34 +1118,60 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
   uint8_t* const slot = ws->dbuf;
   uint32_t* const d_map = (uint32_t*)(ws->dbuf + round16(stride));
   uint32_t* const d_status = d_map + 1;
+  // Speculative pass (mapping 0) window by window: object bytes in, parity
+  // out, MapToGF's flags accumulating on device; the data-chunk bodies below
+  // the object's last word are the caller's own bytes (MapFromGF(m,
+  // MapToGF(x)) = x, map.go:15-33,103-113) and are placed on the host with
+  // each window's inputs.  The device computes every byte that depends on m.
+  const int r = total - need;
+  const uint64_t cl = window_cols(L, (uint64_t)total, kObjStageBytes);
+  const uint64_t nwin = (L + cl - 1) / cl;
   auto body = [&]() -> int {
-    const Span in{const_cast<uint8_t*>(data), 0, size};
-    if (int rc = staged_h2d(ws, slot, &in, 1)) return rc;
-    if (int rc = slime_rs_encode_objects(plan, slot, stride, size, 1, d_map, d_status, ws->stream)) return rc;
-    // Below the object's last word a data chunk is the object's own bytes
-    // (MapFromGF(m, MapToGF(x)) = x, map.go:15-33,103-113): place them while
-    // the device encodes; the tail (partial word, padding) comes back from it.
-    std::vector<CopyItem> items;
-    for (int j = 0; j < need; ++j) {
-      const uint64_t lo = (uint64_t)j * chunk;
-      if (lo < size) items.push_back({chunks[j], data + lo, std::min(size, lo + chunk) - lo});
-    }
-    parallel_copy(items.data(), items.size());
+    HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    if (int rc = run_windows(
+            ws, slot, nwin, (size_t)total * round64(cl * 4),
+            [&](uint64_t c, int, Window& w) {
+              const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
+              for (int j = 0; j < need; ++j) {
+                const uint64_t lo = (uint64_t)j * chunk + 4 * c0, hi = std::min(size, lo + 4 * nc);
+                if (lo >= hi) continue;
+                w.in.push_back({const_cast<uint8_t*>(data) + lo, lo, hi - lo});
+                w.host.push_back({chunks[j] + 4 * c0, data + lo, hi - lo});
+              }
+              for (int i = 0; i < r; ++i)
+                w.out.push_back({chunks[need + i] + 4 * c0, (uint64_t)(need + i) * chunk + 4 * c0, 4 * nc});
+            },
+            [&](uint64_t c, int, hipStream_t st) -> int {
+              BytesLaunch a = bytes_launch(plan, slot, stride, L, size, 1, 0, d_status, d_map);
+              a.col0 = c * cl;
+              a.ncols = std::min(cl, L - a.col0);
+              HIP_TRY(launch_encode_bytes(a, st));
+              return 0;
+            }))
+      return rc;
+    HIP_TRY(launch_select_mapping(d_map, d_status, 1, ws->stream));
     uint32_t ms[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
-    if (ms[1] != 0) {  // MapToGF's random fallback (map.go:64-66)
+    const bool redo = ms[0] != 0 || ms[1] != 0;
+    if (ms[1] != 0) {  // MapToGF's random fallback (map.go:64-66): resolved and re-encoded on device
       if (int rc = slime_rs_resolve_fallbacks(plan, slot, stride, size, 1, d_map, d_status, ws->stream, nullptr))
         return rc;
       HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
       HIP_TRY(hipStreamSynchronize(ws->stream));
+    } else if (ms[0] != 0) {  // mapping 1<<31: re-encode the whole object (map.go:47-62)
+      HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, stride, L, size, 1, 1, d_status, d_map), ws->stream));
     }
+    // The data-chunk tail (partial word, splitVector padding), and every
+    // parity chunk again if the mapping was not 0.
     std::vector<Span> out;
     for (int j = 0; j < need; ++j) {
       const uint64_t lo = (uint64_t)j * chunk, start = std::max(size, lo);
       if (start < lo + chunk) out.push_back({chunks[j] + (start - lo), start, lo + chunk - start});
     }
-    for (int i = need; i < total; ++i) out.push_back({chunks[i], (uint64_t)i * chunk, chunk});
+    if (redo)
+      for (int i = need; i < total; ++i) out.push_back({chunks[i], (uint64_t)i * chunk, chunk});
     if (int rc = staged_d2h(ws, slot, out.data(), out.size())) return rc;
     *mapping = ms[0];
     return 0;
@@ -1119,14 +1210,31 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   if (int rc = ws->reserve(round16(stride) + 16)) return rc;
   uint8_t* const slot = ws->dbuf;
   uint32_t* const d_map = (uint32_t*)(ws->dbuf + round16(stride));
+  // Window by window: survivors' columns in, all need data rows decoded,
+  // the object's bytes of those columns out.
+  const uint64_t cl = window_cols(L, 2 * (uint64_t)need, kObjStageBytes);
+  const uint64_t nwin = (L + cl - 1) / cl;
   auto body = [&]() -> int {
     HIP_TRY(hipMemcpyAsync(d_map, &mapping, 4, hipMemcpyHostToDevice, ws->stream));
-    std::vector<Span> in;
-    for (int q = 0; q < need; ++q) in.push_back({const_cast<uint8_t*>(chunks[q]), (uint64_t)q * chunk_bytes, chunk_bytes});
-    if (int rc = staged_h2d(ws, slot, in.data(), in.size())) return rc;
-    if (int rc = slime_rs_decode_objects(plan, slot, stride, L, 1, d_map, ws->stream)) return rc;
-    const Span o{out, body_bytes, got};
-    return staged_d2h(ws, slot, &o, 1);
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    return run_windows(
+        ws, slot, nwin, (size_t)2 * need * round64(cl * 4),
+        [&](uint64_t c, int, Window& w) {
+          const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
+          for (int q = 0; q < need; ++q)
+            w.in.push_back({const_cast<uint8_t*>(chunks[q]) + 4 * c0, (uint64_t)q * chunk_bytes + 4 * c0, 4 * nc});
+          for (int t = 0; t < need; ++t) {
+            const uint64_t o = (uint64_t)t * chunk_bytes + 4 * c0;
+            if (o < got) w.out.push_back({out + o, body_bytes + o, std::min(4 * nc, got - o)});
+          }
+        },
+        [&](uint64_t c, int, hipStream_t st) -> int {
+          BytesLaunch a = bytes_launch(plan, slot, stride, L, 0, 1, 0, nullptr, d_map);
+          a.col0 = c * cl;
+          a.ncols = std::min(cl, L - a.col0);
+          HIP_TRY(launch_decode_bytes(a, st));
+          return 0;
+        });
   };
   const int rc = body();
   if (rc) drain_stages(ws);
