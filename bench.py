@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall time budget of the CPU sample")
     ap.add_argument("--bytes-path", type=int, default=1,
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
+    ap.add_argument("--host-path", type=int, default=1,
+                    help="rank 0 at N=1: PCIe-inclusive writeChunks/reconstruct from host memory (never `value`)")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
     return ap.parse_args()
@@ -175,6 +177,39 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
             "fallback_redraws": redraws, "verified": ok,
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative mapping-0 pass + "
                     "1<<31 re-encode pass) and repair of erased chunks from chunk bytes"}
+
+
+def host_leg(need, total, erase, obj_mib=64, reps=5):
+    """PCIe-inclusive object rate from host memory (HTTP bodies <= 64 MiB):
+    slime_rs_write_chunks and slime_rs_reconstruct on caller-reused buffers,
+    median of `reps`.  Reported beside the device-resident `value`, never as it."""
+    import numpy as np
+    from slime_amd import objects
+    rng = np.random.default_rng(0x5113E)
+    data = rng.integers(0, 256, size=obj_mib << 20, dtype=np.uint8)
+    cb = objects.chunk_size(data.size, need)
+    chunks = [np.zeros(cb, dtype=np.uint8) for _ in range(total)]
+    out = np.zeros(data.size, dtype=np.uint8)
+    have = [i for i in range(total) if i not in erase][:need]
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+
+    box = {}
+    t_w = med(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
+    surv = [chunks[i] for i in have]
+    t_r = med(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
+    ok = bool(np.array_equal(out, data))
+    return {"write_chunks_gibs": round(data.size / GIB / t_w, 2), "reconstruct_gibs": round(data.size / GIB / t_r, 2),
+            "object_mib": obj_mib, "erased": erase, "verified": ok,
+            "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
+                    "PCIe-inclusive; not `value`"}
 
 
 def main():
@@ -319,6 +354,8 @@ def main():
             "cpu_baseline": None,
             "object_bytes_path": bytes_path,
         }
+        if world == 1 and args.host_path:
+            line["host_path"] = host_leg(need, total, erase)
         if world == 1 and args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib, args.cpu_seconds)
         print(json.dumps(line), flush=True)

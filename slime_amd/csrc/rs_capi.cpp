@@ -8,8 +8,12 @@
 #include "slime_rs.h"
 
 #include <hip/hip_runtime.h>
+#include <ctype.h>
+#include <sched.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -185,6 +189,44 @@ int cached_plan(const PlanKey& key, slime_rs_plan** out,
 
 // ---- per-call device workspaces (host entry points) ----------------------------
 
+// NUMA placement of a host page, the GPU and the calling CPU (diagnostics:
+// SLIME_RS_PIPE_TRACE).  -1 where unknown.
+struct NumaInfo {
+  int page_node = -1, gpu_node = -1, cpu = -1, cpu_node = -1;
+};
+
+int sysfs_int(const std::string& path) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return -1;
+  int v = -1;
+  if (fscanf(f, "%d", &v) != 1) v = -1;
+  fclose(f);
+  return v;
+}
+
+NumaInfo numa_info(int device, const void* page) {
+  NumaInfo ni;
+  int node = -1;
+  // get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR): the node backing `page`
+  if (syscall(SYS_get_mempolicy, &node, nullptr, 0, page, 3) == 0) ni.page_node = node;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) == hipSuccess) {
+    std::string id(bus);
+    for (auto& ch : id) ch = (char)tolower(ch);
+    ni.gpu_node = sysfs_int("/sys/bus/pci/devices/" + id + "/numa_node");
+  }
+  ni.cpu = sched_getcpu();
+  if (ni.cpu >= 0)
+    for (int n = 0; n < 64; ++n) {
+      const std::string d = "/sys/devices/system/node/node" + std::to_string(n) + "/cpu" + std::to_string(ni.cpu);
+      if (access(d.c_str(), F_OK) == 0) {
+        ni.cpu_node = n;
+        break;
+      }
+    }
+  return ni;
+}
+
 struct Workspace {
   static constexpr int kStages = 3;  // host pipeline depth (host_apply)
   int device = -1;
@@ -220,6 +262,11 @@ struct Workspace {
     pcap = 0;
     HIP_TRY(hipHostMalloc((void**)&pin, bytes, hipHostMallocDefault));
     pcap = bytes;
+    if (getenv("SLIME_RS_PIPE_TRACE")) {
+      const NumaInfo ni = numa_info(device, pin);
+      fprintf(stderr, "slime_rs pinned %zu MiB: page node %d, gpu node %d, cpu %d (node %d)\n", bytes >> 20,
+              ni.page_node, ni.gpu_node, ni.cpu, ni.cpu_node);
+    }
     return 0;
   }
   int ensure_stages() {
@@ -419,9 +466,16 @@ int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std
 }
 
 // io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its kernels.
+// SLIME_RS_PIPE_TRACE=1 prints each call's split of host time to stderr.
 template <class Io, class Launch>
-int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io, Launch&& launch) {
+int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io,
+                Launch&& launch) {
   if (n == 0) return 0;
+  static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  const auto t_start = clk::now();
+  double t_in = 0, t_wait = 0, t_out = 0, t_enq = 0;
   const int S = (int)std::min<uint64_t>(Workspace::kStages, n);
   if (int rc = ws->reserve_pinned(stage_bytes * S)) return rc;
   if (int rc = ws->ensure_stages()) return rc;
@@ -429,11 +483,15 @@ int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&
   std::vector<CopyItem> items;
   auto pin_of = [&](int s) { return ws->pin + (size_t)s * stage_bytes; };
   auto land = [&](int s) -> int {
+    auto t0 = clk::now();
     HIP_TRY(hipEventSynchronize(ws->sev[s]));
+    t_wait += ms_since(t0);
+    t0 = clk::now();
     const Window& w = win[s];
     items.clear();
     for (size_t i = 0; i < w.out.size(); ++i) items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
     parallel_copy(items.data(), items.size());
+    t_out += ms_since(t0);
     return 0;
   };
   auto body = [&]() -> int {
@@ -460,12 +518,16 @@ int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&
       }
       if (off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
       items.insert(items.end(), w.host.begin(), w.host.end());
+      auto t0 = clk::now();
       parallel_copy(items.data(), items.size());
+      t_in += ms_since(t0);
+      t0 = clk::now();
       hipStream_t st = ws->sst[s];
       if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;
       if (int rc = launch(c, s, st)) return rc;
       if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) return rc;
       HIP_TRY(hipEventRecord(ws->sev[s], st));
+      t_enq += ms_since(t0);
     }
     for (uint64_t c = n > (uint64_t)S ? n - S : 0; c < n; ++c)
       if (int rc = land((int)(c % S))) return rc;
@@ -473,6 +535,9 @@ int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&
   };
   const int rc = body();
   if (rc) drain_stages(ws);
+  if (trace)
+    fprintf(stderr, "slime_rs %s windows=%llu copy_in=%.3f enqueue=%.3f wait=%.3f copy_out=%.3f total=%.3f ms\n", what,
+            (unsigned long long)n, t_in, t_enq, t_wait, t_out, ms_since(t_start));
   return rc;
 }
 
@@ -493,10 +558,8 @@ int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
   const size_t stage_dev = (size_t)(nin + nout) * rs * 4;
   if (int rc = ws->reserve(stage_dev * std::min<uint64_t>(Workspace::kStages, n))) return rc;
   uint8_t* const dev = ws->dbuf;
-  static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
-  const auto t0 = std::chrono::steady_clock::now();
-  const int rc = run_windows(
-      ws, dev, n, (size_t)(nin + nout) * round64(rs * 4),
+  return run_windows(
+      "rows", ws, dev, n, (size_t)(nin + nout) * round64(rs * 4),
       [&](uint64_t c, int s, Window& w) {
         const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
         const uint64_t base = (uint64_t)s * stage_dev;
@@ -508,11 +571,6 @@ int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
         const uint32_t* di = (const uint32_t*)(dev + (size_t)s * stage_dev);
         return execute(plan, di, 0, rs, (uint32_t*)di + nin * rs, 0, rs, nc, 1, st);
       });
-  if (trace)
-    fprintf(stderr, "slime_rs staged L=%llu windows=%llu total=%.3f ms\n", (unsigned long long)L,
-            (unsigned long long)n,
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-  return rc;
 }
 
 // Register mode: page-lock the caller's rows for the duration of the call
@@ -1130,7 +1188,7 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
     HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
     if (int rc = run_windows(
-            ws, slot, nwin, (size_t)total * round64(cl * 4),
+            "write_chunks", ws, slot, nwin, (size_t)total * round64(cl * 4),
             [&](uint64_t c, int, Window& w) {
               const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
               for (int j = 0; j < need; ++j) {
@@ -1218,7 +1276,7 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
     HIP_TRY(hipMemcpyAsync(d_map, &mapping, 4, hipMemcpyHostToDevice, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
     return run_windows(
-        ws, slot, nwin, (size_t)2 * need * round64(cl * 4),
+        "reconstruct", ws, slot, nwin, (size_t)2 * need * round64(cl * 4),
         [&](uint64_t c, int, Window& w) {
           const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
           for (int q = 0; q < need; ++q)

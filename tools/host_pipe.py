@@ -126,10 +126,10 @@ def main():
                            env=env, capture_output=True, text=True, timeout=300)
         print(r.stdout.strip() or json.dumps({"variant": v, "rc": r.returncode, "err": r.stderr[-800:]}), flush=True)
         if "SLIME_RS_PIPE_TRACE" in v:  # per-call host-time split, last call of each size
-            lines = [ln for ln in r.stderr.splitlines() if ln.startswith("slime_rs staged")]
+            lines = [ln for ln in r.stderr.splitlines() if ln.startswith("slime_rs ")]
             seen = {}
             for ln in lines:
-                seen[ln.split()[2]] = ln
+                seen[" ".join(ln.split()[1:3])] = ln
             for ln in seen.values():
                 print("  " + ln, flush=True)
 
