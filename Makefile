@@ -58,3 +58,9 @@ hashprobe: tools/libhashprobe.so
 tools/libhashprobe.so: tools/hash_probe.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: hashprobe
+
+# Placement-mode probe (tools only): make placeprobe
+placeprobe: tools/libplaceprobe.so
+tools/libplaceprobe.so: tools/placement_probe.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: placeprobe

@@ -324,6 +324,82 @@ def test_plan_matrix_unaligned_layouts_and_noncanonical(torch_dev):
             assert np.array_equal(got[o, i], want[i])
 
 
+@pytest.mark.parametrize("need,total", [(8, 12), (10, 14), (4, 6)])
+@pytest.mark.parametrize("L", [5 * 1024 + 1, 3 * 1024 + 2, 2 * 1024 + 3, 4097, 65, 7])
+def test_realigned_layouts_vs_oracle(torch_dev, need, total, L):
+    """Shard bases off 16-byte boundaries by 1..3 words (realigned loads and
+    stores, tile and shard boundaries, in-place parity and a separate
+    destination at every base offset)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    nobj = 3
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    for off in range(4):
+        buf = torch.empty(off + nobj * total * L + 3, dtype=torch.int32, device="cuda")
+        D.fill_symbols(buf, seed=L * 13 + off)
+        before = buf.clone()
+        plan(buf, lay, buf, lay, L, nobj, src_offset=off, dst_offset=off + need * L)
+        torch.cuda.synchronize()
+        whole = buf.cpu().numpy().view(np.uint32)
+        # nothing outside the parity stripes moved (partial granules at both ends)
+        mask = np.ones(whole.size, dtype=bool)
+        for o in range(nobj):
+            s0 = off + o * total * L + need * L
+            mask[s0: s0 + (total - need) * L] = False
+        assert np.array_equal(whole[mask], before.cpu().numpy().view(np.uint32)[mask]), off
+        h = whole[off: off + nobj * total * L].reshape(nobj, total, L)
+        for o in range(nobj):
+            ref = np.ascontiguousarray(h[o].copy())
+            OC.encode_object(ref, need, total)
+            assert np.array_equal(h[o], ref), (off, o)
+        # rebuild a data and a parity shard into a separate buffer at every offset
+        erase = [1, need]
+        have = [i for i in range(total) if i not in erase][:need]
+        rec = D.Plan.reconstruct(need, total, have, erase)
+        for doff in range(4):
+            out = torch.zeros(doff + nobj * len(erase) * L + 2, dtype=torch.int32, device="cuda")
+            rec(buf, lay, out, D.layout_of(len(erase), L), L, nobj, src_offset=off, dst_offset=doff)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint32)
+            assert not got[:doff].any() and not got[doff + nobj * len(erase) * L:].any()
+            got = got[doff: doff + nobj * len(erase) * L].reshape(nobj, len(erase), L)
+            for o in range(nobj):
+                for i, t in enumerate(erase):
+                    assert np.array_equal(got[o, i], h[o, t]), (off, doff, o, t)
+
+
+def test_full_size_c5_roundtrip(torch_dev):
+    """BASELINE C5 shape (10/14, 1 GiB objects, L = 26843546: shard bases 8 bytes
+    off 16-byte boundaries) on two objects: encode, erase, rebuild in place."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, nobj = 10, 14, 2
+    L = -(-(1 << 30) // 4 // need)
+    assert L % 4 == 2
+    buf = _objects(torch, nobj, total, L, seed=0xC5)
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    v = buf.view(nobj, total, L)
+    h = v[1].cpu().numpy().view(np.uint32)
+    cols = np.sort(np.concatenate([np.arange(0, 1100), np.arange(L - 1100, L),
+                                   np.random.default_rng(5).choice(L, size=4096, replace=False)]))
+    ref = OC.apply_matrix(rs.ParityMatrix(need, total - need)[need:], [h[j, cols] for j in range(need)])
+    for i in range(total - need):
+        assert np.array_equal(h[need + i, cols], ref[i])
+    for erase in ([0, 1, 2, 3], [0, 5, 10, 13]):
+        truth = v[:, erase, :].clone()
+        v[:, erase, :] = -1
+        have = [i for i in range(total) if i not in erase][:need]
+        D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)(buf, lay, buf, lay, L, nobj)
+        torch.cuda.synchronize()
+        assert torch.equal(v[:, erase, :], truth), erase
+        del truth
+    del buf, v
+    torch.cuda.empty_cache()
+
+
 def test_full_size_roundtrip_and_linearity(torch_dev):
     """BASELINE C3/C4 shape (8/12, 256 MiB objects) on a few objects: properties."""
     torch = torch_dev

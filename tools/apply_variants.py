@@ -56,7 +56,7 @@ def main():
                                  ctypes.c_uint32, ctypes.c_void_p]
     need, total, nobj = args.need, args.total, args.nobj
     r = total - need
-    L = (args.mib << 20) // 4 // need
+    L = -(-(args.mib << 20) // 4 // need)  # perVector = ceil(ceil(S/4)/need), splitVector
     pads = [int(p) for p in args.pad.split(",")]
     maxss = L + max(pads)
     tail = nobj * r * maxss if args.separate == 2 else 0  # 2: destination in the same allocation, after the objects

@@ -33,7 +33,7 @@ has() { for s in "${STEPS[@]}"; do [ "$s" = "$1" ] && return 0; done; return 1; 
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || true
 nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
 
-has tests && run pytest_gpu 900 python -m pytest tests -m gpu -x -q
+has tests && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 has smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 has micro && run micro 600 python tools/microbench.py
 has bench && run bench 600 python bench.py
@@ -75,6 +75,20 @@ fi
 if has grid; then
   for g in 1024 4096 8192; do
     run bench_grid$g 300 env SLIME_RS_GRID_TARGET=$g python bench.py --steps 5 --cpu-baseline 0
+  done
+fi
+has placeprobe && run placeprobe 600 python tools/placement_probe.py
+has placemap && run placemap 600 python tools/placement_map.py
+if has placepmc; then  # counters on fast vs slow buffers (kernel-trace durations classify each dispatch)
+  i=0
+  for set in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_TCC_WRITE_REQ_LATENCY_sum" \
+             "TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum TCC_EA0_WRREQ_LEVEL_sum" \
+             "TCC_EA0_WRREQ" \
+             "TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_WRITEBACK_sum" \
+             "TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum"; do
+    i=$((i+1))
+    run ppmc$i 240 rocprofv3 --pmc $set --kernel-trace -d "$OUT/ppmc$i" -o run --output-format csv -- \
+      python3 tools/placement_probe.py --reps 2
   done
 fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
