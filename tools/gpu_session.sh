@@ -91,6 +91,15 @@ if has placepmc; then  # counters on fast vs slow buffers (kernel-trace duration
       python3 tools/placement_probe.py --reps 2
   done
 fi
+if has gridk; then  # block budget per k (SLIME_RS_GRID_TARGET), device-resident encode+decode
+  for kn in "8 12 256 128 0,1,2,3" "10 14 1024 16 0,1,2,3" "12 16 1024 16 0,1,2,3" "16 20 1024 16 0,1,2,3" "4 6 64 32 0,1"; do
+    set -- $kn
+    for g in 256 512 1024; do
+      run gridk_${1}_${2}_g$g 300 env SLIME_RS_GRID_TARGET=$g python bench.py --need $1 --total $2 --object-mib $3 \
+        --objects $4 --erase $5 --steps 5 --warmup 1 --cpu-baseline 0 --bytes-path 0 --host-path 0
+    done
+  done
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
