@@ -46,14 +46,21 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 }
 
 // Launch geometry: `target` resident 256-lane blocks (8 per CU at 2048 on 256
-// CUs), spread over at most `inflight` objects at a time.  Environment
+// CUs), spread over at most `inflight` objects at a time.  The default block
+// budget is 512, and 256 for 9 <= k <= 12 (U = 4 at k = 9, 10 holds 36-40 KiB
+// of symbols per wave; fewer, fatter waves measured +5..18% at 10/14 and
+// +2% at 12/16 on 1 GiB objects, profiles/r01/gridk/).  Environment
 // overrides exist for the tuning harness only.
 struct Geometry {
-  uint64_t target, inflight;
+  uint64_t target, inflight;  // target 0: per-k default
 };
 const Geometry& geometry() {
-  static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 512), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
+  static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
   return g;
+}
+template <int K>
+constexpr uint64_t default_blocks() {
+  return K >= 9 && K <= 12 ? 256 : 512;
 }
 
 template <int K, bool VEC>
@@ -63,7 +70,8 @@ hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   const Geometry& geo = geometry();
   uint64_t gy = a.nobj < geo.inflight ? a.nobj : geo.inflight;
   if (gy > 65535) gy = 65535;
-  uint64_t gx = (geo.target + gy - 1) / gy;
+  const uint64_t target = geo.target ? geo.target : default_blocks<K>();
+  uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = (a.ncols + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
