@@ -379,24 +379,6 @@ int stage_ring(Workspace* ws) {
   return ws->ensure_stages();
 }
 
-// Host spans -> dev; ws->stream waits for every piece before its next launch.
-int staged_h2d(Workspace* ws, uint8_t* dev, const Span* sp, size_t n) {
-  if (int rc = stage_ring(ws)) return rc;
-  const std::vector<Span> pcs = pieces_of(sp, n);
-  const int S = Workspace::kStages;
-  for (size_t p = 0; p < pcs.size(); ++p) {
-    const int s = (int)(p % S);
-    uint8_t* pin = ws->pin + (size_t)s * kStageBytes;
-    if (p >= (size_t)S) HIP_TRY(hipEventSynchronize(ws->sev[s]));  // stage buffer free again
-    const CopyItem it{pin, pcs[p].host, pcs[p].bytes};
-    parallel_copy(&it, 1);
-    HIP_TRY(hipMemcpyAsync(dev + pcs[p].dev_off, pin, pcs[p].bytes, hipMemcpyHostToDevice, ws->sst[s]));
-    HIP_TRY(hipEventRecord(ws->sev[s], ws->sst[s]));
-  }
-  for (int s = 0; s < S && (size_t)s < pcs.size(); ++s) HIP_TRY(hipStreamWaitEvent(ws->stream, ws->sev[s], 0));
-  return 0;
-}
-
 // dev -> host spans after everything queued on ws->stream so far; returns
 // when the host copies are complete.
 int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
