@@ -184,3 +184,71 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in src.replace("oracle/", ""), f
+
+
+# The reference's exported Go API (and the unexported names its own tests
+# call), with the signatures the cgo shim must keep: internal/rs/vector.go:18,50;
+# matrix.go:8,27,35,99; matrixcache.go:11; gf/map.go:15,74,103; gf/gf.go:5,46.
+GO_API = {
+    "go/internal/rs/rs.go": [
+        "func CreateParity(data [][]uint32, index int, out []uint32) []uint32",
+        "func RecoverData(chunks [][]uint32, indices []int) [][]uint32",
+        "func ParityMatrix(d, p int) [][]uint32",
+        "func ParityMatrixCached(d, p int) [][]uint32",
+        "func vandermondeMatrix(d, p int) [][]uint32",
+        "func solveSubIdentity(m [][]uint32)",
+        "func cloneMatrix(m [][]uint32) [][]uint32",
+    ],
+    "go/internal/rs/gf/gf.go": [
+        "const MaxVal = 1<<32 - 5",
+        "func MapToGF(in []byte) (uint32, []uint32)",
+        "func MapToGFWith(in []byte, n uint32) []uint32",
+        "func MapFromGF(inn uint32, inv []uint32) []byte",
+        "func MInverse(in uint32) uint32",
+        "func Raise(x, n uint32) uint32",
+    ],
+}
+
+
+def _header_arity():
+    text = open(os.path.join(ROOT, "include", "slime_rs.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    arity = {}
+    for name, params in re.findall(r"\b(slime_\w+)\s*\(([^)]*)\)\s*;", text):
+        params = params.strip()
+        arity[name] = 0 if params in ("", "void") else params.count(",") + 1
+    return arity
+
+
+def _call_args(src, start):
+    """Top-level argument count of the call whose '(' is at src[start]."""
+    depth, n, nonempty = 0, 1, False
+    for ch in src[start:]:
+        if ch in "([{":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                return n if nonempty else 0
+        elif ch == "," and depth == 1:
+            n += 1
+        if depth >= 1 and not ch.isspace():
+            nonempty = True
+    raise AssertionError("unbalanced call")
+
+
+def test_go_shim_keeps_the_reference_api_and_binds_the_header():
+    """The cgo shim (compile-unverified: no Go toolchain here) declares the
+    reference's Go API verbatim and calls only C entry points the header
+    declares, each with the header's argument count."""
+    arity = _header_arity()
+    for path, decls in GO_API.items():
+        src = open(os.path.join(ROOT, path)).read()
+        for d in decls:
+            assert d in src, (path, d)
+        for m in re.finditer(r"\bC\.(slime_\w+)\(", src):
+            name = m.group(1)
+            assert name in arity, (path, name)
+            assert _call_args(src, m.end() - 1) == arity[name], (path, name)
