@@ -58,6 +58,17 @@ const Geometry& geometry() {
   static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
   return g;
 }
+// Column segments per object (rs_apply_kernel): enough that the batch has
+// about 256 independent object segments in flight -- 128 x 256 MiB objects
+// reach 6.1 TB/s unsegmented, 32 x 64 MiB objects need 8 segments each to get
+// from 5.08 to 5.54 TB/s (profiles/r01/segs/) -- and at least 1024 vectors
+// (4 U=4 tiles) per segment.  Env SLIME_RS_SEGMENTS forces a count (tuning).
+uint32_t segments_for(uint32_t nobj, uint64_t ncols) {
+  static const uint64_t forced = env_u64("SLIME_RS_SEGMENTS", 0);
+  const uint64_t want = forced ? forced : (256 + nobj - 1) / nobj;
+  const uint64_t max_s = (ncols >> 2) / 1024 ? (ncols >> 2) / 1024 : 1;
+  return (uint32_t)(want < max_s ? want : max_s);
+}
 template <int K>
 constexpr uint64_t default_blocks() {
   return K >= 9 && K <= 12 ? 256 : 512;
@@ -68,16 +79,18 @@ hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   constexpr int U = unroll_for<K>();
   const uint64_t per_block = VEC && K > 0 ? 4ull * kBlock * U : (uint64_t)kBlock;
   const Geometry& geo = geometry();
-  uint64_t gy = a.nobj < geo.inflight ? a.nobj : geo.inflight;
+  const uint32_t nseg = VEC && K > 0 ? segments_for(a.nobj, a.ncols) : 1u;
+  const uint64_t nwork = (uint64_t)a.nobj * nseg;
+  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
   if (gy > 65535) gy = 65535;
   const uint64_t target = geo.target ? geo.target : default_blocks<K>();
   uint64_t gx = (target + gy - 1) / gy;
-  const uint64_t need = (a.ncols + per_block - 1) / per_block;
+  const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL((rs_apply_kernel<K, VEC, U, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
                      dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
-                     a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k);
+                     a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
   return hipGetLastError();
 }
 

@@ -89,6 +89,10 @@ __device__ __forceinline__ void row4(const uint4 (&x)[K], const u32x16& c, uint3
 // and the wave streams U KiB contiguous per shard.  K == 0: generic k.
 // Objects: blockIdx.y strides over objects, so gridDim.y bounds how many
 // objects (x shards) are streamed concurrently.
+// Segments: each object's columns are cut into `nseg` contiguous segments
+// that are scheduled like separate objects (blockIdx.y strides over
+// object x segment), so a batch of few objects still keeps many independent
+// stripe streams in flight; nseg = 1 is the plain per-object walk.
 //
 // ROT: each object walks its column tiles starting at a per-object rotation
 // (a bijection of [0, ntiles)), so the ~k x objects-in-flight concurrent
@@ -99,32 +103,37 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
-    uint32_t rows, uint32_t k) {
+    uint32_t rows, uint32_t k, uint32_t nseg) {
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
-  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
-    const uint32_t* __restrict__ ib = in + (uint64_t)obj * in_obj_stride;
-    uint32_t* __restrict__ ob = out + (uint64_t)obj * out_obj_stride;
-    uint64_t done = 0;
+  const uint64_t nvec = VEC && K > 0 ? ncols >> 2 : 0;
+  const uint64_t seg_vec = (nvec + nseg - 1) / nseg;  // 16-byte vectors per segment
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg, seg = wi % nseg;
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
     if constexpr (VEC && K > 0) {
       uint64_t ioff[K];
 #pragma unroll
       for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
-      const uint64_t nvec = ncols >> 2;
+      // This segment's vectors [v0, v1).
+      const uint64_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+      const uint64_t v1 = v0 + seg_vec < nvec ? v0 + seg_vec : nvec;
       const uint32_t lane = threadIdx.x & 63;
       const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
       const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-      const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
-      const uint64_t rot = ROT && ntiles ? ((uint64_t)obj * 0x9E3779B97F4A7C15ull >> 20) % ntiles : 0;
+      const uint64_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+      const uint64_t rot = ROT && ntiles ? ((uint64_t)wi * 0x9E3779B97F4A7C15ull >> 20) % ntiles : 0;
       for (uint64_t step = wave; step < ntiles; step += nwaves) {
         uint64_t t = step + rot;
         if (t >= ntiles) t -= ntiles;
-        const uint64_t g0 = t * (64 * U) + lane;
+        const uint64_t g0 = v0 + t * (64 * U) + lane;
         uint4 x[U][K];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint64_t b = (g0 + 64 * u) << 2;
-          if (g0 + 64 * u < nvec) {
+          if (g0 + 64 * u < v1) {
 #pragma unroll
             for (int j = 0; j < K; ++j) x[u][j] = ld16<NTL>(ib + ioff[j] + b);
           }
@@ -135,13 +144,15 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
           uint32_t* const orow = ob + (uint64_t)out_idx[i] * out_shard;
 #pragma unroll
           for (int u = 0; u < U; ++u)
-            if (g0 + 64 * u < nvec) row4<K, NTS>(x[u], c, orow + ((g0 + 64 * u) << 2));
+            if (g0 + 64 * u < v1) row4<K, NTS>(x[u], c, orow + ((g0 + 64 * u) << 2));
         }
       }
-      done = nvec << 2;
     }
-    for (uint64_t b = done + tid; b < ncols; b += nthr) apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx,
-                                                                        out_shard, rows, k, b);
+    // Columns past the last whole vector (all columns for the one-column
+    // kernels), one per lane, by the object's last segment.
+    if (seg == nseg - 1)
+      for (uint64_t b = (nvec << 2) + tid; b < ncols; b += nthr)
+        apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
   }
 }
 

@@ -12,21 +12,22 @@ namespace {
 template <int K, int U, bool NTL, bool NTS, bool ROT = false>
 void go(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os, const uint32_t* coeff,
         const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy,
-        hipStream_t s) {
+        hipStream_t s, uint32_t nseg) {
   hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS, ROT>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
-                     os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K);
+                     os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
 }
 }  // namespace
 
 extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is,
                          uint64_t oo, uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
-                         uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream) {
+                         uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream,
+                         uint32_t nseg) {
   hipStream_t s = (hipStream_t)stream;
 #define V2(id, U, NTL, NTS, ROT)                                                                            \
   case id:                                                                                                 \
-    if (k == 8) go<8, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);     \
-    else if (k == 10) go<10, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s); \
-    else if (k == 4) go<4, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s);   \
+    if (k == 8) go<8, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);     \
+    else if (k == 10) go<10, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 4) go<4, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
     else return -2;                                                                                        \
     break;
 #define V(id, U, NTL, NTS) V2(id, U, NTL, NTS, false)

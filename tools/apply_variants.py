@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", type=str, default="0,2,4,6,8,9,10")
     ap.add_argument("--blocks", type=str, default="256,384,512,768,1024")
-    ap.add_argument("--inflight", type=str, default="0", help="objects in flight (0 = all)")
+    ap.add_argument("--inflight", type=str, default="0", help="work items (object segments) in flight (0 = all)")
+    ap.add_argument("--nseg", type=str, default="1", help="column segments per object (comma list)")
     ap.add_argument("--decode", type=int, default=0, help="time reconstruct of data 0..e-1 instead of encode")
     ap.add_argument("--pad", type=str, default="0", help="shard stride = L + pad symbols (comma list)")
     ap.add_argument("--hunt", choices=["any", "slow", "fast"], default="any",
@@ -53,7 +54,7 @@ def main():
     lib.av_launch.restype = ctypes.c_int
     lib.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                 ctypes.c_uint32, ctypes.c_void_p]
+                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
     need, total, nobj = args.need, args.total, args.nobj
     r = total - need
     L = -(-(args.mib << 20) // 4 // need)  # perVector = ceil(ceil(S/4)/need), splitVector
@@ -127,37 +128,42 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
         view = lambda: shards()[:, slot0:slot0 + r, :]  # noqa: E731
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
-    def launch(v, gx, gy):
+    def launch(v, gx, gy, nseg=1):
         rc = lib.av_launch(v, need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
-                           ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream))
+                           ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream), nseg)
         assert rc == 0, rc
 
-    ys = [nobj if int(y) == 0 else int(y) for y in args.inflight.split(",")]
-    geos = [(int(t), y) for t, y in itertools.product(args.blocks.split(","), ys) if y <= nobj]
+    segs = [int(x) for x in args.nseg.split(",")]
+    geos = []
+    for t, y0, ns in itertools.product(args.blocks.split(","), args.inflight.split(","), segs):
+        y = nobj * ns if int(y0) == 0 else int(y0)
+        if y <= nobj * ns:
+            geos.append((int(t), y, ns))
     times = {(v, g): [] for v in VARIANTS for g in geos}
     for _ in range(args.rounds):
         for v in VARIANTS:
-            for t, y in geos:
+            for t, y, ns in geos:
                 gx = max(1, t // y)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(s)
-                launch(v, gx, y)
+                launch(v, gx, y, ns)
                 b.record(s)
                 torch.cuda.synchronize()
-                times[(v, (t, y))].append(a.elapsed_time(b))
-    # correctness of every variant (last geometry run of each)
+                times[(v, (t, y, ns))].append(a.elapsed_time(b))
+    # correctness of every variant and segment count
     bad = []
     for v in VARIANTS:
-        view().zero_()
-        launch(v, 4, 8)
-        torch.cuda.synchronize()
-        if not torch.equal(view(), ref):
-            bad.append(v)
+        for ns in segs:
+            view().zero_()
+            launch(v, 4, 8, ns)
+            torch.cuda.synchronize()
+            if not torch.equal(view(), ref):
+                bad.append((v, ns))
     alg = nobj * 4 * L * total
     rows = []
-    for (v, (t, y)), ts in times.items():
+    for (v, (t, y, ns)), ts in times.items():
         med = statistics.median(ts)
-        rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "ms": round(med, 3),
+        rows.append({"variant": VARIANTS[v], "blocks": t, "objects_in_flight": y, "nseg": ns, "ms": round(med, 3),
                      "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: -x["GBps"])
     return {"separate": int(args.separate if args.separate >= 0 else separate), "bad_variants": bad,

@@ -100,6 +100,27 @@ if has gridk; then  # block budget per k (SLIME_RS_GRID_TARGET), device-resident
     done
   done
 fi
+if has shapes; then  # BASELINE shapes through bench.py (device-resident, encode + repair)
+  run shape_c3_64mib_shards 300 python bench.py --object-mib 512 --objects 64 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run shape_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run shape_c5_all64 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run shape_c4_mixed 300 python bench.py --erase 0,3,8,11 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+fi
+if has segs; then  # column segments per object (more independent stripe streams for small batches)
+  run segs_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 8 --blocks 512,1024 --nseg 1,2,4,8
+  run segs_c2dec 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --decode 1 --variants 8 --blocks 512,1024 --nseg 1,2,4,8
+  run segs_c3 300 python tools/apply_variants.py --variants 8 --blocks 512,1024 --nseg 1,2,4
+  run segs_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --variants 8 --blocks 256,512 --nseg 1,2,4,8
+  run segs_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --decode 1 --variants 8 --blocks 256,512 --nseg 1,2,4,8
+fi
+if has shapes2; then  # product defaults vs forced segment counts on the small-batch shapes
+  for sg in 0 1 4 16; do
+    run sh2_c2_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+    run sh2_c5_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  done
+  run sh2_c3 300 python bench.py --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run sh2_c5_all64 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py

@@ -44,7 +44,7 @@ def main():
     av.av_launch.restype = ctypes.c_int
     av.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                 ctypes.c_uint32, ctypes.c_void_p]
+                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
     import numpy as np
     coeff = np.zeros((total - need, 16), dtype=np.uint32)
     coeff[:, :need] = enc.coefficients()
@@ -85,14 +85,14 @@ def main():
 
                 def go(mix=mix, ptr=ptr):
                     assert lib.pp_launch(mix, ptr, total * L, L, L, 1, 512, 1, sink.data_ptr(),
-                                         ctypes.c_void_p(s.cuda_stream)) == 0
+                                         ctypes.c_void_p(s.cuda_stream), 1) == 0
                 per.append(round(L * 4 * nstripes / (timed(go) * 1e-3) / 1e9))
             row[name] = {"median": statistics.median(per), "min": min(per), "max": max(per), "per_object": per}
         for gy in (1, 2, 8, 32, 128):
             def prod(gy=gy):
                 assert av.av_launch(8, need, t.data_ptr(), t.data_ptr(), total * L, L, total * L, L, c_t.data_ptr(),
                                     ii.data_ptr(), oi.data_ptr(), L, nobj, total - need, max(1, 512 // gy), gy,
-                                    ctypes.c_void_p(s.cuda_stream)) == 0
+                                    ctypes.c_void_p(s.cuda_stream), 1) == 0
             row[f"product_inflight{gy}_GBps"] = round(nobj * L * 4 * total / (timed(prod) * 1e-3) / 1e9, 1)
         out.append(row)
         print(json.dumps({k: (v if not isinstance(v, dict) else {kk: vv for kk, vv in v.items() if kk != "per_object"})
