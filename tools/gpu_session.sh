@@ -121,6 +121,14 @@ if has shapes2; then  # product defaults vs forced segment counts on the small-b
   run sh2_c3 300 python bench.py --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
   run sh2_c5_all64 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
 fi
+if has slowsegs; then  # on a slow allocation (if the box has one): do more independent streams help?
+  run slowsegs_enc 400 python tools/apply_variants.py --hunt slow --variants 8,11 --blocks 512,1024 --nseg 1,2,4,8,16
+  run slowsegs_dec 400 python tools/apply_variants.py --hunt slow --decode 1 --separate 0 --variants 8 --blocks 512,1024 --nseg 1,2,4,8,16
+fi
+if has offsets; then  # batch base offset inside one allocation; once plain, once under the profiler
+  run offsets_plain 300 python tools/offset_probe.py
+  run offsets_prof 300 rocprofv3 --kernel-trace -d "$OUT/offsets_prof" -o run --output-format csv -- python3 tools/offset_probe.py
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
