@@ -28,9 +28,9 @@ struct ApplyLaunch {
   bool vec_ok;              // 16-byte units per lane (needs 4-byte aligned bases; see rs_capi.cpp)
 };
 
-// Row stride (words) of a device coefficient table: padded to 16 words for the
-// k <= 16 kernels (one s_load_dwordx16 per row), exactly k otherwise.
-inline uint32_t coeff_stride(uint32_t k) { return k <= 16 ? 16u : k; }
+// Row stride (words) of a device coefficient table: k rounded up to 16 words,
+// so every 16-coefficient chunk of a row is one aligned s_load_dwordx16.
+inline uint32_t coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 

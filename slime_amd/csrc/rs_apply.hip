@@ -99,6 +99,26 @@ hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   return a.vec_ok ? launch_k<K, true>(a, s) : launch_k<K, false>(a, s);
 }
 
+// k > 16: rs_apply_wide_kernel, 16 output rows per pass over the inputs.
+hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
+  constexpr int RB = 16;
+  const uint64_t per_block = 4ull * kBlock;
+  const uint32_t nseg = segments_for(a.nobj, a.ncols);
+  const uint64_t nwork = (uint64_t)a.nobj * nseg;
+  const Geometry& geo = geometry();
+  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
+  if (gy > 65535) gy = 65535;
+  const uint64_t target = geo.target ? geo.target : 512;
+  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL((apply::rs_apply_wide_kernel<RB, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
+                     dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
+                     a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t s) {
@@ -121,7 +141,7 @@ hipError_t launch_apply(const ApplyLaunch& a, hipStream_t s) {
     case 14: return dispatch_vec<14>(a, s);
     case 15: return dispatch_vec<15>(a, s);
     case 16: return dispatch_vec<16>(a, s);
-    default: return launch_k<0, false>(a, s);
+    default: return a.vec_ok ? launch_wide(a, s) : launch_k<0, false>(a, s);
   }
 }
 

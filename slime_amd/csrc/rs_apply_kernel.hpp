@@ -12,9 +12,11 @@ namespace apply {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-// Device coefficient tables: rows padded to 16 words (64 B) for k <= 16 so a
-// row arrives in one s_load_dwordx16; row stride k for the generic kernel.
+// Device coefficient tables: rows padded to a multiple of 16 words (64 B), so
+// a row (k <= 16) or a 16-coefficient chunk of one (wide k) arrives in one
+// s_load_dwordx16.  kCoeffStride is the row stride of the k <= 16 kernels.
 constexpr int kCoeffStride = 16;
+__host__ __device__ constexpr uint32_t wide_coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -59,7 +61,7 @@ __device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, ui
     }
   } else {
     for (uint32_t i = 0; i < rows; ++i) {
-      const uint32_t* c = coeff + (uint64_t)i * k;
+      const uint32_t* c = coeff + (uint64_t)i * wide_coeff_stride(k);
       uint64_t lo = 0;
       uint32_t hi = 0;
       for (uint32_t j = 0; j < k; ++j) mac(lo, hi, ib[(uint64_t)in_idx[j] * in_shard + b], c[j]);
@@ -153,6 +155,80 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
     if (seg == nseg - 1)
       for (uint64_t b = (nvec << 2) + tid; b < ncols; b += nthr)
         apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
+  }
+}
+
+// Wide k (k > 16, up to the reference's 100 shards): the same 4-columns-per-
+// lane streaming as rs_apply_kernel, with the inputs taken in chunks of 16
+// shards and the outputs in blocks of up to RB rows.  Per row and column the
+// running value is a canonical 32-bit residue: each chunk's 16 products are
+// accumulated exactly on top of it (96-bit, gfp.hpp) and folded once, so a
+// block of RB rows costs 4 VGPRs per row instead of 12.  Inputs are read once
+// per row block: once in all for rows <= RB.
+template <int RB, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void rs_apply_wide_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, uint32_t nseg) {
+  constexpr int KC = 16;
+  const uint32_t cs = wide_coeff_stride(k);
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
+  const uint64_t nvec = ncols >> 2;
+  const uint64_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg, seg = wi % nseg;
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint64_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint64_t v1 = v0 + seg_vec < nvec ? v0 + seg_vec : nvec;
+    for (uint64_t g = v0 + wave * 64 + lane; g - lane < v1; g += nwaves * 64) {
+      const bool valid = g < v1;
+      const uint64_t b = g << 2;
+      for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
+        uint32_t acc[RB][4];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
+        for (uint32_t j0 = 0; j0 < k; j0 += KC) {
+          uint4 x[KC];
+#pragma unroll
+          for (int j = 0; j < KC; ++j)
+            x[j] = valid && j0 + j < k ? ld16<NTL>(ib + (uint64_t)in_idx[j0 + j] * in_shard + b) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            if (r0 + i < rows) {
+              // Padding coefficients past k are zero (plan table), so the
+              // whole chunk runs unconditionally.
+              const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0);
+              uint64_t lo0 = acc[i][0], lo1 = acc[i][1], lo2 = acc[i][2], lo3 = acc[i][3];
+              uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+              for (int j = 0; j < KC; ++j)
+                mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+              acc[i][0] = fold96(lo0, hi0);
+              acc[i][1] = fold96(lo1, hi1);
+              acc[i][2] = fold96(lo2, hi2);
+              acc[i][3] = fold96(lo3, hi3);
+            }
+          }
+        }
+        if (valid) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+            if (r0 + i < rows)
+              st16<NTS>(ob + (uint64_t)out_idx[r0 + i] * out_shard + b,
+                        make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+        }
+      }
+    }
+    if (seg == nseg - 1)
+      for (uint64_t b = (nvec << 2) + tid; b < ncols; b += nthr)
+        apply_column<0>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
   }
 }
 

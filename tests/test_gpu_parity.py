@@ -84,15 +84,18 @@ def test_create_parity_reuses_out_buffer():
     assert np.all(buf[10:] == 7)
 
 
-@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (17, 21)])
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (17, 21), (33, 50), (64, 80)])
 def test_recover_data_vs_oracle(need, total):
     rng = np.random.default_rng(need)
     L = 777
     data = rand_vecs(rng, need, L, canonical=True, edges=False)
     code = data + [OC.create_parity(data, need + i)[1] for i in range(total - need)]
     pyrng = random.Random(total)
-    sets = list(itertools.combinations(range(total), need))
-    pyrng.shuffle(sets)
+    if total <= 24:
+        sets = list(itertools.combinations(range(total), need))
+        pyrng.shuffle(sets)
+    else:  # too many subsets to list: sample them
+        sets = [pyrng.sample(range(total), need) for _ in range(12)]
     for have in sets[:40]:
         have = list(have)
         pyrng.shuffle(have)  # any order, as RecoverData allows
@@ -239,7 +242,8 @@ def _host(t, nobj, n, L):
 
 @pytest.mark.parametrize("need,total,L,nobj", [(2, 3, 1000, 3), (4, 6, 4096, 5), (8, 12, 12345, 4),
                                                (10, 14, 8191, 3), (8, 12, 3, 7), (16, 20, 1024, 2),
-                                               (20, 24, 999, 2)])
+                                               (20, 24, 999, 2), (17, 21, 4100, 3), (33, 40, 5003, 2),
+                                               (40, 60, 4096 + 7, 2), (50, 100, 2051, 2), (20, 24, 3 * 4096, 5)])
 def test_plan_encode_vs_oracle(torch_dev, need, total, L, nobj):
     torch = torch_dev
     from slime_amd import device as D

@@ -129,6 +129,12 @@ if has offsets; then  # batch base offset inside one allocation; once plain, onc
   run offsets_plain 300 python tools/offset_probe.py
   run offsets_prof 300 rocprofv3 --kernel-trace -d "$OUT/offsets_prof" -o run --output-format csv -- python3 tools/offset_probe.py
 fi
+if has widek; then  # k > 16: the generic one-column kernel
+  run widek_16_20 300 python bench.py --need 16 --total 20 --object-mib 256 --objects 32 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run widek_20_24 300 python bench.py --need 20 --total 24 --object-mib 256 --objects 32 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run widek_32_40 300 python bench.py --need 32 --total 40 --object-mib 256 --objects 32 --erase 0,1,2,3,4,5,6,7 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run widek_64_80 300 python bench.py --need 64 --total 80 --object-mib 256 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
