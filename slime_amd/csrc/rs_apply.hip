@@ -99,9 +99,10 @@ hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   return a.vec_ok ? launch_k<K, true>(a, s) : launch_k<K, false>(a, s);
 }
 
-// k > 16: rs_apply_wide_kernel, 16 output rows per pass over the inputs.
-hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
-  constexpr int RB = 16;
+// k > 16: rs_apply_wide_kernel -- all inputs in registers with 8-row blocks
+// up to k = 32, 16-shard chunks with 16-row blocks above.
+template <int KC, int RB>
+hipError_t launch_wide_k(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t per_block = 4ull * kBlock;
   const uint32_t nseg = segments_for(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
@@ -113,10 +114,14 @@ hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((apply::rs_apply_wide_kernel<RB, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
+  hipLaunchKernelGGL((apply::rs_apply_wide_kernel<KC, RB, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
                      dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
                      a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
   return hipGetLastError();
+}
+
+hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
+  return a.k <= 32 ? launch_wide_k<32, 8>(a, stream) : launch_wide_k<16, 16>(a, stream);
 }
 
 }  // namespace

@@ -165,13 +165,17 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
 // accumulated exactly on top of it (96-bit, gfp.hpp) and folded once, so a
 // block of RB rows costs 4 VGPRs per row instead of 12.  Inputs are read once
 // per row block: once in all for rows <= RB.
-template <int RB, bool NTL, bool NTS>
+//
+// KC (16 or 32) is the chunk width: KC = 32 holds all inputs of a k <= 32
+// code in registers at once (one HBM round trip per step), KC = 16 keeps the
+// register budget for 16-row blocks at larger k.
+template <int KC, int RB, bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void rs_apply_wide_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, uint32_t nseg) {
-  constexpr int KC = 16;
+  static_assert(KC % 16 == 0, "chunks are whole 16-coefficient loads");
   const uint32_t cs = wide_coeff_stride(k);
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
@@ -204,12 +208,18 @@ __global__ __launch_bounds__(kBlock) void rs_apply_wide_kernel(
             if (r0 + i < rows) {
               // Padding coefficients past k are zero (plan table), so the
               // whole chunk runs unconditionally.
-              const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0);
               uint64_t lo0 = acc[i][0], lo1 = acc[i][1], lo2 = acc[i][2], lo3 = acc[i][3];
               uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
 #pragma unroll
-              for (int j = 0; j < KC; ++j)
-                mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+              for (int h = 0; h < KC; h += 16) {
+                if (j0 + h < k) {
+                  const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0 + h);
+#pragma unroll
+                  for (int j = 0; j < 16; ++j)
+                    mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[h + j].x, x[h + j].y, x[h + j].z, x[h + j].w,
+                         c[j]);
+                }
+              }
               acc[i][0] = fold96(lo0, hi0);
               acc[i][1] = fold96(lo1, hi1);
               acc[i][2] = fold96(lo2, hi2);
