@@ -170,7 +170,8 @@ int slime_rs_plan_destroy(slime_rs_plan_t plan);
  * its `total` chunks of 4L bytes (chunk c at slot + c*4L, L = ceil(ceil(S/4)/need),
  * multi_store.go:272).  The object's S bytes are the first S bytes of its slot,
  * so the data chunks are in place: after encoding, chunk c of the slot is
- * exactly MapFromGF(mapping, part c) (multi_store.go:526-554).  need <= 16. */
+ * exactly MapFromGF(mapping, part c) (multi_store.go:526-554).  Any need (k > 16
+ * runs the 16-chunk byte kernels). */
 
 /* Encode nobj objects of S bytes: mapping[o] receives gf.MapToGF's choice
  * (map.go:35-62) and status[o] = 1 marks an object that needs MapToGF's random
@@ -205,7 +206,7 @@ uint64_t slime_rs_chunk_size(uint64_t size, int need);
  * in one device pass (fused byte kernels) with pinned, overlapped transfers.
  * chunks[0..total-1] each receive slime_rs_chunk_size(size, need) bytes;
  * *mapping receives MappingValue.  The random-mapping fallback draws from the
- * library's stream (slime_gf_seed).  need must be 1..16 and total > need;
+ * library's stream (slime_gf_seed).  need >= 1 and total > need;
  * size 0 gives mapping 0 and empty chunks.  Synchronous; thread-safe. */
 int slime_rs_write_chunks(const uint8_t *data, uint64_t size, int need, int total, uint8_t *const *chunks,
                           uint32_t *mapping);
@@ -215,7 +216,7 @@ int slime_rs_write_chunks(const uint8_t *data, uint64_t size, int need, int tota
  * chunk indices, and the file's MappingValue -> the object's `size` bytes in
  * out:  chunk := MapToGFWith(data, mapping); RecoverData(chunks, indices);
  * MapFromGF each data row; data[:size].  Same panics as RecoverData for bad
- * indices; need must be <= 16.  Bytes past need*chunk_bytes are zero, as
+ * indices.  Bytes past need*chunk_bytes are zero, as
  * in the reference's data[:Size] of a zeroed buffer.  Synchronous. */
 int slime_rs_reconstruct(const uint8_t *const *chunks, const int *indices, int need, uint64_t chunk_bytes,
                          uint32_t mapping, uint64_t size, uint8_t *out);

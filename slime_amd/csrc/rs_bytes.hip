@@ -54,25 +54,48 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-#define SLIME_K_SWITCH(fn)                   \
-  switch (a.k) {                             \
-    case 1: return fn<1>(a, s);              \
-    case 2: return fn<2>(a, s);              \
-    case 3: return fn<3>(a, s);              \
-    case 4: return fn<4>(a, s);              \
-    case 5: return fn<5>(a, s);              \
-    case 6: return fn<6>(a, s);              \
-    case 7: return fn<7>(a, s);              \
-    case 8: return fn<8>(a, s);              \
-    case 9: return fn<9>(a, s);              \
-    case 10: return fn<10>(a, s);            \
-    case 11: return fn<11>(a, s);            \
-    case 12: return fn<12>(a, s);            \
-    case 13: return fn<13>(a, s);            \
-    case 14: return fn<14>(a, s);            \
-    case 15: return fn<15>(a, s);            \
-    case 16: return fn<16>(a, s);            \
-    default: return hipErrorInvalidValue;    \
+// need > 16: the 16-chunk byte kernels (rs_bytes_kernel.hpp, "wide k").
+constexpr int kWideRows = 8;
+
+hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const dim3 g = grid_for(ncols, a.phase == 0 ? a.nobj : 1);
+  if (a.phase == 0)
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<kWideRows, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride,
+                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping);
+  else
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<kWideRows, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride,
+                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping);
+  return hipGetLastError();
+}
+
+hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<kWideRows>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s,
+                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
+                     a.mapping);
+  return hipGetLastError();
+}
+
+#define SLIME_K_SWITCH(fn)               \
+  switch (a.k) {                         \
+    case 1: return fn##_k<1>(a, s);      \
+    case 2: return fn##_k<2>(a, s);      \
+    case 3: return fn##_k<3>(a, s);      \
+    case 4: return fn##_k<4>(a, s);      \
+    case 5: return fn##_k<5>(a, s);      \
+    case 6: return fn##_k<6>(a, s);      \
+    case 7: return fn##_k<7>(a, s);      \
+    case 8: return fn##_k<8>(a, s);      \
+    case 9: return fn##_k<9>(a, s);      \
+    case 10: return fn##_k<10>(a, s);    \
+    case 11: return fn##_k<11>(a, s);    \
+    case 12: return fn##_k<12>(a, s);    \
+    case 13: return fn##_k<13>(a, s);    \
+    case 14: return fn##_k<14>(a, s);    \
+    case 15: return fn##_k<15>(a, s);    \
+    case 16: return fn##_k<16>(a, s);    \
+    default: return fn##_wide(a, s);     \
   }
 
 }  // namespace
@@ -81,14 +104,14 @@ hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0) return hipSuccess;
   if (a.col0 % 4 || a.col0 + a.ncols > a.L) return hipErrorInvalidValue;
-  SLIME_K_SWITCH(enc_k)
+  SLIME_K_SWITCH(enc)
 }
 
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.L == 0 || a.rows == 0) return hipSuccess;
   if (a.col0 % 4 || a.col0 + a.ncols > a.L) return hipErrorInvalidValue;
-  SLIME_K_SWITCH(dec_k)
+  SLIME_K_SWITCH(dec)
 }
 
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t s) {

@@ -124,66 +124,75 @@ struct Flags {
   }
 };
 
-// Load the K data-chunk words of window columns [b, b+ncol) as symbols
+// Load data chunk j's words of window columns [b, b+ncol) as symbols
 // (mapping m, splitVector padding), folding the packed words into MapToGF's
 // flags.  `slot` points at the window (object slot + 4*col0); the object word
 // index of chunk j, window column b is j*L + col0 + b.
 // INTERIOR: every word of the unit is a full object word (the bulk of every
 // object) -- no padding/partial-word checks.
+template <bool INTERIOR, bool FLAGS>
+__device__ __forceinline__ void load_data_symbol(const uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0,
+                                                 uint32_t j, uint64_t b, int ncol, const ObjWords& ow, uint32_t m,
+                                                 uint32_t (&x)[4], Flags* fl) {
+  const uint8_t* src = slot + (uint64_t)j * chunk + 4 * b;
+  uint32_t raw[4] = {0, 0, 0, 0};
+  if (ncol == 4) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+    raw[0] = v.x, raw[1] = v.y, raw[2] = v.z, raw[3] = v.w;
+  } else {
+    raw[0] = *reinterpret_cast<const uint32_t*>(src);
+  }
+  if constexpr (INTERIOR) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t p = be(raw[c]);
+      if (FLAGS) fl->add(c, p);
+      x[c] = p ^ m;
+    }
+  } else {
+    const uint64_t w0 = (uint64_t)j * L + col0 + b;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bool pad;
+      const uint32_t p = packed_word(raw[c], w0 + c, ow, &pad);
+      if (FLAGS && !pad && c < ncol) fl->add(c, p);
+      x[c] = pad ? 0u : p ^ m;
+    }
+  }
+}
+
 template <int K, bool INTERIOR, bool FLAGS>
 __device__ __forceinline__ void load_data_symbols(const uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0,
                                                   uint64_t b, int ncol, const ObjWords& ow, uint32_t m,
                                                   uint32_t (&x)[K][4], Flags* fl) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const uint8_t* src = slot + (uint64_t)j * chunk + 4 * b;
-    uint32_t raw[4] = {0, 0, 0, 0};
-    if (ncol == 4) {
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
-      raw[0] = v.x, raw[1] = v.y, raw[2] = v.z, raw[3] = v.w;
-    } else {
-      raw[0] = *reinterpret_cast<const uint32_t*>(src);
-    }
-    if constexpr (INTERIOR) {
+  for (int j = 0; j < K; ++j) load_data_symbol<INTERIOR, FLAGS>(slot, chunk, L, col0, j, b, ncol, ow, m, x[j], fl);
+}
+
+// Data chunk j's bytes from the last object word on (only units that reach
+// it): BE(packed) for the partial word, BE(m) for splitVector padding words.
+__device__ __forceinline__ void fix_data_tail_one(uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0,
+                                                  uint32_t j, uint64_t b, int ncol, const ObjWords& ow, uint32_t m,
+                                                  const uint32_t (&x)[4]) {
+  const uint64_t w0 = (uint64_t)j * L + col0 + b;
+  if (w0 + ncol < ow.nw) return;
+  uint32_t fix[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t p = be(raw[c]);
-        if (FLAGS) fl->add(c, p);
-        x[j][c] = p ^ m;
-      }
-    } else {
-      const uint64_t w0 = (uint64_t)j * L + col0 + b;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        bool pad;
-        const uint32_t p = packed_word(raw[c], w0 + c, ow, &pad);
-        if (FLAGS && !pad && c < ncol) fl->add(c, p);
-        x[j][c] = pad ? 0u : p ^ m;
-      }
-    }
+  for (int c = 0; c < 4; ++c) fix[c] = be(w0 + c >= ow.nw ? m : x[c] ^ m);
+  uint8_t* d = slot + (uint64_t)j * chunk + 4 * b;
+  if (ncol == 4) {
+    const u32x4 v = {fix[0], fix[1], fix[2], fix[3]};
+    *reinterpret_cast<u32x4*>(d) = v;
+  } else {
+    *reinterpret_cast<uint32_t*>(d) = fix[0];
   }
 }
 
-// Data-chunk bytes from the last object word on (only units that reach it):
-// BE(packed) for the partial word, BE(m) for splitVector padding words.
 template <int K>
 __device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uint64_t L, uint64_t col0, uint64_t b,
                                               int ncol, const ObjWords& ow, uint32_t m, const uint32_t (&x)[K][4]) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const uint64_t w0 = (uint64_t)j * L + col0 + b;
-    if (w0 + ncol < ow.nw) continue;
-    uint32_t fix[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) fix[c] = be(w0 + c >= ow.nw ? m : x[j][c] ^ m);
-    uint8_t* d = slot + (uint64_t)j * chunk + 4 * b;
-    if (ncol == 4) {
-      const u32x4 v = {fix[0], fix[1], fix[2], fix[3]};
-      *reinterpret_cast<u32x4*>(d) = v;
-    } else {
-      *reinterpret_cast<uint32_t*>(d) = fix[0];
-    }
-  }
+  for (int j = 0; j < K; ++j) fix_data_tail_one(slot, chunk, L, col0, j, b, ncol, ow, m, x[j]);
 }
 
 // MODE 0: speculative encode with m = 0, OR-ing MapToGF's flag bits into
@@ -333,6 +342,165 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
       uint32_t x[K][4];
       load_chunk_symbols<K>(slot, ioff, b, 1, m, x);
       rows_out<K>(x, rows, coeff, out_idx, slot, chunk, 4 * b, m, 1);
+    }
+  }
+}
+
+// ---- wide k (need > 16): the byte kernels in 16-chunk form ------------------
+// Same column walk as rs_apply_wide_kernel (4 columns per lane, one unit per
+// step), with the byte<->symbol transforms of the kernels above: inputs in
+// chunks of 16 data chunks, outputs in blocks of RB rows, a canonical 32-bit
+// running residue per row and column.
+
+// One chunk of up to 16 row coefficients applied on top of acc (exact, folded).
+__device__ __forceinline__ void wide_mac_chunk(const uint32_t (&x)[16][4], const u32x16& c, uint32_t (&acc)[4]) {
+  uint64_t lo0 = acc[0], lo1 = acc[1], lo2 = acc[2], lo3 = acc[3];
+  uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j][0], x[j][1], x[j][2], x[j][3], c[j]);
+  acc[0] = fold96(lo0, hi0);
+  acc[1] = fold96(lo1, hi1);
+  acc[2] = fold96(lo2, hi2);
+  acc[3] = fold96(lo3, hi3);
+}
+
+// MODE as in encode_bytes_kernel.  Column tails (past the last whole vector
+// of the window) go one column per lane with ncol = 1.
+template <int RB, int MODE>
+__global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping) {
+  constexpr int KC = 16;
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  const uint64_t nunits = nvec + (ncols & 3);  // whole vectors, then one unit per tail column
+  constexpr bool F = MODE == 0;
+  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+    uint32_t m = 0;
+    if constexpr (MODE == 1) {
+      m = mapping[obj];
+      if (m == 0 || flags[obj] != 0) continue;
+    }
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;
+    uint8_t* const par = slot + (uint64_t)k * chunk;
+    Flags fl;
+    for (uint64_t g = wave * 64 + lane; g - lane < nunits; g += nwaves * 64) {
+      const bool valid = g < nunits;
+      const bool vec = g < nvec;
+      const int ncol = vec ? 4 : 1;
+      const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
+      for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
+        uint32_t acc[RB][4];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
+        for (uint32_t j0 = 0; j0 < k; j0 += KC) {
+          uint32_t x[KC][4];
+#pragma unroll
+          for (int j = 0; j < KC; ++j) {
+            x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0;
+            if (valid && j0 + j < k) {
+              if (F && r0 == 0)
+                load_data_symbol<false, true>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], &fl);
+              else
+                load_data_symbol<false, false>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], nullptr);
+              if (r0 == 0) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j]);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+            if (r0 + i < rows)
+              wide_mac_chunk(x, *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0), acc[i]);
+        }
+        if (valid) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            if (r0 + i < rows) {
+              uint8_t* dst = par + (uint64_t)out_idx[r0 + i] * chunk + 4 * b;
+              if (vec) {
+                const u32x4 v = {be(acc[i][0] ^ m), be(acc[i][1] ^ m), be(acc[i][2] ^ m), be(acc[i][3] ^ m)};
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+              } else {
+                *reinterpret_cast<uint32_t*>(dst) = be(acc[i][0] ^ m);
+              }
+            }
+          }
+        }
+      }
+    }
+    if constexpr (F) {
+      const uint32_t f = fl.bits();
+      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+      if (wf && lane == 0) atomicOr(&flags[obj], wf);
+    }
+  }
+}
+
+template <int RB>
+__global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
+    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping) {
+  constexpr int KC = 16;
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const uint64_t chunk = 4 * L;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  const uint64_t nunits = nvec + (ncols & 3);
+  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+    const uint32_t m = mapping[obj];
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;
+    for (uint64_t g = wave * 64 + lane; g - lane < nunits; g += nwaves * 64) {
+      const bool valid = g < nunits;
+      const bool vec = g < nvec;
+      const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
+      for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
+        uint32_t acc[RB][4];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
+        for (uint32_t j0 = 0; j0 < k; j0 += KC) {
+          uint32_t x[KC][4];
+#pragma unroll
+          for (int j = 0; j < KC; ++j) {
+            x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0;
+            if (valid && j0 + j < k) {
+              const uint8_t* src = slot + (uint64_t)in_idx[j0 + j] * chunk + 4 * b;
+              if (vec) {
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+                x[j][0] = be(v.x) ^ m, x[j][1] = be(v.y) ^ m, x[j][2] = be(v.z) ^ m, x[j][3] = be(v.w) ^ m;
+              } else {
+                x[j][0] = be(*reinterpret_cast<const uint32_t*>(src)) ^ m;
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+            if (r0 + i < rows)
+              wide_mac_chunk(x, *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0), acc[i]);
+        }
+        if (valid) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i) {
+            if (r0 + i < rows) {
+              uint8_t* dst = slot + (uint64_t)out_idx[r0 + i] * chunk + 4 * b;
+              if (vec) {
+                const u32x4 v = {be(acc[i][0] ^ m), be(acc[i][1] ^ m), be(acc[i][2] ^ m), be(acc[i][3] ^ m)};
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+              } else {
+                *reinterpret_cast<uint32_t*>(dst) = be(acc[i][0] ^ m);
+              }
+            }
+          }
+        }
+      }
     }
   }
 }

@@ -839,7 +839,7 @@ static uint64_t slot_L(uint64_t S, uint32_t need) { return ((S + 3) / 4 + need -
 static int check_slots(const slime_rs_plan* plan, const uint8_t* slots, uint64_t slot_stride, uint64_t L,
                        uint32_t first_out, const char* what) {
   if (!plan || !slots) return fail(Status::InvalidArg, std::string(what) + ": null plan or slots");
-  if (plan->k == 0 || plan->k > 16) return fail(Status::InvalidArg, std::string(what) + ": need must be 1..16");
+  if (plan->k == 0) return fail(Status::InvalidArg, std::string(what) + ": empty plan");
   const uint64_t chunk = 4 * L;
   uint64_t hi = first_out + plan->out_max;
   for (uint32_t j = 0; j < plan->k; ++j) hi = std::max<uint64_t>(hi, plan->in_idx_host[j]);
@@ -1138,8 +1138,7 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
                           uint32_t* mapping) {
   if (!mapping) return fail(Status::InvalidArg, "write_chunks: null mapping");
   *mapping = 0;
-  if (need < 1 || need > 16 || total <= need)
-    return fail(Status::InvalidArg, "write_chunks: need must be 1..16 and total > need");
+  if (need < 1 || total <= need) return fail(Status::InvalidArg, "write_chunks: need must be >= 1 and total > need");
   const uint64_t L = slot_L(size, (uint32_t)need);
   if (L == 0) return 0;  // MapToGF(empty) = (0, []): every chunk is empty
   if (!data || !chunks) return fail(Status::InvalidArg, "write_chunks: null buffer");
@@ -1227,7 +1226,6 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   if (need == 0) return status_of(Status::Empty, "RecoverData");
   if (!chunks || !indices) return fail(Status::InvalidArg, "reconstruct: bad args");
   if (int rc = check_survivors(need, indices)) return rc;
-  if (need > 16) return fail(Status::InvalidArg, "reconstruct: need must be <= 16");
   if (chunk_bytes % 4) return fail(Status::InvalidArg, "reconstruct: chunk_bytes must be a multiple of 4");
   if (size && !out) return fail(Status::InvalidArg, "reconstruct: null out");
   const uint64_t L = chunk_bytes / 4, body_bytes = (uint64_t)need * chunk_bytes, got = std::min(size, body_bytes);

@@ -491,7 +491,7 @@ def _make_slots(torch, objs, need, total, extra=0):
     return torch.from_numpy(host).cuda(), L, chunk, stride
 
 
-@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20)])
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20), (17, 20), (33, 50)])
 @pytest.mark.parametrize("S", [1, 3, 4, 5, 31, 32, 33, 1000, 4096, 65537, 1 << 20])
 def test_encode_objects_matches_write_chunks(torch_dev, need, total, S):
     torch = torch_dev
@@ -548,7 +548,7 @@ def test_encode_objects_random_fallback(torch_dev):
 
 
 @pytest.mark.parametrize("need,total,S", [(4, 6, 5000), (8, 12, 1 << 20), (8, 12, 999999), (10, 14, 77777),
-                                          (2, 3, 3)])
+                                          (2, 3, 3), (20, 24, 300001), (40, 60, 123457)])
 def test_decode_objects_repairs_chunks(torch_dev, need, total, S):
     torch = torch_dev
     from slime_amd import device as D
@@ -598,7 +598,7 @@ def _oracle_reconstruct(chunks, have, mapping, need, size):
     return (out + bytes(max(0, size - len(out))))[:size]
 
 
-@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (16, 20)])
+@pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (16, 20), (20, 24), (40, 56)])
 @pytest.mark.parametrize("S", [1, 3, 4, 5, 33, 4096, 100003, 3 * (8 << 20) + 13])
 @pytest.mark.parametrize("kind", ["plain", "high", "fallback"])
 def test_write_chunks_and_reconstruct_vs_oracle(need, total, S, kind):
