@@ -221,8 +221,10 @@ def main():
         # Control plane only (barrier + max-over-ranks timing): objects are
         # independent, the data path exchanges nothing between GPUs.
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = local
+    # One rank per GPU.  With fewer visible GPUs than local ranks (a 2-rank
+    # rehearsal on a 1-GPU box) ranks share devices round-robin.
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
 
     need, total = args.need, args.total
     r = total - need

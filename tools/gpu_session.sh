@@ -135,6 +135,14 @@ if has widek; then  # k > 16: the generic one-column kernel
   run widek_32_40 300 python bench.py --need 32 --total 40 --object-mib 256 --objects 32 --erase 0,1,2,3,4,5,6,7 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
   run widek_64_80 300 python bench.py --need 64 --total 80 --object-mib 256 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
 fi
+if has ranks2; then  # the N > 1 path end to end: 2 ranks sharing this box's one GPU
+  run ranks2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --objects 64
+fi
+if has widebytes; then  # fused byte path at need > 16
+  run widebytes_20_24 300 python bench.py --need 20 --total 24 --object-mib 256 --objects 32 --steps 3 --cpu-baseline 0 --host-path 0
+  run widebytes_40_56 300 python bench.py --need 40 --total 56 --object-mib 256 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --cpu-baseline 0 --host-path 0
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
