@@ -54,28 +54,36 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// need > 16: the 16-chunk byte kernels (rs_bytes_kernel.hpp, "wide k").
+// need > 16: the chunked byte kernels (rs_bytes_kernel.hpp, "wide k"):
+// every input in registers up to need = 32, 16-chunk steps above.
 constexpr int kWideRows = 8;
 
-hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) {
+template <int KC>
+hipError_t enc_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const dim3 g = grid_for(ncols, a.phase == 0 ? a.nobj : 1);
   if (a.phase == 0)
-    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<kWideRows, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride,
-                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping);
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 0>), g, dim3(kBlock), 0, s, a.slots,
+                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
+                       a.mapping);
   else
-    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<kWideRows, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride,
-                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping);
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 1>), g, dim3(kBlock), 0, s, a.slots,
+                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
+                       a.mapping);
   return hipGetLastError();
 }
 
-hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
+template <int KC>
+hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<kWideRows>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<KC, kWideRows>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s,
                      a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
                      a.mapping);
   return hipGetLastError();
 }
+
+hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) { return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s); }
+hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) { return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s); }
 
 #define SLIME_K_SWITCH(fn)               \
   switch (a.k) {                         \

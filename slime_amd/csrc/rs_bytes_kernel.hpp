@@ -352,12 +352,23 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
 // chunks of 16 data chunks, outputs in blocks of RB rows, a canonical 32-bit
 // running residue per row and column.
 
-// One chunk of up to 16 row coefficients applied on top of acc (exact, folded).
-__device__ __forceinline__ void wide_mac_chunk(const uint32_t (&x)[16][4], const u32x16& c, uint32_t (&acc)[4]) {
+// One chunk of KC inputs (KC a multiple of 16; coefficients past k are zero
+// in the plan table) applied on top of a row's running residues, exactly,
+// with one fold.  `crow` points at the row's coefficients for the chunk.
+template <int KC>
+__device__ __forceinline__ void wide_mac_chunk(const uint32_t (&x)[KC][4], const uint32_t* __restrict__ crow,
+                                               uint32_t j0, uint32_t k, uint32_t (&acc)[4]) {
   uint64_t lo0 = acc[0], lo1 = acc[1], lo2 = acc[2], lo3 = acc[3];
   uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j][0], x[j][1], x[j][2], x[j][3], c[j]);
+  for (int h = 0; h < KC; h += 16) {
+    if (j0 + h < k) {
+      const u32x16 c = *reinterpret_cast<const u32x16*>(crow + h);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[h + j][0], x[h + j][1], x[h + j][2], x[h + j][3], c[j]);
+    }
+  }
   acc[0] = fold96(lo0, hi0);
   acc[1] = fold96(lo1, hi1);
   acc[2] = fold96(lo2, hi2);
@@ -366,15 +377,16 @@ __device__ __forceinline__ void wide_mac_chunk(const uint32_t (&x)[16][4], const
 
 // MODE as in encode_bytes_kernel.  Column tails (past the last whole vector
 // of the window) go one column per lane with ncol = 1.
-template <int RB, int MODE>
+// KC = 32 holds every input of a need <= 32 code in registers at once.
+template <int KC, int RB, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping) {
-  constexpr int KC = 16;
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -395,6 +407,11 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
       const bool vec = g < nvec;
       const int ncol = vec ? 4 : 1;
       const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
+      // Interior step (wave-uniform): every data word the step touches is a
+      // whole object word, below the object's last word.
+      const uint64_t gw = g - lane;
+      const bool interior =
+          gw + 64 <= nvec && (uint64_t)(k - 1) * L + col0 + ((gw + 64) << 2) < first_tail_word;
       for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
         uint32_t acc[RB][4];
 #pragma unroll
@@ -405,17 +422,23 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
           for (int j = 0; j < KC; ++j) {
             x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0;
             if (valid && j0 + j < k) {
-              if (F && r0 == 0)
-                load_data_symbol<false, true>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], &fl);
-              else
-                load_data_symbol<false, false>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], nullptr);
-              if (r0 == 0) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j]);
+              if (interior) {
+                if (F && r0 == 0)
+                  load_data_symbol<true, true>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], &fl);
+                else
+                  load_data_symbol<true, false>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], nullptr);
+              } else {
+                if (F && r0 == 0)
+                  load_data_symbol<false, true>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], &fl);
+                else
+                  load_data_symbol<false, false>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], nullptr);
+                if (r0 == 0) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j]);
+              }
             }
           }
 #pragma unroll
           for (int i = 0; i < RB; ++i)
-            if (r0 + i < rows)
-              wide_mac_chunk(x, *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0), acc[i]);
+            if (r0 + i < rows) wide_mac_chunk<KC>(x, coeff + (uint64_t)(r0 + i) * cs + j0, j0, k, acc[i]);
         }
         if (valid) {
 #pragma unroll
@@ -442,12 +465,11 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
   }
 }
 
-template <int RB>
+template <int KC, int RB>
 __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping) {
-  constexpr int KC = 16;
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
@@ -483,8 +505,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
           }
 #pragma unroll
           for (int i = 0; i < RB; ++i)
-            if (r0 + i < rows)
-              wide_mac_chunk(x, *reinterpret_cast<const u32x16*>(coeff + (uint64_t)(r0 + i) * cs + j0), acc[i]);
+            if (r0 + i < rows) wide_mac_chunk<KC>(x, coeff + (uint64_t)(r0 + i) * cs + j0, j0, k, acc[i]);
         }
         if (valid) {
 #pragma unroll
