@@ -143,6 +143,23 @@ if has widebytes; then  # fused byte path at need > 16
   run widebytes_20_24 300 python bench.py --need 20 --total 24 --object-mib 256 --objects 32 --steps 3 --cpu-baseline 0 --host-path 0
   run widebytes_40_56 300 python bench.py --need 40 --total 56 --object-mib 256 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --cpu-baseline 0 --host-path 0
 fi
+if has sizes; then  # object size vs k: is 10/14 slower because of k or because of 1 GiB objects?
+  run sizes_10_14_256m 300 python bench.py --need 10 --total 14 --object-mib 256 --objects 128 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run sizes_8_12_1g 300 python bench.py --need 8 --total 12 --object-mib 1024 --objects 32 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run sizes_10_14_1g 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 32 --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  run sizes_8_12_256m 300 python bench.py --steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0
+fi
+if has clocks; then  # box state under sustained load: which clocks/limits differ on slow-placement boxes?
+  ( timeout -k 5 40 python tools/sustained.py --seconds 12 --idle 1 > "$OUT/clocks_load.log" 2>&1 ) &
+  LOADPID=$!
+  sleep 8
+  timeout -k 5 30 rocm-smi --showclocks --showperflevel --showpower --showmaxpower --showtemp --showmemuse > "$OUT/clocks_smi_load.log" 2>&1
+  timeout -k 5 40 amd-smi metric -g 0 > "$OUT/clocks_amdsmi_load.log" 2>&1
+  wait $LOADPID
+  timeout -k 5 40 amd-smi static -g 0 > "$OUT/clocks_amdsmi_static.log" 2>&1
+  timeout -k 5 40 amd-smi partition > "$OUT/clocks_partition.log" 2>&1 || true
+  echo "=== clocks done" | tee -a "$OUT/session.log"
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
