@@ -212,6 +212,25 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
                     "PCIe-inclusive; not `value`"}
 
 
+def board_info(dev: int) -> dict | None:
+    """Board model and HBM vendor of `dev` (amd-smi), so a bench line can be
+    matched with the board it ran on (placement modes differ between boards,
+    DESIGN.md).  None when amd-smi is unavailable."""
+    import subprocess
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}.0"
+        out = subprocess.run(["amd-smi", "static", "-g", bdf], capture_output=True, text=True, timeout=30).stdout
+    except Exception:  # noqa: BLE001 - diagnostics only
+        return None
+    info = {"bdf": bdf}
+    for line in out.splitlines():
+        key, _, val = line.strip().partition(": ")
+        if key in ("MODEL_NUMBER", "PRODUCT_NAME", "OAM_ID") or (key == "VENDOR" and "HBM" not in val and val):
+            info.setdefault(key.lower(), val.strip())
+    return info if len(info) > 1 else None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -356,6 +375,7 @@ def main():
             "cpu_baseline": None,
             "object_bytes_path": bytes_path,
         }
+        line["device"] = board_info(dev)
         if world == 1 and args.host_path:
             line["host_path"] = host_leg(need, total, erase)
         if world == 1 and args.cpu_baseline:

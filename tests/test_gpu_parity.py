@@ -669,3 +669,41 @@ def test_object_entry_points_reuse_caller_buffers():
     dst = np.full(len(obj) + 5, 0xCD, dtype=np.uint8)
     got = objects.reconstruct([chunks[i] for i in (1, 3, 4, 5)], [1, 3, 4, 5], m, len(obj), out=dst)
     assert got.ctypes.data == dst.ctypes.data and got.tobytes() == obj and (dst[len(obj):] == 0xCD).all()
+
+
+def test_fuzz_random_shapes_and_layouts(torch_dev):
+    """Seeded random shapes across every kernel form (k = 1..16 templates, the
+    wide kernel, column segments, padded and misaligned strides): encode in
+    place, then rebuild a random erasure set into a separate buffer."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = random.Random(0xF022)
+    for case in range(48):
+        need = rng.choice([1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 15, 16, 17, 24, 31, 33, 40])
+        total = need + rng.randint(1, min(12, 100 - need))
+        L = rng.choice([1, 2, 3, 5, 63, 64, 255, 1024, 4099, 8192 + rng.randint(0, 7), rng.randint(1, 30000)])
+        nobj = rng.randint(1, 5)
+        pad = rng.choice([0, 0, 1, 3, 4, 64])
+        off = rng.randint(0, 3)
+        SS = L + pad
+        lay = D.layout_of(total, L, SS)
+        buf = torch.empty(off + nobj * total * SS, dtype=torch.int32, device="cuda")
+        D.fill_symbols(buf, seed=case)
+        D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, src_offset=off, dst_offset=off + need * SS)
+        torch.cuda.synchronize()
+        h = buf.cpu().numpy().view(np.uint32)[off:].reshape(nobj, total, SS)[:, :, :L]
+        for o in range(nobj):
+            ref = np.ascontiguousarray(h[o].copy())
+            OC.encode_object(ref, need, total)
+            assert np.array_equal(h[o], ref), (case, need, total, L, nobj, pad, off, o)
+        e = rng.randint(1, total - need)
+        erase = sorted(rng.sample(range(total), e))
+        have = [i for i in range(total) if i not in erase][:need]
+        out = torch.zeros(nobj * e * L + 1, dtype=torch.int32, device="cuda")
+        D.Plan.reconstruct(need, total, have, erase)(buf, lay, out, D.layout_of(e, L), L, nobj, src_offset=off,
+                                                     dst_offset=1)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)[1:].reshape(nobj, e, L)
+        for o in range(nobj):
+            for i, t in enumerate(erase):
+                assert np.array_equal(got[o, i], h[o, t]), (case, need, total, L, erase, o, t)

@@ -31,6 +31,7 @@ run() {  # run <name> <limit-seconds> <command...>
 has() { for s in "${STEPS[@]}"; do [ "$s" = "$1" ] && return 0; done; return 1; }
 
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > "$OUT/device.txt" || true
+timeout 30 amd-smi static -g 0 2>/dev/null | grep -E "MODEL_NUMBER|PRODUCT_NAME|VENDOR: |OAM_ID" >> "$OUT/device.txt" || true
 nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
 
 has tests && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
