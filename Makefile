@@ -11,7 +11,14 @@ LIB      := slime_amd/lib/libslime_rs.so
 OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_bytes.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
-all: $(LIB) oracle
+CXXTEST  := tests/cpp/rs_host_test
+
+all: $(LIB) oracle $(CXXTEST)
+
+# C++ host mirror of the Go API (include/slime_rs.hpp) and its parity tests.
+$(CXXTEST): tests/cpp/rs_host_test.cpp include/slime_rs.hpp include/slime_rs.h $(LIB)
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
+	  -Wl,-rpath,'$$ORIGIN/../../slime_amd/lib'
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -30,7 +37,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(CXXTEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,0 +1,244 @@
+// slime_rs.hpp — C++ host mirror of encryptio/slime's Go packages
+// internal/rs and internal/rs/gf over the C-ABI in slime_rs.h.
+//
+// The reference is compiled Go; with no Go toolchain in this image the
+// testable host side above the C-ABI is this header (the cgo shim in go/ is
+// the maintainer's drop-in).  Same names, argument meaning and error
+// behaviour as the reference:
+//   Go []uint32 / [][]uint32  ->  slime::rs::Vector / slime::rs::Matrix
+//   Go []byte                 ->  std::vector<uint8_t>
+//   Go panic(msg)             ->  throw slime::Panic (what() = the reference's text)
+// Header-only; link with -lslime_rs.
+#ifndef SLIME_RS_HPP
+#define SLIME_RS_HPP
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "slime_rs.h"
+
+namespace slime {
+
+// Where the reference panics (status 1..8): what() is the reference's panic
+// message, or Go's runtime "index out of range" text for status 8.
+struct Panic : std::runtime_error {
+  int status;
+  Panic(int st, const std::string& msg) : std::runtime_error(msg), status(st) {}
+};
+
+// Any other failure of the library: no device, HIP error, misuse.
+struct NativeError : std::runtime_error {
+  int status;
+  NativeError(int st, const std::string& msg) : std::runtime_error(msg), status(st) {}
+};
+
+namespace detail {
+inline void check(int rc) {
+  if (rc == SLIME_RS_OK) return;
+  const std::string last = slime_rs_last_error();
+  if (rc >= SLIME_RS_ERR_VARYING_LENGTH && rc <= SLIME_RS_ERR_INDEX_RANGE) {
+    std::string msg = slime_rs_status_string(rc);
+    if (rc == SLIME_RS_ERR_INDEX_RANGE && !last.empty()) msg = last;
+    throw Panic(rc, msg);
+  }
+  throw NativeError(rc, std::string("slime_rs error ") + std::to_string(rc) + ": " + last);
+}
+}  // namespace detail
+
+namespace gf {
+
+// gf.MaxVal (internal/rs/gf/map.go:7)
+constexpr uint32_t MaxVal = SLIME_GF_MAXVAL;
+
+// gf.MInverse (internal/rs/gf/gf.go:5), gf.Raise (gf.go:46)
+inline uint32_t MInverse(uint32_t in) { return slime_gf_minverse(in); }
+inline uint32_t Raise(uint32_t x, uint32_t n) { return slime_gf_raise(x, n); }
+
+// gf.MapToGF (internal/rs/gf/map.go:15): (mapping, words).
+inline std::pair<uint32_t, std::vector<uint32_t>> MapToGF(const std::vector<uint8_t>& in) {
+  std::vector<uint32_t> out((in.size() + 3) / 4);
+  uint32_t mapping = 0;
+  detail::check(slime_gf_map_to_gf(in.empty() ? nullptr : in.data(), in.size(), &mapping,
+                                   out.empty() ? nullptr : out.data()));
+  return {mapping, std::move(out)};
+}
+
+// gf.MapToGFWith (internal/rs/gf/map.go:74)
+inline std::vector<uint32_t> MapToGFWith(const std::vector<uint8_t>& in, uint32_t n) {
+  std::vector<uint32_t> out((in.size() + 3) / 4);
+  detail::check(slime_gf_map_to_gf_with(in.empty() ? nullptr : in.data(), in.size(), n,
+                                        out.empty() ? nullptr : out.data()));
+  return out;
+}
+
+// gf.MapFromGF (internal/rs/gf/map.go:103)
+inline std::vector<uint8_t> MapFromGF(uint32_t inn, const std::vector<uint32_t>& inv) {
+  std::vector<uint8_t> out(4 * inv.size());
+  detail::check(slime_gf_map_from_gf(inn, inv.empty() ? nullptr : inv.data(), inv.size(),
+                                     out.empty() ? nullptr : out.data()));
+  return out;
+}
+
+}  // namespace gf
+
+namespace rs {
+
+using Vector = std::vector<uint32_t>;
+using Matrix = std::vector<Vector>;
+
+namespace detail {
+inline Matrix rows_of(const uint32_t* flat, int rows, int cols) {
+  Matrix m((size_t)rows, Vector((size_t)cols));
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) m[i][j] = flat[(size_t)i * cols + j];
+  return m;
+}
+inline Vector flat_of(const Matrix& m) {
+  Vector f;
+  for (const Vector& r : m) f.insert(f.end(), r.begin(), r.end());
+  return f;
+}
+struct Rows {  // pointer + length arrays for the C-ABI (C never keeps them)
+  std::vector<const uint32_t*> ptrs;
+  std::vector<uint64_t> lens;
+  explicit Rows(const Matrix& m) {
+    for (const Vector& r : m) {
+      ptrs.push_back(r.data());
+      lens.push_back(r.size());
+    }
+  }
+};
+}  // namespace detail
+
+// vandermondeMatrix (internal/rs/matrix.go:8): (d+p) x d, m[i][j] = (j+1)^i.
+inline Matrix vandermondeMatrix(int d, int p) {
+  Vector f((size_t)(d + p) * (size_t)(d > 0 ? d : 0));
+  slime::detail::check(slime_rs_vandermonde_matrix(d, p, f.data()));
+  return detail::rows_of(f.data(), d + p, d);
+}
+
+// ParityMatrix (internal/rs/matrix.go:27): systematic (d+p) x d code matrix.
+inline Matrix ParityMatrix(int d, int p) {
+  Vector f((size_t)(d + p) * (size_t)(d > 0 ? d : 0));
+  slime::detail::check(slime_rs_parity_matrix(d, p, f.data()));
+  return detail::rows_of(f.data(), d + p, d);
+}
+
+// ParityMatrixCached (internal/rs/matrixcache.go:11): one shared, read-only
+// matrix per (d, p) for the life of the process.
+inline const Matrix& ParityMatrixCached(int d, int p) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, std::unique_ptr<Matrix>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({d, p});
+  if (it != cache.end()) return *it->second;
+  const uint32_t* flat = nullptr;
+  slime::detail::check(slime_rs_parity_matrix_cached(d, p, &flat));
+  auto m = std::make_unique<Matrix>(detail::rows_of(flat, d + p, d));
+  const Matrix& ref = *m;
+  cache.emplace(std::make_pair(d, p), std::move(m));
+  return ref;
+}
+
+// solveSubIdentity (internal/rs/matrix.go:35), in place.
+inline void solveSubIdentity(Matrix& m) {
+  if (m.empty()) return;
+  Vector f = detail::flat_of(m);
+  slime::detail::check(slime_rs_solve_sub_identity(f.data(), (int)m.size(), (int)m[0].size()));
+  m = detail::rows_of(f.data(), (int)m.size(), (int)m[0].size());
+}
+
+// cloneMatrix (internal/rs/matrix.go:99)
+inline Matrix cloneMatrix(const Matrix& m) { return m; }
+
+// invertMatrix (internal/rs/matrix.go:112): inverse of a d x d matrix.
+inline Matrix invertMatrix(const Matrix& m) {
+  const int d = (int)m.size();
+  Vector f = detail::flat_of(m), inv((size_t)d * d);
+  slime::detail::check(slime_rs_invert_matrix(f.data(), d, inv.data()));
+  return detail::rows_of(inv.data(), d, d);
+}
+
+// CreateParity (internal/rs/vector.go:18): code row `index` of `data`,
+// computed on the GPU.  Like Go, `out` is reused when its capacity holds
+// len(data[0]) symbols, and the slice actually used is returned.
+inline Vector CreateParity(const Matrix& data, int index, Vector out = {}) {
+  detail::Rows rows(data);
+  const size_t L = data.empty() ? 0 : data[0].size();
+  bool same = !data.empty();
+  for (const Vector& r : data) same = same && r.size() == L;
+  if (same) {
+    if (out.capacity() < L) out = Vector();
+    out.resize(L);
+  }
+  slime::detail::check(slime_rs_create_parity(rows.ptrs.data(), rows.lens.data(), (int)data.size(), index,
+                                              same ? out.data() : nullptr));
+  return out;
+}
+
+// All total-len(data) parity rows in one GPU pass (the batched form of the
+// caller's loop, multi_store.go:528-531).  Additive: no reference counterpart.
+inline Matrix CreateParities(const Matrix& data, int total) {
+  detail::Rows rows(data);
+  const size_t L = data.empty() ? 0 : data[0].size();
+  const int r = total - (int)data.size();
+  Matrix out(r > 0 ? (size_t)r : 0, Vector(L));
+  std::vector<uint32_t*> optrs;
+  for (Vector& o : out) optrs.push_back(o.data());
+  slime::detail::check(slime_rs_create_parities(rows.ptrs.data(), rows.lens.data(), (int)data.size(), total,
+                                                optrs.empty() ? nullptr : optrs.data()));
+  return out;
+}
+
+// RecoverData (internal/rs/vector.go:50): every data row from any len(chunks)
+// code rows with the given indices.
+inline Matrix RecoverData(const Matrix& chunks, const std::vector<int>& indices) {
+  detail::Rows rows(chunks);
+  const size_t L = chunks.empty() ? 0 : chunks[0].size();
+  Matrix out(chunks.size(), Vector(L));
+  std::vector<uint32_t*> optrs;
+  for (Vector& o : out) optrs.push_back(o.data());
+  slime::detail::check(slime_rs_recover_data(rows.ptrs.data(), rows.lens.data(), (int)chunks.size(),
+                                             indices.empty() ? nullptr : indices.data(), (int)indices.size(),
+                                             optrs.empty() ? nullptr : optrs.data()));
+  return out;
+}
+
+// The data path of Multi.writeChunks (multi_store.go:526-531, :554) in one
+// fused device pass: (MappingValue, chunk bytes).  Additive.
+inline std::pair<uint32_t, std::vector<std::vector<uint8_t>>> WriteChunks(const std::vector<uint8_t>& data,
+                                                                         int need, int total) {
+  const uint64_t cb = slime_rs_chunk_size(data.size(), need);
+  std::vector<std::vector<uint8_t>> chunks(total > 0 ? (size_t)total : 0, std::vector<uint8_t>(cb));
+  std::vector<uint8_t*> ptrs;
+  for (auto& c : chunks) ptrs.push_back(c.data());
+  uint32_t mapping = 0;
+  slime::detail::check(slime_rs_write_chunks(data.empty() ? nullptr : data.data(), data.size(), need, total,
+                                             ptrs.empty() ? nullptr : ptrs.data(), &mapping));
+  return {mapping, std::move(chunks)};
+}
+
+// The slow path of Multi.reconstruct (multi_store.go:215-241): the object's
+// `size` bytes from `need` chunks and their indices.  Additive.
+inline std::vector<uint8_t> ReconstructObject(const std::vector<std::vector<uint8_t>>& chunks,
+                                              const std::vector<int>& indices, uint32_t mapping, uint64_t size) {
+  std::vector<const uint8_t*> ptrs;
+  for (const auto& c : chunks) ptrs.push_back(c.data());
+  std::vector<uint8_t> out(size);
+  slime::detail::check(slime_rs_reconstruct(ptrs.empty() ? nullptr : ptrs.data(),
+                                            indices.empty() ? nullptr : indices.data(), (int)chunks.size(),
+                                            chunks.empty() ? 0 : chunks[0].size(), mapping, size,
+                                            out.empty() ? nullptr : out.data()));
+  return out;
+}
+
+}  // namespace rs
+}  // namespace slime
+
+#endif  // SLIME_RS_HPP
