@@ -126,6 +126,7 @@ if has slowsegs; then  # on a slow allocation (if the box has one): do more inde
   run slowsegs_enc 400 python tools/apply_variants.py --hunt slow --variants 8,11 --blocks 512,1024 --nseg 1,2,4,8,16
   run slowsegs_dec 400 python tools/apply_variants.py --hunt slow --decode 1 --separate 0 --variants 8 --blocks 512,1024 --nseg 1,2,4,8,16
 fi
+has mall && run mall 300 bash -c "make ubench >/dev/null && python tools/mall_probe.py"
 if has offsets; then  # batch base offset inside one allocation; once plain, once under the profiler
   run offsets_plain 300 python tools/offset_probe.py
   run offsets_prof 300 rocprofv3 --kernel-trace -d "$OUT/offsets_prof" -o run --output-format csv -- python3 tools/offset_probe.py
@@ -160,6 +161,10 @@ if has clocks; then  # box state under sustained load: which clocks/limits diffe
   timeout -k 5 40 amd-smi static -g 0 > "$OUT/clocks_amdsmi_static.log" 2>&1
   timeout -k 5 40 amd-smi partition > "$OUT/clocks_partition.log" 2>&1 || true
   echo "=== clocks done" | tee -a "$OUT/session.log"
+fi
+if has slowsweep; then  # kernel knobs on whatever box this is (the log names its placement mode)
+  run sweep_enc 400 python tools/apply_variants.py --variants 8,2,6,11 --blocks 256,512,1024,2048 --nseg 1,4,16
+  run sweep_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 8,2,6,11 --blocks 256,512,1024,2048 --nseg 1,4,16
 fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
