@@ -34,6 +34,11 @@ inline uint32_t coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 
+// Column segments per object for a launch over nobj objects of ncols
+// columns (the apply and byte kernels cut each object into this many
+// contiguous segments scheduled like separate objects).
+uint32_t object_segments(uint32_t nobj, uint64_t ncols);
+
 // --- fused byte-domain encode/decode over object slots (rs_bytes.hip) --------
 // Slot o at slots + o*slot_stride bytes; chunk c at slot + c*4L.  coeff /
 // in_idx / out_idx are a plan's device tables.  Encode: phase 0 = speculative

@@ -22,6 +22,22 @@
 #include "rs_apply_kernel.hpp"
 
 namespace slime {
+
+// Column segments per object (rs_apply_kernel): enough that the batch has
+// about 256 independent object segments in flight -- 128 x 256 MiB objects
+// reach 6.1 TB/s unsegmented, 32 x 64 MiB objects need 8 segments each to get
+// from 5.08 to 5.54 TB/s (profiles/r01/segs/) -- and at least 1024 vectors
+// (4 U=4 tiles) per segment.  Env SLIME_RS_SEGMENTS forces a count (tuning).
+uint32_t object_segments(uint32_t nobj, uint64_t ncols) {
+  static const uint64_t forced = [] {
+    const char* e = getenv("SLIME_RS_SEGMENTS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (uint64_t)v : 0ull;
+  }();
+  const uint64_t want = forced ? forced : (256 + nobj - 1) / nobj;
+  const uint64_t max_s = (ncols >> 2) / 1024 ? (ncols >> 2) / 1024 : 1;
+  return (uint32_t)(want < max_s ? want : max_s);
+}
 namespace {
 
 using apply::kBlock;
@@ -58,17 +74,6 @@ const Geometry& geometry() {
   static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
   return g;
 }
-// Column segments per object (rs_apply_kernel): enough that the batch has
-// about 256 independent object segments in flight -- 128 x 256 MiB objects
-// reach 6.1 TB/s unsegmented, 32 x 64 MiB objects need 8 segments each to get
-// from 5.08 to 5.54 TB/s (profiles/r01/segs/) -- and at least 1024 vectors
-// (4 U=4 tiles) per segment.  Env SLIME_RS_SEGMENTS forces a count (tuning).
-uint32_t segments_for(uint32_t nobj, uint64_t ncols) {
-  static const uint64_t forced = env_u64("SLIME_RS_SEGMENTS", 0);
-  const uint64_t want = forced ? forced : (256 + nobj - 1) / nobj;
-  const uint64_t max_s = (ncols >> 2) / 1024 ? (ncols >> 2) / 1024 : 1;
-  return (uint32_t)(want < max_s ? want : max_s);
-}
 template <int K>
 constexpr uint64_t default_blocks() {
   return K >= 9 && K <= 12 ? 256 : 512;
@@ -79,7 +84,7 @@ hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   constexpr int U = unroll_for<K>();
   const uint64_t per_block = VEC && K > 0 ? 4ull * kBlock * U : (uint64_t)kBlock;
   const Geometry& geo = geometry();
-  const uint32_t nseg = VEC && K > 0 ? segments_for(a.nobj, a.ncols) : 1u;
+  const uint32_t nseg = VEC && K > 0 ? object_segments(a.nobj, a.ncols) : 1u;
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
   uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
   if (gy > 65535) gy = 65535;
@@ -104,7 +109,7 @@ hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
 template <int KC, int RB>
 hipError_t launch_wide_k(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t per_block = 4ull * kBlock;
-  const uint32_t nseg = segments_for(a.nobj, a.ncols);
+  const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
   const Geometry& geo = geometry();
   uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;

@@ -17,11 +17,12 @@ constexpr int bytes_unroll() {
   return K <= 8 ? 4 : (K <= 12 ? 2 : 1);
 }
 
-dim3 grid_for(uint64_t L, uint32_t objects_in_flight) {
-  uint64_t gy = objects_in_flight < 65535u ? objects_in_flight : 65535u;
+// 512 resident blocks over `work` object segments of about ncols/nseg columns.
+dim3 grid_for(uint64_t ncols, uint64_t work, uint32_t nseg) {
+  uint64_t gy = work < 65535u ? work : 65535u;
   if (gy < 1) gy = 1;
   uint64_t gx = (512 + gy - 1) / gy;
-  const uint64_t need = (L + 4ull * kBlock - 1) / (4ull * kBlock);
+  const uint64_t need = (ncols / nseg + 4ull * kBlock - 1) / (4ull * kBlock);
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
   return dim3((uint32_t)gx, (uint32_t)gy);
@@ -34,13 +35,15 @@ hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
   // MapToGF maps with 1<<31 (~7.5% of 256 MiB random objects), so the whole
   // grid sweeps them one after another instead of 512/nobj blocks each.
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const dim3 g = grid_for(ncols, a.phase == 0 ? a.nobj : 1);
   if (a.phase == 0) {
-    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
-                       ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+    const uint32_t nseg = object_segments(a.nobj, ncols);
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock),
+                       0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
+                       a.flags, a.mapping, nseg);
   } else {
-    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), g, dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
-                       ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping);
+    hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), grid_for(ncols, 1, 1), dim3(kBlock), 0, s, a.slots,
+                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
+                       a.mapping, 1u);
   }
   return hipGetLastError();
 }
@@ -49,8 +52,10 @@ template <int K>
 hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = bytes_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s, a.slots,
-                     a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping);
+  const uint32_t nseg = object_segments(a.nobj, ncols);
+  hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock), 0, s,
+                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx,
+                     a.mapping, nseg);
   return hipGetLastError();
 }
 
@@ -61,24 +66,26 @@ constexpr int kWideRows = 8;
 template <int KC>
 hipError_t enc_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const dim3 g = grid_for(ncols, a.phase == 0 ? a.nobj : 1);
-  if (a.phase == 0)
-    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 0>), g, dim3(kBlock), 0, s, a.slots,
-                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
-                       a.mapping);
-  else
-    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 1>), g, dim3(kBlock), 0, s, a.slots,
-                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
-                       a.mapping);
+  if (a.phase == 0) {
+    const uint32_t nseg = object_segments(a.nobj, ncols);
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 0>),
+                       grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock), 0, s, a.slots, a.slot_stride,
+                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping, nseg);
+  } else {
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 1>), grid_for(ncols, 1, 1), dim3(kBlock), 0,
+                       s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
+                       a.flags, a.mapping, 1u);
+  }
   return hipGetLastError();
 }
 
 template <int KC>
 hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<KC, kWideRows>), grid_for(ncols, a.nobj), dim3(kBlock), 0, s,
-                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
-                     a.mapping);
+  const uint32_t nseg = object_segments(a.nobj, ncols);
+  hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<KC, kWideRows>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg),
+                     dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff,
+                     a.in_idx, a.out_idx, a.mapping, nseg);
   return hipGetLastError();
 }
 

@@ -195,6 +195,27 @@ __device__ __forceinline__ void fix_data_tail(uint8_t* slot, uint64_t chunk, uin
   for (int j = 0; j < K; ++j) fix_data_tail_one(slot, chunk, L, col0, j, b, ncol, ow, m, x[j]);
 }
 
+// Work item wi of a launch = (object, column segment): each object's window
+// is cut into nseg contiguous segments of whole vectors, scheduled like
+// separate objects on blockIdx.y (rs_apply_kernel does the same), so a
+// small batch keeps many independent chunk streams in flight.  The columns
+// past the last whole vector belong to the object's last segment.
+struct Segment {
+  uint32_t obj;
+  bool last;
+  uint64_t v0, v1;  // vectors [v0, v1) of the window
+};
+__device__ __forceinline__ Segment segment_of(uint64_t wi, uint32_t nseg, uint64_t nvec) {
+  const uint64_t per = (nvec + nseg - 1) / nseg;
+  const uint32_t seg = (uint32_t)(wi % nseg);
+  Segment g;
+  g.obj = (uint32_t)(wi / nseg);
+  g.last = seg == nseg - 1;
+  g.v0 = (uint64_t)seg * per < nvec ? (uint64_t)seg * per : nvec;
+  g.v1 = g.v0 + per < nvec ? g.v0 + per : nvec;
+  return g;
+}
+
 // MODE 0: speculative encode with m = 0, OR-ing MapToGF's flag bits into
 //         flags[obj] (the caller's status array, zeroed first).
 // MODE 1: re-encode objects with mapping[obj] != 0 and status[obj] == 0.
@@ -208,18 +229,20 @@ template <int K, int U, int MODE, bool FAST = true, bool FLAGS_ON = true>
 __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping) {
+    uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping, uint32_t nseg) {
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
-  const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
   // Units whose columns reach the object's last word (or padding) need the
   // data-chunk tail fix; every other unit skips that branch.
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
-  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint64_t ntiles = (sg.v1 - sg.v0 + 64 * U - 1) / (64 * U);
     uint32_t m = 0;
     if constexpr (MODE == 1) {
       m = mapping[obj];
@@ -230,12 +253,12 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
     constexpr bool F = MODE == 0 && FLAGS_ON;
     Flags fl;
     for (uint64_t step = wave; step < ntiles; step += nwaves) {
-      const uint64_t g0 = step * (64 * U) + lane;
+      const uint64_t g0 = sg.v0 + step * (64 * U) + lane;
       // Interior step: the highest word the wave's units touch (last data
       // chunk, last unit) is below the object's last word: no checks needed.
-      const uint64_t top = (uint64_t)(K - 1) * L + col0 + ((step * (64 * U) + 64 * U) << 2);
+      const uint64_t top = (uint64_t)(K - 1) * L + col0 + ((sg.v0 + step * (64 * U) + 64 * U) << 2);
       uint32_t x[U][K][4];
-      if (FAST && top < first_tail_word && (step + 1) * (64 * U) <= nvec) {
+      if (FAST && top < first_tail_word && sg.v0 + (step + 1) * (64 * U) <= sg.v1) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
           load_data_symbols<K, true, F>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
@@ -248,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
       int n = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (g0 + 64 * u < nvec) {
+        if (g0 + 64 * u < sg.v1) {
           load_data_symbols<K, false, F>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
           n = u + 1;
         }
@@ -261,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
       }
       rows_out_units<K, U>(x, n, rows, coeff, out_idx, par, chunk, g0, m);
     }
-    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < ncols; b += nwaves * 64) {
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; sg.last && b < ncols; b += nwaves * 64) {
       uint32_t x[K][4];
       load_data_symbols<K, false, F>(slot, chunk, L, col0, b, 1, ow, m, x, &fl);
       fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
@@ -313,32 +336,34 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
                                                               const uint32_t* __restrict__ coeff,
                                                               const uint32_t* __restrict__ in_idx,
                                                               const uint32_t* __restrict__ out_idx,
-                                                              const uint32_t* __restrict__ mapping) {
+                                                              const uint32_t* __restrict__ mapping, uint32_t nseg) {
   const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
-  const uint64_t ntiles = (nvec + 64 * U - 1) / (64 * U);
-  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint64_t ntiles = (sg.v1 - sg.v0 + 64 * U - 1) / (64 * U);
     const uint32_t m = mapping[obj];
     uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
     uint64_t ioff[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * chunk;
     for (uint64_t step = wave; step < ntiles; step += nwaves) {
-      const uint64_t g0 = step * (64 * U) + lane;
+      const uint64_t g0 = sg.v0 + step * (64 * U) + lane;
       uint32_t x[U][K][4];
       int n = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (g0 + 64 * u < nvec) {
+        if (g0 + 64 * u < sg.v1) {
           load_chunk_symbols<K>(slot, ioff, (g0 + 64 * u) << 2, 4, m, x[u]);
           n = u + 1;
         }
       rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot, chunk, g0, m);
     }
-    for (uint64_t b = (nvec << 2) + wave * 64 + lane; b < ncols; b += nwaves * 64) {
+    for (uint64_t b = (nvec << 2) + wave * 64 + lane; sg.last && b < ncols; b += nwaves * 64) {
       uint32_t x[K][4];
       load_chunk_symbols<K>(slot, ioff, b, 1, m, x);
       rows_out<K>(x, rows, coeff, out_idx, slot, chunk, 4 * b, m, 1);
@@ -382,7 +407,8 @@ template <int KC, int RB, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
-    const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping) {
+    const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping,
+    uint32_t nseg) {
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
@@ -391,9 +417,12 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
-  const uint64_t nunits = nvec + (ncols & 3);  // whole vectors, then one unit per tail column
   constexpr bool F = MODE == 0;
-  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    // Units: the segment's whole vectors, then (last segment) one per tail column.
+    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
     uint32_t m = 0;
     if constexpr (MODE == 1) {
       m = mapping[obj];
@@ -402,8 +431,8 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
     uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;
     uint8_t* const par = slot + (uint64_t)k * chunk;
     Flags fl;
-    for (uint64_t g = wave * 64 + lane; g - lane < nunits; g += nwaves * 64) {
-      const bool valid = g < nunits;
+    for (uint64_t g = sg.v0 + wave * 64 + lane; g - lane < u1; g += nwaves * 64) {
+      const bool valid = g < u1;
       const bool vec = g < nvec;
       const int ncol = vec ? 4 : 1;
       const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
@@ -411,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
       // whole object word, below the object's last word.
       const uint64_t gw = g - lane;
       const bool interior =
-          gw + 64 <= nvec && (uint64_t)(k - 1) * L + col0 + ((gw + 64) << 2) < first_tail_word;
+          gw + 64 <= sg.v1 && (uint64_t)(k - 1) * L + col0 + ((gw + 64) << 2) < first_tail_word;
       for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
         uint32_t acc[RB][4];
 #pragma unroll
@@ -469,19 +498,21 @@ template <int KC, int RB>
 __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
-    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping) {
+    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
-  const uint64_t nunits = nvec + (ncols & 3);
-  for (uint32_t obj = blockIdx.y; obj < nobj; obj += gridDim.y) {
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
     const uint32_t m = mapping[obj];
     uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;
-    for (uint64_t g = wave * 64 + lane; g - lane < nunits; g += nwaves * 64) {
-      const bool valid = g < nunits;
+    for (uint64_t g = sg.v0 + wave * 64 + lane; g - lane < u1; g += nwaves * 64) {
+      const bool valid = g < u1;
       const bool vec = g < nvec;
       const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
       for (uint32_t r0 = 0; r0 < rows; r0 += RB) {

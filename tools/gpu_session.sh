@@ -166,6 +166,10 @@ if has slowsweep; then  # kernel knobs on whatever box this is (the log names it
   run sweep_enc 400 python tools/apply_variants.py --variants 8,2,6,11 --blocks 256,512,1024,2048 --nseg 1,4,16
   run sweep_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 8,2,6,11 --blocks 256,512,1024,2048 --nseg 1,4,16
 fi
+if has bytesshapes; then  # fused byte path on small and large batches
+  run bshape_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 --cpu-baseline 0 --host-path 0
+  run bshape_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --steps 3 --cpu-baseline 0 --host-path 0
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
