@@ -170,6 +170,15 @@ if has bytesshapes; then  # fused byte path on small and large batches
   run bshape_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 --cpu-baseline 0 --host-path 0
   run bshape_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --steps 3 --cpu-baseline 0 --host-path 0
 fi
+if has c5segs; then  # C5 (10/14, 64 x 1 GiB) with forced segment counts
+  for sg in 0 2 8 16; do
+    run c5segs_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0
+  done
+fi
+if has k10; then  # why is 10/14 slower than 8/12?  unroll x blocks x segments at C5 shape (64 x 1 GiB -> 32 here)
+  run k10_enc 400 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 8,10,6 --blocks 256,384,512,768 --nseg 1,4
+  run k8_1g_enc 400 python tools/apply_variants.py --need 8 --total 12 --mib 1024 --nobj 32 --variants 8,10,6 --blocks 256,512 --nseg 1,4
+fi
 has allocvar && run allocvar 600 python tools/alloc_variance.py --rounds 8
 has contig && run contig 600 python tools/alloc_contig.py --rounds 6
 has hbmmap && run hbmmap 600 python tools/hbm_map.py
