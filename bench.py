@@ -11,7 +11,7 @@ GPU, no data-path collective: "weak" scaling, each rank owns its own batch).
 
 value = (sum of object bytes encoded + decoded over all ranks) / (max over
 ranks of the timed K steps), in GiB/s.  roofline: algorithmic HBM bytes per
-launch of the dominant kernel (rs_apply_kernel<8>) / its average duration,
+launch of the dominant kernel (rs_apply_pipe_kernel<8>) / its average duration,
 from HIP events recorded on the launch stream.  cpu_baseline: the oracle's
 faithful scalar C restatement of the reference's Go path, on a bounded sample.
 
@@ -321,11 +321,15 @@ def main():
     dec_alg = nobj * 4 * L * (need + len(erase))
     launch_ms = (enc_ms + dec_ms) / 2
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
+    # The product dispatch (rs_apply.hip): the pipelined kernel for shards
+    # under 4 GiB, unless SLIME_RS_PIPE=0.
+    kname = "rs_apply_pipe_kernel" if L < (1 << 30) and os.environ.get("SLIME_RS_PIPE", "1") != "0" \
+        else "rs_apply_kernel"
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}":
+            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}" and tj.get("kernel") == kname:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -364,7 +368,7 @@ def main():
             "verified": bad == 0.0,
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"rs_apply_kernel<{need},vec>",
+                "kernel": f"{kname}<{need},vec>",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -99,9 +99,59 @@ hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Software-pipelined product kernel (rs_apply_pipe_kernel): each wave keeps
+// its next tile's loads in flight while it computes the current one, so
+// fewer, fatter waves keep HBM busy.  In-process A/B against the
+// non-pipelined kernel on fast-placement boxes (profiles/r01/pipe/, HBM GB/s,
+// best product geometry -> pipelined): 4/6 C2 5480 -> 5557, 6/9 5431 -> 5643,
+// 8/12 C3 6075 -> 6177, 10/14 C5 5530 -> 5595, 12/16 5041 -> 5225,
+// 16/20 5172 -> 5317.  pipe_unroll<K>() 16-byte units per lane per tile (two
+// register sets of K x U x 16 B; K = 12 at U = 3 spills into AGPRs, which
+// measured fine), pipe_blocks<K>() 256-lane blocks.
+template <int K>
+constexpr int pipe_unroll() {
+  return K == 1 ? 4 : K == 2 ? 2 : K <= 4 ? 1 : K <= 12 ? 3 : 1;
+}
+template <int K>
+constexpr uint64_t pipe_blocks() {
+  return K <= 12 ? 256 : 1024;
+}
+
+template <int K>
+hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
+  constexpr int U = pipe_unroll<K>();
+  const uint64_t per_block = 4ull * kBlock * U;
+  const Geometry& geo = geometry();
+  const uint32_t nseg = object_segments(a.nobj, a.ncols);
+  const uint64_t nwork = (uint64_t)a.nobj * nseg;
+  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
+  if (gy > 65535) gy = 65535;
+  const uint64_t target = geo.target ? geo.target : pipe_blocks<K>();
+  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL((apply::rs_apply_pipe_kernel<K, U, kNtLoads, kNtStores>), dim3((uint32_t)gx, (uint32_t)gy),
+                     dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
+                     a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
+  return hipGetLastError();
+}
+
+// The pipelined kernel addresses a shard with 32-bit byte offsets: it needs
+// ncols * 4 < 2^32 (shards under 4 GiB -- objects under 4 GiB x need).
+// Larger shards, and SLIME_RS_PIPE=0 (tuning), take rs_apply_kernel.
+bool pipe_ok(const ApplyLaunch& a) {
+  static const bool enabled = [] {
+    const char* e = getenv("SLIME_RS_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return enabled && a.ncols < (1ull << 30);
+}
+
 template <int K>
 hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
-  return a.vec_ok ? launch_k<K, true>(a, s) : launch_k<K, false>(a, s);
+  if (!a.vec_ok) return launch_k<K, false>(a, s);
+  return pipe_ok(a) ? launch_pipe<K>(a, s) : launch_k<K, true>(a, s);
 }
 
 // k > 16: rs_apply_wide_kernel -- all inputs in registers with 8-row blocks

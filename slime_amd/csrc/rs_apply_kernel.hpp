@@ -70,6 +70,16 @@ __device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, ui
   }
 }
 
+// One output row over 4 columns.
+template <int K>
+__device__ __forceinline__ uint4 dot4(const uint4 (&x)[K], const u32x16& c) {
+  uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
+  uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+  return make_uint4(fold96(lo0, hi0), fold96(lo1, hi1), fold96(lo2, hi2), fold96(lo3, hi3));
+}
+
 // Accumulate one output row over 4 columns and store it.
 template <int K, bool NTS>
 __device__ __forceinline__ void row4(const uint4 (&x)[K], const u32x16& c, uint32_t* dst) {
@@ -154,6 +164,113 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
     // kernels), one per lane, by the object's last segment.
     if (seg == nseg - 1)
       for (uint64_t b = (nvec << 2) + tid; b < ncols; b += nthr)
+        apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
+  }
+}
+
+// Software-pipelined form of the vectorised rs_apply_kernel: a wave issues
+// the loads of its NEXT tile before it computes and stores the current one,
+// so its own loads stay in flight through the math (two register sets of
+// U x K x 16 B, alternating; no copies).  Same tiles, same segments, same
+// results as rs_apply_kernel<K, true, U, ...>.
+// Loads are unconditional (lanes past the segment end re-read its last
+// vector), so the waitcnt pass sees a fixed count of loads per tile and can
+// wait for one register set while the other is still in flight.
+// Addressing: a shard is < 4 GiB (L < 2^30 symbols, checked by the host),
+// so every access is a wave-uniform 64-bit shard base (SGPRs) plus a 32-bit
+// per-lane byte offset -- the saddr form of global_load/store, one VGPR per
+// address instead of a 64-bit VGPR pair built by two VALU ops.
+template <bool NT>
+__device__ __forceinline__ uint4 ld16_at(const uint32_t* base, uint32_t byte_off) {
+  return ld16<NT>(reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + byte_off));
+}
+
+// Loads are unconditional (lanes past the segment end re-read its last
+// vector), so the waitcnt pass sees a fixed count of loads per tile and can
+// wait for one register set while the other is still in flight.
+template <int K, int U, bool NTL>
+__device__ __forceinline__ void load_tile(uint4 (&x)[U][K], const uint32_t* const (&sb)[K], uint32_t g0, uint32_t v1) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t g = g0 + 64 * u < v1 ? g0 + 64 * u : v1 - 1;
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[u][j] = ld16_at<NTL>(sb[j], g << 4);
+  }
+}
+
+// One output row of a tile: math outside the store branch, so every
+// register set is consumed on every path.
+template <int K, int U, bool NTS>
+__device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
+                                         const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+                                         uint64_t out_shard, uint32_t i, uint32_t g0, uint32_t v1) {
+  const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+  char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint4 r = dot4<K>(x[u], c);
+    if (g0 + 64 * u < v1) st16<NTS>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), r);
+  }
+}
+
+// Row 0 is peeled (rows >= 1 always): it reads every symbol of the tile, so
+// the waitcnt pass resolves the tile's loads there, with per-load counts that
+// leave the other register set in flight, and the runtime row loop after it
+// has nothing left to wait for.
+template <int K, int U, bool NTS>
+__device__ __forceinline__ void store_tile(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
+                                           const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+                                           uint64_t out_shard, uint32_t rows, uint32_t g0, uint32_t v1) {
+  tile_row<K, U, NTS>(x, ob, coeff, out_idx, out_shard, 0, g0, v1);
+  for (uint32_t i = 1; i < rows; ++i) tile_row<K, U, NTS>(x, ob, coeff, out_idx, out_shard, i, g0, v1);
+}
+
+template <int K, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, uint32_t nseg) {
+  static_assert(K > 0, "compile-time k only");
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
+  // Vector indices within a shard are 32-bit (host guarantees L < 2^30).
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  // Wave-uniform (readfirstlane) 32-bit tile counters: the tile loop is a
+  // scalar loop with scalar compares.
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = ib + (uint64_t)in_idx[j] * in_shard;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    uint4 xa[U][K], xb[U][K];
+    uint32_t step = wave;
+    if (step < ntiles) load_tile<K, U, NTL>(xa, sb, v0 + step * (64 * U) + lane, v1);
+    // The last prefetch of a wave (past ntiles) re-reads its current tile.
+    while (step < ntiles) {
+      uint32_t next = step + nwaves;
+      load_tile<K, U, NTL>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, NTS>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      step = next;
+      if (step >= ntiles) break;
+      next = step + nwaves;
+      load_tile<K, U, NTL>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, NTS>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      step = next;
+    }
+    if (seg == nseg - 1)
+      for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)
         apply_column<K>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
   }
 }

@@ -16,6 +16,13 @@ void go(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo
   hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS, ROT>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
                      os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
 }
+template <int K, int U, bool NTL, bool NTS>
+void gp(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os, const uint32_t* coeff,
+        const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy,
+        hipStream_t s, uint32_t nseg) {
+  hipLaunchKernelGGL((rs_apply_pipe_kernel<K, U, NTL, NTS>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os,
+                     coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
+}
 }  // namespace
 
 extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is,
@@ -28,9 +35,26 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
     if (k == 8) go<8, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);     \
     else if (k == 10) go<10, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
     else if (k == 4) go<4, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 6) go<6, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 12) go<12, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 16) go<16, U, NTL, NTS, ROT>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 4) gp<4, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 6) gp<6, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 12) gp<12, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 16) gp<16, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
     else return -2;                                                                                        \
     break;
 #define V(id, U, NTL, NTS) V2(id, U, NTL, NTS, false)
+#define P(id, U)                                                                                            \
+  case id:                                                                                                 \
+    if (k == 8) gp<8, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);     \
+    else if (k == 10) gp<10, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 4) gp<4, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 6) gp<6, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);   \
+    else if (k == 12) gp<12, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else if (k == 16) gp<16, U, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg); \
+    else return -2;                                                                                        \
+    break;
   switch (variant) {
     V(0, 1, true, false)
     V(1, 1, false, false)
@@ -45,10 +69,14 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
     V(10, 3, true, true)
     V2(11, 4, true, true, true)
     V2(12, 2, true, true, true)
+    P(13, 1)
+    P(14, 2)
+    P(15, 3)
     default:
       return -1;
   }
 #undef V
+#undef P
 #undef V2
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

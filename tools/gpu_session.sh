@@ -232,4 +232,20 @@ if has pmc; then
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o bench --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0
 fi
+if has pipe; then  # software-pipelined apply kernel (variants 13-15) against the product forms
+  V=8,10,6,13,14,15
+  run pipe_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants $V --blocks 256,512,768,1024 --nseg 8
+  run pipe_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --decode 1 --separate 0 --variants $V --blocks 256,512,768,1024 --nseg 8
+  run pipe_c3 300 python tools/apply_variants.py --variants $V --blocks 256,512,768,1024 --nseg 2
+  run pipe_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants $V --blocks 256,512,768,1024 --nseg 2
+  run pipe_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants $V --blocks 256,512,768,1024 --nseg 8
+fi
+if has pipek; then  # the pipelined kernel at the other k <= 16 (product: U4 <= 10, U2 above)
+  V=8,6,13,14,15
+  run pipek_4_6 300 python tools/apply_variants.py --need 4 --total 6 --mib 256 --nobj 128 --variants $V --blocks 256,512,1024 --nseg 2
+  run pipek_6_9 300 python tools/apply_variants.py --need 6 --total 9 --mib 256 --nobj 128 --variants $V --blocks 256,512,1024 --nseg 2
+  run pipek_8_12 300 python tools/apply_variants.py --need 8 --total 12 --mib 256 --nobj 128 --variants $V --blocks 256,512,1024 --nseg 2
+  run pipek_12_16 300 python tools/apply_variants.py --need 12 --total 16 --mib 1024 --nobj 16 --variants $V --blocks 256,512,1024 --nseg 16
+  run pipek_16_20 300 python tools/apply_variants.py --need 16 --total 20 --mib 1024 --nobj 16 --variants $V --blocks 256,512,1024 --nseg 16
+fi
 echo "=== session done" | tee -a "$OUT/session.log"

@@ -13,26 +13,32 @@ import json
 import sys
 
 
+KERNELS = ("rs_apply_pipe_kernel", "rs_apply_kernel")  # product apply kernels (rs_apply.hip)
+
+
 def per_dispatch(d, counter):
-    vals = {}
+    vals, seen = {}, set()
     for path in glob.glob(f"{d}/*counter_collection.csv"):
         for r in csv.DictReader(open(path)):
-            if "rs_apply_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            name = next((k for k in KERNELS if k + "<" in r["Kernel_Name"]), None)
+            if name and r["Counter_Name"] == counter:
                 vals[int(r["Dispatch_Id"])] = float(r["Counter_Value"])
-    return vals
+                seen.add(name)
+    return vals, seen
 
 
 def main():
     fetch_dir, write_dir, config = sys.argv[1:4]
-    f = per_dispatch(fetch_dir, "FETCH_SIZE")
-    w = per_dispatch(write_dir, "WRITE_SIZE")
+    f, fk = per_dispatch(fetch_dir, "FETCH_SIZE")
+    w, wk = per_dispatch(write_dir, "WRITE_SIZE")
+    assert len(fk | wk) == 1, f"expected one apply kernel, saw {fk | wk}"
     fetch_kib = sum(f.values()) / len(f)
     write_kib = sum(w.values()) / len(w)
     read_bytes = 2 * fetch_kib * 1024
     write_bytes = write_kib * 1024
     print(json.dumps({
         "config": config,
-        "kernel": "rs_apply_kernel",
+        "kernel": (fk | wk).pop(),
         "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
         "fetch_size_kib_avg": fetch_kib,
         "write_size_kib_avg": write_kib,
