@@ -248,4 +248,13 @@ if has pipek; then  # the pipelined kernel at the other k <= 16 (product: U4 <= 
   run pipek_12_16 300 python tools/apply_variants.py --need 12 --total 16 --mib 1024 --nobj 16 --variants $V --blocks 256,512,1024 --nseg 16
   run pipek_16_20 300 python tools/apply_variants.py --need 16 --total 20 --mib 1024 --nobj 16 --variants $V --blocks 256,512,1024 --nseg 16
 fi
+if has pipeab; then  # product dispatch with and without the pipelined kernel, BASELINE shapes, same box
+  B="--steps 5 --cpu-baseline 0 --bytes-path 0 --host-path 0"
+  for pp in 1 0; do
+    run ab_c3_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py $B
+    run ab_c2_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 $B
+    run ab_c5_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 10 --total 14 --object-mib 1024 --objects 32 $B
+    run ab_64mib_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --object-mib 512 --objects 64 $B
+  done
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
