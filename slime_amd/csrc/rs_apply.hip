@@ -43,8 +43,8 @@ namespace {
 using apply::kBlock;
 using apply::rs_apply_kernel;
 
-// Product variant of the vectorised kernel (tools/apply_variants.py sweep,
-// DESIGN.md "Tuning"): each wave streams U KiB of every shard per step with
+// Non-pipelined vectorised kernel (the fallback for shards >= 4 GiB and
+// SLIME_RS_PIPE=0; tools/apply_variants.py sweep, DESIGN.md "Tuning"): each wave streams U KiB of every shard per step with
 // non-temporal loads and stores (read-once/write-once streams).  U = 4 up to
 // k = 10 (<= 192 VGPRs, 2 waves/SIMD at the 512-block grid), U = 2 beyond so
 // the k x U x 16 B of symbols stay in registers without dropping below that.
@@ -139,13 +139,11 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
 
 // The pipelined kernel addresses a shard with 32-bit byte offsets: it needs
 // ncols * 4 < 2^32 (shards under 4 GiB -- objects under 4 GiB x need).
-// Larger shards, and SLIME_RS_PIPE=0 (tuning), take rs_apply_kernel.
+// Larger shards, and SLIME_RS_PIPE=0 (tuning; read per launch so the parity
+// tests can cover the fallback kernel in-process), take rs_apply_kernel.
 bool pipe_ok(const ApplyLaunch& a) {
-  static const bool enabled = [] {
-    const char* e = getenv("SLIME_RS_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return enabled && a.ncols < (1ull << 30);
+  const char* e = getenv("SLIME_RS_PIPE");
+  return !(e && e[0] == '0') && a.ncols < (1ull << 30);
 }
 
 template <int K>

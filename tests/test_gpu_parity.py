@@ -707,3 +707,40 @@ def test_fuzz_random_shapes_and_layouts(torch_dev):
         for o in range(nobj):
             for i, t in enumerate(erase):
                 assert np.array_equal(got[o, i], h[o, t]), (case, need, total, L, erase, o, t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20)])
+def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
+    """The non-pipelined apply kernel (shards >= 4 GiB; SLIME_RS_PIPE=0) at
+    small sizes: encode in place, misaligned bases, reconstruct into a
+    separate buffer -- and the pipelined product form on the same inputs."""
+    torch = torch_dev
+    from slime_amd import device as D
+    nobj, L = 3, 3 * 1024 + 5
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    erase = [0, need]
+    have = [i for i in range(total) if i not in erase][:need]
+    rec = D.Plan.reconstruct(need, total, have, erase)
+    outs = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("SLIME_RS_PIPE", pipe)
+        for off in (0, 1):
+            buf = torch.empty(off + nobj * total * L, dtype=torch.int32, device="cuda")
+            D.fill_symbols(buf, seed=need * 31 + off)
+            plan(buf, lay, buf, lay, L, nobj, src_offset=off, dst_offset=off + need * L)
+            out = torch.zeros(nobj * len(erase) * L, dtype=torch.int32, device="cuda")
+            rec(buf, lay, out, D.layout_of(len(erase), L), L, nobj, src_offset=off)
+            torch.cuda.synchronize()
+            h = buf.cpu().numpy().view(np.uint32)[off:].reshape(nobj, total, L)
+            got = out.cpu().numpy().view(np.uint32).reshape(nobj, len(erase), L)
+            for o in range(nobj):
+                ref = np.ascontiguousarray(h[o].copy())
+                OC.encode_object(ref, need, total)
+                assert np.array_equal(h[o], ref), (pipe, off, o)
+                for i, t in enumerate(erase):
+                    assert np.array_equal(got[o, i], h[o, t]), (pipe, off, o, t)
+            outs[(pipe, off)] = h.copy()
+    for off in (0, 1):
+        assert np.array_equal(outs[("0", off)], outs[("1", off)])
