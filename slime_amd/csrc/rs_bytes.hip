@@ -1,5 +1,6 @@
 // Fused byte-domain encode/decode launchers (kernels: rs_bytes_kernel.hpp).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "kernels.hpp"
 #include "rs_bytes_kernel.hpp"
@@ -17,19 +18,73 @@ constexpr int bytes_unroll() {
   return K <= 8 ? 4 : (K <= 12 ? 2 : 1);
 }
 
-// 512 resident blocks over `work` object segments of about ncols/nseg columns.
-dim3 grid_for(uint64_t ncols, uint64_t work, uint32_t nseg) {
+// `target` resident blocks (default 512) over `work` object segments of about
+// ncols/nseg columns, U units of 4 columns per lane per step.
+dim3 grid_for(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t target = 512, int U = 1) {
   uint64_t gy = work < 65535u ? work : 65535u;
   if (gy < 1) gy = 1;
-  uint64_t gx = (512 + gy - 1) / gy;
-  const uint64_t need = (ncols / nseg + 4ull * kBlock - 1) / (4ull * kBlock);
+  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t need = (ncols / nseg + 4ull * kBlock * U - 1) / (4ull * kBlock * U);
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
   return dim3((uint32_t)gx, (uint32_t)gy);
 }
 
+// Software-pipelined forms (rs_bytes_kernel.hpp), the product for need <= 16
+// when a chunk is under 4 GiB (32-bit offsets) unless SLIME_RS_PIPE=0 (read
+// per launch, as in rs_apply.hip).  Geometry as the pipelined apply kernel.
+template <int K>
+constexpr int pipe_unroll() {
+  return K == 1 ? 4 : K == 2 ? 2 : K <= 4 ? 1 : K <= 12 ? 3 : 1;
+}
+template <int K>
+constexpr uint64_t pipe_blocks() {
+  return K <= 12 ? 256 : 1024;
+}
+bool pipe_ok(const BytesLaunch& a) {
+  const char* e = getenv("SLIME_RS_PIPE");
+  return !(e && e[0] == '0') && a.L < (1ull << 30);
+}
+
+// The encode keeps its flags and the edge-tile path live beside the two
+// register sets: U = 2 up to need 8, 1 above (no spills to scratch).
+template <int K>
+constexpr int enc_pipe_unroll() {
+  return K <= 8 ? 2 : 1;
+}
+
+template <int K>
+hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
+  constexpr int U = enc_pipe_unroll<K>();
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  if (a.phase == 0) {
+    const uint32_t nseg = object_segments(a.nobj, ncols);
+    hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, U, 0>),
+                       grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, pipe_blocks<K>(), U), dim3(kBlock), 0, s,
+                       a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
+                       a.mapping, nseg);
+  } else {
+    hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, U, 1>), grid_for(ncols, 1, 1, pipe_blocks<K>(), U),
+                       dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
+                       a.out_idx, a.flags, a.mapping, 1u);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
+  constexpr int U = pipe_unroll<K>();
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t nseg = object_segments(a.nobj, ncols);
+  hipLaunchKernelGGL((bytes::decode_bytes_pipe_kernel<K, U>),
+                     grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, pipe_blocks<K>(), U), dim3(kBlock), 0, s, a.slots,
+                     a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, nseg);
+  return hipGetLastError();
+}
+
 template <int K>
 hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a)) return enc_pipe<K>(a, s);
   constexpr int U = bytes_unroll<K>();
   // Phase 0 streams every object at once; phase 1 re-encodes the few objects
   // MapToGF maps with 1<<31 (~7.5% of 256 MiB random objects), so the whole
@@ -50,6 +105,7 @@ hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
 
 template <int K>
 hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a)) return dec_pipe<K>(a, s);
   constexpr int U = bytes_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t nseg = object_segments(a.nobj, ncols);

@@ -371,6 +371,212 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restric
   }
 }
 
+// ---- software-pipelined forms (need <= 16, chunks < 4 GiB) -----------------
+// The byte kernels above with rs_apply_pipe_kernel's pipeline: a wave issues
+// the raw 16-byte loads of its next tile before it transforms, computes and
+// stores the current one (two register sets of K x U raw vectors).  Loads
+// are unconditional (lanes past the segment end re-read its last vector:
+// flags are running maxima, so the repeats change nothing), and the raw ->
+// symbol transform reads every loaded register before any row math, so the
+// waitcnt pass resolves a tile's loads there and leaves the other set in
+// flight.  Addresses are wave-uniform chunk bases plus 32-bit byte offsets
+// (chunk = 4L < 4 GiB, checked by the host).
+template <int K, int U>
+__device__ __forceinline__ void load_raw_tile(uint4 (&r)[U][K], const uint8_t* const (&cb)[K], uint32_t g0,
+                                              uint32_t v1) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t g = g0 + 64 * u < v1 ? g0 + 64 * u : v1 - 1;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r[u][j] = apply::ld16_at<true>(reinterpret_cast<const uint32_t*>(cb[j]), g << 4);
+  }
+}
+
+// Rows of a tile from its symbols (columns as 4-vectors), BE(symbol ^ m)
+// stored into chunk out_idx[i] of the window at `base`, for the lanes whose
+// unit lies inside the segment.
+template <int K, int U>
+__device__ __forceinline__ void rows_tile(const uint4 (&x)[U][K], uint32_t rows, const uint32_t* __restrict__ coeff,
+                                          const uint32_t* __restrict__ out_idx, uint8_t* base, uint64_t chunk,
+                                          uint32_t g0, uint32_t v1, uint32_t m) {
+  for (uint32_t i = 0; i < rows; ++i) {
+    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    uint8_t* const orow = base + (uint64_t)out_idx[i] * chunk;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 r = apply::dot4<K>(x[u], c);
+      const u32x4 v = {be(r.x ^ m), be(r.y ^ m), be(r.z ^ m), be(r.w ^ m)};
+      if (g0 + 64 * u < v1) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(orow + ((g0 + 64 * u) << 4)));
+    }
+  }
+}
+
+template <int K, int U>
+__global__ __launch_bounds__(kBlock) void decode_bytes_pipe_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
+    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
+  const uint64_t chunk = 4 * L;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t v0 = (uint32_t)sg.v0, v1 = (uint32_t)sg.v1;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    const uint32_t m = mapping[sg.obj];
+    uint8_t* const slot = slots + (uint64_t)sg.obj * slot_stride + 4 * col0;  // window base
+    const uint8_t* cb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) cb[j] = slot + (uint64_t)in_idx[j] * chunk;
+    uint4 ra[U][K], rb[U][K];
+    uint32_t step = wave;
+    if (step < ntiles) load_raw_tile<K, U>(ra, cb, v0 + step * (64 * U) + lane, v1);
+    while (step < ntiles) {
+      uint32_t next = step + nwaves;
+      load_raw_tile<K, U>(rb, cb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          ra[u][j] = make_uint4(be(ra[u][j].x) ^ m, be(ra[u][j].y) ^ m, be(ra[u][j].z) ^ m, be(ra[u][j].w) ^ m);
+      rows_tile<K, U>(ra, rows, coeff, out_idx, slot, chunk, v0 + step * (64 * U) + lane, v1, m);
+      step = next;
+      if (step >= ntiles) break;
+      next = step + nwaves;
+      load_raw_tile<K, U>(ra, cb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          rb[u][j] = make_uint4(be(rb[u][j].x) ^ m, be(rb[u][j].y) ^ m, be(rb[u][j].z) ^ m, be(rb[u][j].w) ^ m);
+      rows_tile<K, U>(rb, rows, coeff, out_idx, slot, chunk, v0 + step * (64 * U) + lane, v1, m);
+      step = next;
+    }
+    uint64_t ioff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * chunk;
+    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
+      uint32_t x[K][4];
+      load_chunk_symbols<K>(slot, ioff, b, 1, m, x);
+      rows_out<K>(x, rows, coeff, out_idx, slot, chunk, 4 * b, m, 1);
+    }
+  }
+}
+
+// Interior tile of the encode: raw data-chunk vectors -> symbols (mapping
+// m, MapToGF flags; no padding or partial word), then every parity row.
+template <int K, int U, bool F>
+__device__ __forceinline__ void encode_interior_tile(uint4 (&r)[U][K], uint8_t* par, uint64_t chunk, uint32_t m,
+                                                     uint32_t rows, const uint32_t* __restrict__ coeff,
+                                                     const uint32_t* __restrict__ out_idx, uint32_t g0, uint32_t v1,
+                                                     Flags& fl) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      uint32_t w[4] = {r[u][j].x, r[u][j].y, r[u][j].z, r[u][j].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t p = be(w[c]);
+        if (F) fl.add(c, p);
+        w[c] = p ^ m;
+      }
+      r[u][j] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  rows_tile<K, U>(r, rows, coeff, out_idx, par, chunk, g0, v1, m);
+}
+
+// MODE as in encode_bytes_kernel.  A segment's tiles split into an interior
+// prefix -- whole tiles whose highest word (last data chunk, last unit) is
+// below the object's last word: the pipelined loop -- and the few edge tiles
+// after it (padding, the partial last word, the segment's partial last
+// tile), which take encode_bytes_kernel's edge step without the pipeline.
+template <int K, int U, int MODE>
+__global__ __launch_bounds__(kBlock) void encode_bytes_pipe_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping, uint32_t nseg) {
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  constexpr bool F = MODE == 0;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint32_t v0 = (uint32_t)sg.v0, v1 = (uint32_t)sg.v1;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    uint32_t m = 0;
+    if constexpr (MODE == 1) {
+      m = mapping[obj];
+      if (m == 0 || flags[obj] != 0) continue;  // uniform per block
+    }
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
+    uint8_t* const par = slot + (uint64_t)K * chunk;
+    // Interior tiles st < nint: end = v0 + (st+1)*64U <= v1 and
+    // (K-1)L + col0 + 4*end < first_tail_word.
+    const uint64_t lim = (uint64_t)(K - 1) * L + col0;
+    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    if (end_max > v1) end_max = v1;
+    const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / (64 * U)) : 0u;
+    const uint8_t* cb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) cb[j] = slot + (uint64_t)j * chunk;
+    Flags fl;
+    uint4 ra[U][K], rb[U][K];
+    uint32_t step = wave;
+    if (step < nint) load_raw_tile<K, U>(ra, cb, v0 + step * (64 * U) + lane, v1);
+    while (step < nint) {
+      uint32_t next = step + nwaves;
+      load_raw_tile<K, U>(rb, cb, v0 + (next < nint ? next : step) * (64 * U) + lane, v1);
+      encode_interior_tile<K, U, F>(ra, par, chunk, m, rows, coeff, out_idx, v0 + step * (64 * U) + lane, v1, fl);
+      step = next;
+      if (step >= nint) break;
+      next = step + nwaves;
+      load_raw_tile<K, U>(ra, cb, v0 + (next < nint ? next : step) * (64 * U) + lane, v1);
+      encode_interior_tile<K, U, F>(rb, par, chunk, m, rows, coeff, out_idx, v0 + step * (64 * U) + lane, v1, fl);
+      step = next;
+    }
+    // Edge tiles (encode_bytes_kernel's edge step).
+    for (uint32_t st = nint + wave; st < ntiles; st += nwaves) {
+      const uint64_t g0 = (uint64_t)v0 + (uint64_t)st * (64 * U) + lane;
+      uint32_t x[U][K][4];
+      int n = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (g0 + 64 * u < v1) {
+          load_data_symbols<K, false, F>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], &fl);
+          n = u + 1;
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u >= n) break;
+        const uint64_t b = (g0 + 64 * u) << 2;
+        if ((uint64_t)(K - 1) * L + col0 + b + 4 > first_tail_word)
+          fix_data_tail<K>(slot, chunk, L, col0, b, 4, ow, m, x[u]);
+      }
+      rows_out_units<K, U>(x, n, rows, coeff, out_idx, par, chunk, g0, m);
+    }
+    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
+      uint32_t x[K][4];
+      load_data_symbols<K, false, F>(slot, chunk, L, col0, b, 1, ow, m, x, &fl);
+      fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
+      rows_out<K>(x, rows, coeff, out_idx, par, chunk, 4 * b, m, 1);
+    }
+    if constexpr (F) {
+      const uint32_t f = fl.bits();
+      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+      if (wf && lane == 0) atomicOr(&flags[obj], wf);
+    }
+  }
+}
+
 // ---- wide k (need > 16): the byte kernels in 16-chunk form ------------------
 // Same column walk as rs_apply_wide_kernel (4 columns per lane, one unit per
 // step), with the byte<->symbol transforms of the kernels above: inputs in

@@ -491,9 +491,17 @@ def _make_slots(torch, objs, need, total, extra=0):
     return torch.from_numpy(host).cuda(), L, chunk, stride
 
 
+@pytest.fixture(params=["1", "0"], ids=["pipelined", "fallback"])
+def kernel_form(request, monkeypatch):
+    """Byte kernels: the pipelined product form and the non-pipelined form
+    (chunks >= 4 GiB), selected per launch by SLIME_RS_PIPE."""
+    monkeypatch.setenv("SLIME_RS_PIPE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20), (17, 20), (33, 50)])
-@pytest.mark.parametrize("S", [1, 3, 4, 5, 31, 32, 33, 1000, 4096, 65537, 1 << 20])
-def test_encode_objects_matches_write_chunks(torch_dev, need, total, S):
+@pytest.mark.parametrize("S", [1, 3, 4, 5, 31, 32, 33, 1000, 4096, 65537, 1 << 20, 3 * (1 << 20) + 7])
+def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total, S):
     torch = torch_dev
     from slime_amd import device as D
     rng = np.random.default_rng(S * 31 + need)
@@ -548,8 +556,9 @@ def test_encode_objects_random_fallback(torch_dev):
 
 
 @pytest.mark.parametrize("need,total,S", [(4, 6, 5000), (8, 12, 1 << 20), (8, 12, 999999), (10, 14, 77777),
-                                          (2, 3, 3), (20, 24, 300001), (40, 60, 123457)])
-def test_decode_objects_repairs_chunks(torch_dev, need, total, S):
+                                          (2, 3, 3), (20, 24, 300001), (40, 60, 123457), (6, 9, 5 * (1 << 20) + 3),
+                                          (12, 16, 3 * (1 << 20) + 1), (16, 20, 2 * (1 << 20))])
+def test_decode_objects_repairs_chunks(torch_dev, kernel_form, need, total, S):
     torch = torch_dev
     from slime_amd import device as D
     rng = np.random.default_rng(S)

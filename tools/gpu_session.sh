@@ -257,4 +257,12 @@ if has pipeab; then  # product dispatch with and without the pipelined kernel, B
     run ab_64mib_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --object-mib 512 --objects 64 $B
   done
 fi
+if has bytesab; then  # byte kernels with and without the pipeline (both legs of bench.py switch)
+  B="--steps 5 --cpu-baseline 0 --host-path 0"
+  for pp in 1 0; do
+    run bab_c3_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py $B
+    run bab_c2_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 $B
+    run bab_c5_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 $B
+  done
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
