@@ -265,4 +265,8 @@ if has bytesab; then  # byte kernels with and without the pipeline (both legs of
     run bab_c5_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 $B
   done
 fi
+if has c5geo; then  # 10/14 geometry with the pipelined kernel: segments x segments-in-flight x blocks
+  run c5geo_enc 400 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 14,15 --blocks 256,384,512 --nseg 2,4,8 --inflight 0,64,128 --rounds 2
+  run c5geo_c3 400 python tools/apply_variants.py --variants 14,15 --blocks 256,384,512 --nseg 1,2,4 --inflight 0,64,128 --rounds 2
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
