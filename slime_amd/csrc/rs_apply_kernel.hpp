@@ -275,6 +275,137 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
   }
 }
 
+// ---- wide k, software-pipelined ------------------------------------------
+// A wave's work is a stream of items (tile, row block rb, input chunk jc):
+// one 64-vector tile per step, row blocks of RB rows, chunks of 16 input
+// shards.  Each item loads 16 vectors (shard indices past k are clamped to
+// k-1; their coefficients are zero in the plan table) and MACs them into the
+// row block's RB running residues (canonical 32-bit, one fold per chunk);
+// the last chunk of a row block stores it.  The next item's 16 loads are
+// issued before the current item's math (two register sets), so a wave
+// always has a chunk in flight.  Row 0 of a block always exists and
+// consumes every loaded register unconditionally (waitcnt, see
+// rs_apply_pipe_kernel).
+struct WideItem {
+  uint32_t tile, rb, jc;  // tile: the wave's step index (< ntiles when valid)
+};
+__device__ __forceinline__ void wide_next(WideItem& it, uint32_t nch, uint32_t nrb, uint32_t nwaves) {
+  if (++it.jc == nch) {
+    it.jc = 0;
+    if (++it.rb == nrb) {
+      it.rb = 0;
+      it.tile += nwaves;
+    }
+  }
+}
+
+// 16 input vectors of chunk jc at vector g (clamped to the segment).
+template <bool NTL>
+__device__ __forceinline__ void wide_load16(uint4 (&x)[16], const uint32_t* __restrict__ ib,
+                                            const uint32_t* __restrict__ in_idx, uint64_t in_shard, uint32_t k,
+                                            uint32_t jc, uint32_t g, uint32_t v1) {
+  const uint32_t gc = g < v1 ? g : v1 - 1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t s = jc * 16 + j < k ? jc * 16 + j : k - 1;
+    // An opaque wave-uniform shard base (readfirstlane), so the compiler
+    // keeps it in SGPRs as the saddr operand instead of folding the lane
+    // offset into a 64-bit VGPR address per load.
+    const uint64_t base = (uint64_t)(ib + (uint64_t)in_idx[s] * in_shard);
+    // (readfirstlane returns int: widen through uint32_t, no sign extension)
+    const uint64_t ub = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+    typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
+    const global_u32x4* gp = reinterpret_cast<const global_u32x4*>(ub + (uint64_t)(gc << 4));
+    const u32x4 v = NTL ? __builtin_nontemporal_load(gp) : *gp;
+    x[j] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
+// acc = (acc + sum_j c[j] * x[j]) mod p, exact, one fold.
+__device__ __forceinline__ void wide_mac16(const uint4 (&x)[16], const uint32_t* __restrict__ crow, uint4& acc) {
+  const u32x16 c = *reinterpret_cast<const u32x16*>(crow);
+  uint64_t lo0 = acc.x, lo1 = acc.y, lo2 = acc.z, lo3 = acc.w;
+  uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) mac4(lo0, lo1, lo2, lo3, hi0, hi1, hi2, hi3, x[j].x, x[j].y, x[j].z, x[j].w, c[j]);
+  acc = make_uint4(fold96(lo0, hi0), fold96(lo1, hi1), fold96(lo2, hi2), fold96(lo3, hi3));
+}
+
+// One item's math (and the row block's stores after its last chunk).
+template <int RB, bool NTS>
+__device__ __forceinline__ void wide_item(const uint4 (&x)[16], uint4 (&acc)[RB], const WideItem& it, uint32_t nch,
+                                          uint32_t rows, uint32_t cs, const uint32_t* __restrict__ coeff,
+                                          const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ ob,
+                                          uint64_t out_shard, uint32_t g, uint32_t v1) {
+  if (it.jc == 0) {
+#pragma unroll
+    for (int i = 0; i < RB; ++i) acc[i] = make_uint4(0, 0, 0, 0);
+  }
+  const uint32_t r0 = it.rb * RB;
+  const uint32_t* const c0 = coeff + (uint64_t)r0 * cs + it.jc * 16;
+  wide_mac16(x, c0, acc[0]);
+#pragma unroll
+  for (int i = 1; i < RB; ++i)
+    if (r0 + i < rows) wide_mac16(x, c0 + (uint64_t)i * cs, acc[i]);
+  if (it.jc == nch - 1 && g < v1) {
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      if (r0 + i < rows)
+        st16<NTS>(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ob + (uint64_t)out_idx[r0 + i] * out_shard) +
+                                              ((uint64_t)g << 4)),
+                  acc[i]);
+  }
+}
+
+template <int RB, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void rs_apply_wide_pipe_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, uint32_t nseg) {
+  const uint32_t cs = wide_coeff_stride(k);
+  const uint32_t nch = (k + 15) / 16, nrb = (rows + RB - 1) / RB;
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 63) / 64;
+    uint4 xa[16], xb[16], acc[RB];
+    WideItem it{wave, 0, 0};
+    if (it.tile < ntiles) wide_load16<NTL>(xa, ib, in_idx, in_shard, k, it.jc, v0 + it.tile * 64 + lane, v1);
+    while (it.tile < ntiles) {
+      WideItem nx = it;
+      wide_next(nx, nch, nrb, nwaves);
+      const WideItem& ld = nx.tile < ntiles ? nx : it;
+      wide_load16<NTL>(xb, ib, in_idx, in_shard, k, ld.jc, v0 + ld.tile * 64 + lane, v1);
+      wide_item<RB, NTS>(xa, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
+      it = nx;
+      if (it.tile >= ntiles) break;
+      nx = it;
+      wide_next(nx, nch, nrb, nwaves);
+      const WideItem& ld2 = nx.tile < ntiles ? nx : it;
+      wide_load16<NTL>(xa, ib, in_idx, in_shard, k, ld2.jc, v0 + ld2.tile * 64 + lane, v1);
+      wide_item<RB, NTS>(xb, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
+      it = nx;
+    }
+    if (seg == nseg - 1)
+      for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)
+        apply_column<0>(ib, ob, coeff, in_idx, in_shard, out_idx, out_shard, rows, k, b);
+  }
+}
+
 // Wide k (k > 16, up to the reference's 100 shards): the same 4-columns-per-
 // lane streaming as rs_apply_kernel, with the inputs taken in chunks of 16
 // shards and the outputs in blocks of up to RB rows.  Per row and column the

@@ -719,7 +719,7 @@ def test_fuzz_random_shapes_and_layouts(torch_dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20)])
+@pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20), (20, 24), (17, 30), (40, 56)])
 def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
     """The non-pipelined apply kernel (shards >= 4 GiB; SLIME_RS_PIPE=0) at
     small sizes: encode in place, misaligned bases, reconstruct into a

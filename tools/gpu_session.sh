@@ -21,7 +21,9 @@ run() {  # run <name> <limit-seconds> <command...>
   local rc=$?
   echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
   tail -n 25 "$OUT/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+  # A failed parity run (a wrong or faulting kernel) ends the session too:
+  # nothing after it should run on a kernel that is not known to be right.
+  if [ $rc -ne 0 ] && { [ $rc -ne 1 ] || [ "$name" = pytest_gpu ] || grep -q "illegal memory access" "$OUT/$name.log"; }; then
     echo "!!! $name ended with rc=$rc: stopping the session" | tee -a "$OUT/session.log"
     exit $rc
   fi
@@ -268,5 +270,15 @@ fi
 if has c5geo; then  # 10/14 geometry with the pipelined kernel: segments x segments-in-flight x blocks
   run c5geo_enc 400 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 14,15 --blocks 256,384,512 --nseg 2,4,8 --inflight 0,64,128 --rounds 2
   run c5geo_c3 400 python tools/apply_variants.py --variants 14,15 --blocks 256,384,512 --nseg 1,2,4 --inflight 0,64,128 --rounds 2
+fi
+if has wideab; then  # k > 16: pipelined wide kernel vs the chunked one, and its block budget
+  B="--object-mib 256 --steps 3 --cpu-baseline 0 --bytes-path 0 --host-path 0"
+  for cfg in "20 24 32 0,1,2,3" "32 40 32 0,1,2,3,4,5,6,7" "64 80 16 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15"; do
+    set -- $cfg
+    run wab_$1_$2_p1 300 env SLIME_RS_PIPE=1 python bench.py --need $1 --total $2 --objects $3 --erase $4 $B
+    run wab_$1_$2_p0 300 env SLIME_RS_PIPE=0 python bench.py --need $1 --total $2 --objects $3 --erase $4 $B
+    run wab_$1_$2_p1_g256 300 env SLIME_RS_PIPE=1 SLIME_RS_GRID_TARGET=256 python bench.py --need $1 --total $2 --objects $3 --erase $4 $B
+    run wab_$1_$2_p1_g1024 300 env SLIME_RS_PIPE=1 SLIME_RS_GRID_TARGET=1024 python bench.py --need $1 --total $2 --objects $3 --erase $4 $B
+  done
 fi
 echo "=== session done" | tee -a "$OUT/session.log"
