@@ -135,6 +135,19 @@ hipError_t enc_wide_k(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Pipelined wide decode (rs_bytes_kernel.hpp): 8-row blocks, 16 for more
+// than 8 rebuilt chunks; block budget as the wide apply kernel.
+template <int RB>
+hipError_t dec_wide_pipe(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t nseg = object_segments(a.nobj, ncols);
+  hipLaunchKernelGGL((bytes::decode_bytes_wide_pipe_kernel<RB>),
+                     grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, a.k <= 32 ? 256 : 1024, 1), dim3(kBlock), 0, s,
+                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
+                     a.mapping, nseg);
+  return hipGetLastError();
+}
+
 template <int KC>
 hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
@@ -146,7 +159,10 @@ hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
 }
 
 hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) { return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s); }
-hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) { return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s); }
+hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a)) return a.rows <= 8 ? dec_wide_pipe<8>(a, s) : dec_wide_pipe<16>(a, s);
+  return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s);
+}
 
 #define SLIME_K_SWITCH(fn)               \
   switch (a.k) {                         \

@@ -763,5 +763,98 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
   }
 }
 
+// Pipelined wide decode (need > 16, chunks < 4 GiB): rs_apply_wide_pipe_kernel's
+// item stream over chunk bytes.  Items load 16 raw survivor vectors (indices
+// past k clamped to k-1, zero coefficients); the transform BE(word) ^ m
+// reads every loaded register before the math; the last chunk of a row
+// block stores BE(residue ^ m).
+template <int RB>
+__global__ __launch_bounds__(kBlock) void decode_bytes_wide_pipe_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
+    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
+  using apply::WideItem;
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const uint32_t nch = (k + 15) / 16, nrb = (rows + RB - 1) / RB;
+  const uint64_t chunk = 4 * L;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t v0 = (uint32_t)sg.v0, v1 = (uint32_t)sg.v1;
+    const uint32_t ntiles = (v1 - v0 + 63) / 64;
+    const uint32_t m = mapping[sg.obj];
+    uint8_t* const slot = slots + (uint64_t)sg.obj * slot_stride + 4 * col0;  // window base
+    auto load = [&](uint4 (&x)[16], const WideItem& it) {
+      const uint32_t g = v0 + it.tile * 64 + lane;
+      const uint32_t gc = g < v1 ? g : v1 - 1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t s = it.jc * 16 + j < k ? it.jc * 16 + j : k - 1;
+        const uint64_t base = (uint64_t)(slot + (uint64_t)in_idx[s] * chunk);
+        const uint64_t ub = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+        typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const global_u32x4*>(ub + (uint64_t)(gc << 4)));
+        x[j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    };
+    uint4 acc[RB];
+    auto item = [&](uint4 (&x)[16], const WideItem& it) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = make_uint4(be(x[j].x) ^ m, be(x[j].y) ^ m, be(x[j].z) ^ m, be(x[j].w) ^ m);
+      if (it.jc == 0) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i] = make_uint4(0, 0, 0, 0);
+      }
+      const uint32_t r0 = it.rb * RB;
+      const uint32_t* const c0 = coeff + (uint64_t)r0 * cs + it.jc * 16;
+      apply::wide_mac16(x, c0, acc[0]);
+#pragma unroll
+      for (int i = 1; i < RB; ++i)
+        if (r0 + i < rows) apply::wide_mac16(x, c0 + (uint64_t)i * cs, acc[i]);
+      const uint32_t g = v0 + it.tile * 64 + lane;
+      if (it.jc == nch - 1 && g < v1) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          if (r0 + i < rows) {
+            const u32x4 v = {be(acc[i].x ^ m), be(acc[i].y ^ m), be(acc[i].z ^ m), be(acc[i].w ^ m)};
+            __builtin_nontemporal_store(
+                v, reinterpret_cast<u32x4*>(slot + (uint64_t)out_idx[r0 + i] * chunk + ((uint64_t)g << 4)));
+          }
+      }
+    };
+    uint4 xa[16], xb[16];
+    WideItem it{wave, 0, 0};
+    if (it.tile < ntiles) load(xa, it);
+    while (it.tile < ntiles) {
+      WideItem nx = it;
+      apply::wide_next(nx, nch, nrb, nwaves);
+      load(xb, nx.tile < ntiles ? nx : it);
+      item(xa, it);
+      it = nx;
+      if (it.tile >= ntiles) break;
+      nx = it;
+      apply::wide_next(nx, nch, nrb, nwaves);
+      load(xa, nx.tile < ntiles ? nx : it);
+      item(xb, it);
+      it = nx;
+    }
+    // Columns past the last whole vector of the window, one per lane.
+    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
+      for (uint32_t i = 0; i < rows; ++i) {
+        const uint32_t* crow = coeff + (uint64_t)i * cs;
+        uint64_t lo = 0;
+        uint32_t hi = 0;
+        for (uint32_t j = 0; j < k; ++j)
+          mac(lo, hi, be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m, crow[j]);
+        *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
+      }
+    }
+  }
+}
+
 }  // namespace bytes
 }  // namespace slime

@@ -281,4 +281,11 @@ if has wideab; then  # k > 16: pipelined wide kernel vs the chunked one, and its
     run wab_$1_$2_p1_g1024 300 env SLIME_RS_PIPE=1 SLIME_RS_GRID_TARGET=1024 python bench.py --need $1 --total $2 --objects $3 --erase $4 $B
   done
 fi
+if has widebytesab; then  # need > 16 byte path: pipelined wide decode vs the chunked one
+  B="--object-mib 256 --steps 3 --cpu-baseline 0 --host-path 0"
+  for pp in 1 0; do
+    run wbab_20_24_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 20 --total 24 --objects 32 $B
+    run wbab_40_56_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 40 --total 56 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 $B
+  done
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
