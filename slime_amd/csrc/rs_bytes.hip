@@ -119,6 +119,26 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
 // every input in registers up to need = 32, 16-chunk steps above.
 constexpr int kWideRows = 8;
 
+// Pipelined wide encode (rs_bytes_kernel.hpp): one wave per SIMD (256
+// blocks; the kernel holds its flags and edge path beside two register sets).
+template <int RB>
+hipError_t enc_wide_pipe(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint64_t blocks = 256;
+  if (a.phase == 0) {
+    const uint32_t nseg = object_segments(a.nobj, ncols);
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_pipe_kernel<RB, 0>),
+                       grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), 0, s, a.slots,
+                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
+                       a.mapping, nseg);
+  } else {
+    hipLaunchKernelGGL((bytes::encode_bytes_wide_pipe_kernel<RB, 1>), grid_for(ncols, 1, 1, blocks, 1), dim3(kBlock),
+                       0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
+                       a.flags, a.mapping, 1u);
+  }
+  return hipGetLastError();
+}
+
 template <int KC>
 hipError_t enc_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
@@ -158,7 +178,10 @@ hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) { return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s); }
+hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a)) return a.rows <= 8 ? enc_wide_pipe<8>(a, s) : enc_wide_pipe<16>(a, s);
+  return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s);
+}
 hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
   if (pipe_ok(a)) return a.rows <= 8 ? dec_wide_pipe<8>(a, s) : dec_wide_pipe<16>(a, s);
   return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s);

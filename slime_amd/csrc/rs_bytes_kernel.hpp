@@ -609,6 +609,69 @@ __device__ __forceinline__ void wide_mac_chunk(const uint32_t (&x)[KC][4], const
 // MODE as in encode_bytes_kernel.  Column tails (past the last whole vector
 // of the window) go one column per lane with ncol = 1.
 // KC = 32 holds every input of a need <= 32 code in registers at once.
+// One lane-unit step of the chunked wide encode at unit g (a whole vector,
+// or a tail column past the window's last whole vector): every row block and
+// input chunk, with the data-chunk tail fix on edge steps.
+template <int KC, int RB, bool F>
+__device__ __forceinline__ void encode_wide_step(uint8_t* slot, uint8_t* par, uint64_t chunk, uint64_t L,
+                                                 uint64_t col0, const ObjWords& ow, uint64_t first_tail_word,
+                                                 uint32_t m, uint32_t rows, uint32_t k, uint32_t cs,
+                                                 const uint32_t* __restrict__ coeff,
+                                                 const uint32_t* __restrict__ out_idx, uint64_t g, uint64_t nvec,
+                                                 uint64_t u1, uint64_t seg_v1, uint32_t lane, Flags& fl) {
+  const bool valid = g < u1;
+  const bool vec = g < nvec;
+  const int ncol = vec ? 4 : 1;
+  const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
+  // Interior step (wave-uniform): every data word the step touches is a
+  // whole object word, below the object's last word.
+  const uint64_t gw = g - lane;
+  const bool interior = gw + 64 <= seg_v1 && (uint64_t)(k - 1) * L + col0 + ((gw + 64) << 2) < first_tail_word;
+  for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
+    uint32_t acc[RB][4];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += KC) {
+      uint32_t x[KC][4];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0;
+        if (valid && j0 + j < k) {
+          if (interior) {
+            if (F && r0 == 0)
+              load_data_symbol<true, true>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], &fl);
+            else
+              load_data_symbol<true, false>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], nullptr);
+          } else {
+            if (F && r0 == 0)
+              load_data_symbol<false, true>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], &fl);
+            else
+              load_data_symbol<false, false>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], nullptr);
+            if (r0 == 0) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+        if (r0 + i < rows) wide_mac_chunk<KC>(x, coeff + (uint64_t)(r0 + i) * cs + j0, j0, k, acc[i]);
+    }
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (r0 + i < rows) {
+          uint8_t* dst = par + (uint64_t)out_idx[r0 + i] * chunk + 4 * b;
+          if (vec) {
+            const u32x4 v = {be(acc[i][0] ^ m), be(acc[i][1] ^ m), be(acc[i][2] ^ m), be(acc[i][3] ^ m)};
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+          } else {
+            *reinterpret_cast<uint32_t*>(dst) = be(acc[i][0] ^ m);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int KC, int RB, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
@@ -637,60 +700,9 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
     uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;
     uint8_t* const par = slot + (uint64_t)k * chunk;
     Flags fl;
-    for (uint64_t g = sg.v0 + wave * 64 + lane; g - lane < u1; g += nwaves * 64) {
-      const bool valid = g < u1;
-      const bool vec = g < nvec;
-      const int ncol = vec ? 4 : 1;
-      const uint64_t b = vec ? g << 2 : (nvec << 2) + (g - nvec);
-      // Interior step (wave-uniform): every data word the step touches is a
-      // whole object word, below the object's last word.
-      const uint64_t gw = g - lane;
-      const bool interior =
-          gw + 64 <= sg.v1 && (uint64_t)(k - 1) * L + col0 + ((gw + 64) << 2) < first_tail_word;
-      for (uint32_t r0 = 0; r0 < rows; r0 += RB) {
-        uint32_t acc[RB][4];
-#pragma unroll
-        for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
-        for (uint32_t j0 = 0; j0 < k; j0 += KC) {
-          uint32_t x[KC][4];
-#pragma unroll
-          for (int j = 0; j < KC; ++j) {
-            x[j][0] = x[j][1] = x[j][2] = x[j][3] = 0;
-            if (valid && j0 + j < k) {
-              if (interior) {
-                if (F && r0 == 0)
-                  load_data_symbol<true, true>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], &fl);
-                else
-                  load_data_symbol<true, false>(slot, chunk, L, col0, j0 + j, b, 4, ow, m, x[j], nullptr);
-              } else {
-                if (F && r0 == 0)
-                  load_data_symbol<false, true>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], &fl);
-                else
-                  load_data_symbol<false, false>(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j], nullptr);
-                if (r0 == 0) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, ncol, ow, m, x[j]);
-              }
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < RB; ++i)
-            if (r0 + i < rows) wide_mac_chunk<KC>(x, coeff + (uint64_t)(r0 + i) * cs + j0, j0, k, acc[i]);
-        }
-        if (valid) {
-#pragma unroll
-          for (int i = 0; i < RB; ++i) {
-            if (r0 + i < rows) {
-              uint8_t* dst = par + (uint64_t)out_idx[r0 + i] * chunk + 4 * b;
-              if (vec) {
-                const u32x4 v = {be(acc[i][0] ^ m), be(acc[i][1] ^ m), be(acc[i][2] ^ m), be(acc[i][3] ^ m)};
-                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
-              } else {
-                *reinterpret_cast<uint32_t*>(dst) = be(acc[i][0] ^ m);
-              }
-            }
-          }
-        }
-      }
-    }
+    for (uint64_t g = sg.v0 + wave * 64 + lane; g - lane < u1; g += nwaves * 64)
+      encode_wide_step<KC, RB, F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, g,
+                                  nvec, u1, sg.v1, lane, fl);
     if constexpr (F) {
       const uint32_t f = fl.bits();
       const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
@@ -759,6 +771,125 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
           }
         }
       }
+    }
+  }
+}
+
+// Pipelined wide encode (need > 16, chunks < 4 GiB).  The interior tiles of
+// a segment (whole 64-vector tiles below the object's last word, a prefix)
+// run as rs_apply_wide_pipe_kernel's item stream over data-chunk bytes: the
+// transform (BE, MapToGF flags on the first row block, ^ m) reads every
+// loaded register before the math.  The segment's remaining units (edge
+// tiles, tail columns) take encode_wide_step.  MODE as in encode_bytes_kernel.
+template <int RB, int MODE>
+__global__ __launch_bounds__(kBlock) void encode_bytes_wide_pipe_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping,
+    uint32_t nseg) {
+  using apply::WideItem;
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const uint32_t nch = (k + 15) / 16, nrb = (rows + RB - 1) / RB;
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  constexpr bool F = MODE == 0;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint32_t v0 = (uint32_t)sg.v0, v1 = (uint32_t)sg.v1;
+    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
+    uint32_t m = 0;
+    if constexpr (MODE == 1) {
+      m = mapping[obj];
+      if (m == 0 || flags[obj] != 0) continue;  // uniform per block
+    }
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
+    uint8_t* const par = slot + (uint64_t)k * chunk;
+    // Interior tiles t < nint: end = v0 + 64(t+1) <= v1 and
+    // (k-1)L + col0 + 4*end < first_tail_word.
+    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
+    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    if (end_max > v1) end_max = v1;
+    const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / 64) : 0u;
+    Flags fl;
+    auto load = [&](uint4 (&x)[16], const WideItem& it) {
+      const uint32_t g = v0 + it.tile * 64 + lane;  // interior: always inside the segment
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t s = it.jc * 16 + j < k ? it.jc * 16 + j : k - 1;
+        const uint64_t base = (uint64_t)(slot + (uint64_t)s * chunk);
+        const uint64_t ub = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+        typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const global_u32x4*>(ub + (uint64_t)(g << 4)));
+        x[j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    };
+    uint4 acc[RB];
+    auto item = [&](uint4 (&x)[16], const WideItem& it) {
+      // Indices past k repeat chunk k-1 (real object words; flags are maxima).
+      const bool add_flags = F && it.rb == 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        uint32_t w[4] = {be(x[j].x), be(x[j].y), be(x[j].z), be(x[j].w)};
+        if (add_flags) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) fl.add(c, w[c]);
+        }
+        x[j] = make_uint4(w[0] ^ m, w[1] ^ m, w[2] ^ m, w[3] ^ m);
+      }
+      if (it.jc == 0) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i] = make_uint4(0, 0, 0, 0);
+      }
+      const uint32_t r0 = it.rb * RB;
+      const uint32_t* const c0 = coeff + (uint64_t)r0 * cs + it.jc * 16;
+      apply::wide_mac16(x, c0, acc[0]);
+#pragma unroll
+      for (int i = 1; i < RB; ++i)
+        if (r0 + i < rows) apply::wide_mac16(x, c0 + (uint64_t)i * cs, acc[i]);
+      if (it.jc == nch - 1) {
+        const uint32_t g = v0 + it.tile * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          if (r0 + i < rows) {
+            const u32x4 v = {be(acc[i].x ^ m), be(acc[i].y ^ m), be(acc[i].z ^ m), be(acc[i].w ^ m)};
+            __builtin_nontemporal_store(
+                v, reinterpret_cast<u32x4*>(par + (uint64_t)out_idx[r0 + i] * chunk + ((uint64_t)g << 4)));
+          }
+      }
+    };
+    uint4 xa[16], xb[16];
+    WideItem it{wave, 0, 0};
+    if (it.tile < nint) load(xa, it);
+    while (it.tile < nint) {
+      WideItem nx = it;
+      apply::wide_next(nx, nch, nrb, nwaves);
+      load(xb, nx.tile < nint ? nx : it);
+      item(xa, it);
+      it = nx;
+      if (it.tile >= nint) break;
+      nx = it;
+      apply::wide_next(nx, nch, nrb, nwaves);
+      load(xa, nx.tile < nint ? nx : it);
+      item(xb, it);
+      it = nx;
+    }
+    // Edge tiles and tail columns.
+    for (uint64_t g = (uint64_t)v0 + (uint64_t)nint * 64 + (uint64_t)wave * 64 + lane; g - lane < u1;
+         g += (uint64_t)nwaves * 64)
+      encode_wide_step<16, RB, F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, g,
+                                  nvec, u1, sg.v1, lane, fl);
+    if constexpr (F) {
+      const uint32_t f = fl.bits();
+      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+      if (wf && lane == 0) atomicOr(&flags[obj], wf);
     }
   }
 }
