@@ -200,7 +200,23 @@ __device__ __forceinline__ void load_tile(uint4 (&x)[U][K], const uint32_t* cons
 
 // One output row of a tile: math outside the store branch, so every
 // register set is consumed on every path.
-template <int K, int U, bool NTS>
+// XOR stand-in for dot4 (one full-rate op per term instead of mad + addc):
+// WRONG results, used only by the tuning harness (MATH = false) to measure
+// how much of the pipelined kernel's time the field math costs.
+template <int K>
+__device__ __forceinline__ uint4 xor4(const uint4 (&x)[K], const u32x16& c) {
+  uint4 r = make_uint4(c[0], c[1], c[2], c[3]);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    r.x ^= x[j].x + c[j];
+    r.y ^= x[j].y + c[j];
+    r.z ^= x[j].z + c[j];
+    r.w ^= x[j].w + c[j];
+  }
+  return r;
+}
+
+template <int K, int U, bool NTS, bool MATH = true>
 __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
                                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                          uint64_t out_shard, uint32_t i, uint32_t g0, uint32_t v1) {
@@ -208,7 +224,11 @@ __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __res
   char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint4 r = dot4<K>(x[u], c);
+    uint4 r;
+    if constexpr (MATH)
+      r = dot4<K>(x[u], c);
+    else
+      r = xor4<K>(x[u], c);
     if (g0 + 64 * u < v1) st16<NTS>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), r);
   }
 }
@@ -217,15 +237,16 @@ __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __res
 // the waitcnt pass resolves the tile's loads there, with per-load counts that
 // leave the other register set in flight, and the runtime row loop after it
 // has nothing left to wait for.
-template <int K, int U, bool NTS>
+template <int K, int U, bool NTS, bool MATH = true>
 __device__ __forceinline__ void store_tile(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
                                            const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                            uint64_t out_shard, uint32_t rows, uint32_t g0, uint32_t v1) {
-  tile_row<K, U, NTS>(x, ob, coeff, out_idx, out_shard, 0, g0, v1);
-  for (uint32_t i = 1; i < rows; ++i) tile_row<K, U, NTS>(x, ob, coeff, out_idx, out_shard, i, g0, v1);
+  tile_row<K, U, NTS, MATH>(x, ob, coeff, out_idx, out_shard, 0, g0, v1);
+  for (uint32_t i = 1; i < rows; ++i) tile_row<K, U, NTS, MATH>(x, ob, coeff, out_idx, out_shard, i, g0, v1);
 }
 
-template <int K, int U, bool NTL, bool NTS>
+// MATH = false swaps the field math for xor4 (tuning harness only).
+template <int K, int U, bool NTL, bool NTS, bool MATH = true>
 __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
@@ -261,12 +282,12 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
     while (step < ntiles) {
       uint32_t next = step + nwaves;
       load_tile<K, U, NTL>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
-      store_tile<K, U, NTS>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      store_tile<K, U, NTS, MATH>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
       step = next;
       if (step >= ntiles) break;
       next = step + nwaves;
       load_tile<K, U, NTL>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
-      store_tile<K, U, NTS>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      store_tile<K, U, NTS, MATH>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
       step = next;
     }
     if (seg == nseg - 1)

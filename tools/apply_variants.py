@@ -29,7 +29,8 @@ from slime_amd import device as D  # noqa: E402
 ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain",
                 6: "U2 ntL ntS", 7: "U2 ntS", 8: "U4 ntL ntS", 9: "U4 ntL", 10: "U3 ntL ntS",
                 11: "U4 ntL ntS rot", 12: "U2 ntL ntS rot",
-                13: "pipe U1 ntL ntS", 14: "pipe U2 ntL ntS", 15: "pipe U3 ntL ntS"}
+                13: "pipe U1 ntL ntS", 14: "pipe U2 ntL ntS", 15: "pipe U3 ntL ntS",
+                16: "pipe U3 XOR-math (wrong by design)", 17: "pipe U2 XOR-math (wrong by design)"}
 
 
 def main():

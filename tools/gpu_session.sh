@@ -288,4 +288,9 @@ if has widebytesab; then  # need > 16 byte path: pipelined wide decode vs the ch
     run wbab_40_56_p$pp 300 env SLIME_RS_PIPE=$pp python bench.py --need 40 --total 56 --objects 16 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 $B
   done
 fi
+if has mathcost; then  # pipelined kernel with XOR stand-in math: is the field math on the critical path?
+  run mc_c3 300 python tools/apply_variants.py --variants 15,16,14,17 --blocks 256,512 --nseg 2
+  run mc_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,16 --blocks 256,512 --nseg 2
+  run mc_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,16,14,17 --blocks 256,512 --nseg 8
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
