@@ -63,6 +63,9 @@ def parse():
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
     ap.add_argument("--host-path", type=int, default=1,
                     help="rank 0 at N=1: PCIe-inclusive writeChunks/reconstruct from host memory (never `value`)")
+    ap.add_argument("--shard-align", type=int, default=64,
+                    help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
+                         "starts on a cache-line boundary; 1 = packed, stride L)")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
     return ap.parse_args()
@@ -256,9 +259,14 @@ def main():
         total_objs, scaling = args.global_objects, "strong"
     else:
         nobj, total_objs, scaling = args.objects, args.objects * world, "weak"
-    lay = D.layout_of(total, L)
+    # Device layout: shard stride SS >= L symbols, rounded to --shard-align so
+    # every shard base is line-aligned (L = 26843546 at C5 would put every
+    # shard 8 B off a 16 B boundary; DESIGN.md "Line-aligned segments").  The
+    # pad columns are never read or written; the algorithmic bytes are L's.
+    SS = ceil_div(L, max(1, args.shard_align)) * max(1, args.shard_align)
+    lay = D.layout_of(total, L, SS)
 
-    buf = torch.empty(nobj * total * L, dtype=torch.int32, device=f"cuda:{dev}")
+    buf = torch.empty(nobj * total * SS, dtype=torch.int32, device=f"cuda:{dev}")
     # Data shards: deterministic symbols, distinct per rank (synthetic objects).
     D.fill_symbols(buf, 0x5113E + 7919 * rank)
     enc = D.Plan.encode(need, total, dev)
@@ -269,14 +277,14 @@ def main():
         dec.set_outputs(erase)
         rec, rec_lay = buf, lay
     else:
-        rec = torch.empty(nobj * len(erase) * L, dtype=torch.int32, device=f"cuda:{dev}")
-        rec_lay = D.layout_of(len(erase), L)
+        rec = torch.empty(nobj * len(erase) * SS, dtype=torch.int32, device=f"cuda:{dev}")
+        rec_lay = D.layout_of(len(erase), L, SS)
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * L)
+        enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * SS)
         if ev is not None:
             ev[1].record(stream)
         dec(buf, lay, rec, rec_lay, L, nobj, stream=stream)
@@ -286,8 +294,8 @@ def main():
     # The true contents of every erased slot, before any decode has run: data
     # shards as filled, parity shards from one encode (encode is idempotent on
     # fixed data, so every timed step rewrites the same parity).
-    enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * L)
-    truth = buf.view(nobj, total, L)[:, erase, :].clone()
+    enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * SS)
+    truth = buf.view(nobj, total, SS)[:, erase, :L].clone()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -306,7 +314,8 @@ def main():
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
 
     # Correctness of what was timed: every rebuilt shard equals the true one.
-    got = buf.view(nobj, total, L)[:, erase, :] if args.decode_dst == "inplace" else rec.view(nobj, len(erase), L)
+    got = buf.view(nobj, total, SS)[:, erase, :L] if args.decode_dst == "inplace" \
+        else rec.view(nobj, len(erase), SS)[:, :, :L]
     ok = bool(torch.equal(got, truth))
     del truth
 
@@ -358,7 +367,7 @@ def main():
                 "workload": f"C3+C4: need={need} total={total}, {args.object_mib} MiB objects x {nobj} per GPU; "
                             f"encode all parity + decode erased {erase}",
                 "need": need, "total": total, "object_mib": args.object_mib, "objects_per_gpu": nobj,
-                "symbols_per_shard": L, "erased": erase, "decode_dst": args.decode_dst,
+                "symbols_per_shard": L, "shard_stride_symbols": SS, "erased": erase, "decode_dst": args.decode_dst,
                 "parallelism": f"object-partition x{world} (no RCCL)",
             },
             "encode_gibs": round(obj_bytes / GIB / (enc_ms * 1e-3), 2),

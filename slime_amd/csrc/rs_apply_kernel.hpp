@@ -18,6 +18,18 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kCoeffStride = 16;
 __host__ __device__ constexpr uint32_t wide_coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
+// 16-byte vectors per column segment: an even split rounded UP to a whole
+// 1 KiB of every stream (64 vectors), so every segment -- and with it every
+// wave's tile -- starts on the same 1 KiB grid as its shard base.  An odd
+// split (e.g. 10/14 on 1 GiB objects: 6710886 vectors / 8 = 838861) puts
+// every 1 KiB access of the launch across a cache-line boundary: 10/14 ran
+// at 5.5 TB/s against 6.1 for the same kernel on line-aligned segments
+// (profiles/r01/segalign/).  Trailing segments may come out empty.
+template <typename T>
+__host__ __device__ __forceinline__ T segment_vectors(T nvec, uint32_t nseg) {
+  return ((nvec + nseg - 1) / nseg + 63) & ~(T)63;
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_kernel(
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
   const uint64_t nvec = VEC && K > 0 ? ncols >> 2 : 0;
-  const uint64_t seg_vec = (nvec + nseg - 1) / nseg;  // 16-byte vectors per segment
+  const uint64_t seg_vec = segment_vectors(nvec, nseg);  // 16-byte vectors per segment
   const uint64_t nwork = (uint64_t)nobj * nseg;
   for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
     const uint64_t obj = wi / nseg, seg = wi % nseg;
@@ -188,20 +200,24 @@ __device__ __forceinline__ uint4 ld16_at(const uint32_t* base, uint32_t byte_off
 // Loads are unconditional (lanes past the segment end re-read its last
 // vector), so the waitcnt pass sees a fixed count of loads per tile and can
 // wait for one register set while the other is still in flight.
-template <int K, int U, bool NTL>
+template <int K, int U, bool NTL, bool LOAD = true>
 __device__ __forceinline__ void load_tile(uint4 (&x)[U][K], const uint32_t* const (&sb)[K], uint32_t g0, uint32_t v1) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t g = g0 + 64 * u < v1 ? g0 + 64 * u : v1 - 1;
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[u][j] = ld16_at<NTL>(sb[j], g << 4);
+    for (int j = 0; j < K; ++j)
+      if constexpr (LOAD)
+        x[u][j] = ld16_at<NTL>(sb[j], g << 4);
+      else
+        x[u][j] = make_uint4(g, g + j, g ^ j, g * 3u + j);  // write-only probe
   }
 }
 
 // One output row of a tile: math outside the store branch, so every
 // register set is consumed on every path.
 // XOR stand-in for dot4 (one full-rate op per term instead of mad + addc):
-// WRONG results, used only by the tuning harness (MATH = false) to measure
+// WRONG results, used only by the tuning harness (MODE != 0) to measure
 // how much of the pipelined kernel's time the field math costs.
 template <int K>
 __device__ __forceinline__ uint4 xor4(const uint4 (&x)[K], const u32x16& c) {
@@ -216,7 +232,7 @@ __device__ __forceinline__ uint4 xor4(const uint4 (&x)[K], const u32x16& c) {
   return r;
 }
 
-template <int K, int U, bool NTS, bool MATH = true>
+template <int K, int U, bool NTS, int MODE = 0>
 __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
                                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                          uint64_t out_shard, uint32_t i, uint32_t g0, uint32_t v1) {
@@ -225,10 +241,12 @@ __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __res
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     uint4 r;
-    if constexpr (MATH)
+    if constexpr (MODE == 0)
       r = dot4<K>(x[u], c);
     else
       r = xor4<K>(x[u], c);
+    if constexpr (MODE == 2)  // read-only probe: a store that (for random data) never happens
+      if (r.x != r.y || r.y != r.z || r.z != r.w) continue;
     if (g0 + 64 * u < v1) st16<NTS>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), r);
   }
 }
@@ -237,16 +255,18 @@ __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __res
 // the waitcnt pass resolves the tile's loads there, with per-load counts that
 // leave the other register set in flight, and the runtime row loop after it
 // has nothing left to wait for.
-template <int K, int U, bool NTS, bool MATH = true>
+template <int K, int U, bool NTS, int MODE = 0>
 __device__ __forceinline__ void store_tile(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
                                            const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                            uint64_t out_shard, uint32_t rows, uint32_t g0, uint32_t v1) {
-  tile_row<K, U, NTS, MATH>(x, ob, coeff, out_idx, out_shard, 0, g0, v1);
-  for (uint32_t i = 1; i < rows; ++i) tile_row<K, U, NTS, MATH>(x, ob, coeff, out_idx, out_shard, i, g0, v1);
+  tile_row<K, U, NTS, MODE>(x, ob, coeff, out_idx, out_shard, 0, g0, v1);
+  for (uint32_t i = 1; i < rows; ++i) tile_row<K, U, NTS, MODE>(x, ob, coeff, out_idx, out_shard, i, g0, v1);
 }
 
-// MATH = false swaps the field math for xor4 (tuning harness only).
-template <int K, int U, bool NTL, bool NTS, bool MATH = true>
+// MODE (tuning harness only; the product is MODE 0, the field math):
+//   1 swaps the field math for xor4, 2 also drops the stores (read-only),
+//   3 keeps xor4 and the stores but drops the loads (write-only).
+template <int K, int U, bool NTL, bool NTS, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
@@ -257,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
   // Vector indices within a shard are 32-bit (host guarantees L < 2^30).
   const uint32_t nvec = (uint32_t)(ncols >> 2);
-  const uint32_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
   const uint64_t nwork = (uint64_t)nobj * nseg;
   const uint32_t lane = threadIdx.x & 63;
   // Wave-uniform (readfirstlane) 32-bit tile counters: the tile loop is a
@@ -277,17 +297,17 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
     const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
     uint4 xa[U][K], xb[U][K];
     uint32_t step = wave;
-    if (step < ntiles) load_tile<K, U, NTL>(xa, sb, v0 + step * (64 * U) + lane, v1);
+    if (step < ntiles) load_tile<K, U, NTL, MODE != 3>(xa, sb, v0 + step * (64 * U) + lane, v1);
     // The last prefetch of a wave (past ntiles) re-reads its current tile.
     while (step < ntiles) {
       uint32_t next = step + nwaves;
-      load_tile<K, U, NTL>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
-      store_tile<K, U, NTS, MATH>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      load_tile<K, U, NTL, MODE != 3>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, NTS, MODE>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
       step = next;
       if (step >= ntiles) break;
       next = step + nwaves;
-      load_tile<K, U, NTL>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
-      store_tile<K, U, NTS, MATH>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      load_tile<K, U, NTL, MODE != 3>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, NTS, MODE>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
       step = next;
     }
     if (seg == nseg - 1)
@@ -390,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_wide_pipe_kernel(
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
   const uint32_t nvec = (uint32_t)(ncols >> 2);
-  const uint32_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
   const uint64_t nwork = (uint64_t)nobj * nseg;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -449,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_wide_kernel(
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
   const uint64_t nvec = ncols >> 2;
-  const uint64_t seg_vec = (nvec + nseg - 1) / nseg;
+  const uint64_t seg_vec = segment_vectors(nvec, nseg);
   const uint64_t nwork = (uint64_t)nobj * nseg;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);

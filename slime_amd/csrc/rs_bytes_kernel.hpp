@@ -206,7 +206,7 @@ struct Segment {
   uint64_t v0, v1;  // vectors [v0, v1) of the window
 };
 __device__ __forceinline__ Segment segment_of(uint64_t wi, uint32_t nseg, uint64_t nvec) {
-  const uint64_t per = (nvec + nseg - 1) / nseg;
+  const uint64_t per = apply::segment_vectors(nvec, nseg);
   const uint32_t seg = (uint32_t)(wi % nseg);
   Segment g;
   g.obj = (uint32_t)(wi / nseg);

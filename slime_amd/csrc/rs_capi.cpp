@@ -341,7 +341,7 @@ HostPipe host_pipe_mode() { return (HostPipe)g_host_pipe.load(std::memory_order_
 
 int host_apply_direct(Workspace* ws, const slime_rs_plan* plan, const uint32_t* const* in, uint32_t* const* out,
                       uint64_t L) {
-  const size_t shard = round16(L * 4) / 4;  // keep every shard 16-byte aligned
+  const size_t shard = (L + 63) & ~(size_t)63;  // every shard on a 256 B boundary (line-aligned streams)
   if (int rc = ws->reserve(shard * 4 * ((size_t)plan->k + plan->rows))) return rc;
   uint32_t* d_in = (uint32_t*)ws->dbuf;
   uint32_t* d_out = d_in + shard * plan->k;
@@ -536,7 +536,7 @@ int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
   const uint64_t nin = plan->k, nout = plan->rows;
   const uint64_t cl = window_cols(L, nin + nout, kStageBytes);
   const uint64_t n = (L + cl - 1) / cl;
-  const uint64_t rs = (cl + 3) & ~3ull;  // device row stride: 16-byte aligned rows
+  const uint64_t rs = (cl + 63) & ~63ull;  // device row stride: 256 B aligned rows (line-aligned streams)
   const size_t stage_dev = (size_t)(nin + nout) * rs * 4;
   if (int rc = ws->reserve(stage_dev * std::min<uint64_t>(Workspace::kStages, n))) return rc;
   uint8_t* const dev = ws->dbuf;
@@ -580,7 +580,7 @@ int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32
   for (uint64_t i = 0; i < nout; ++i)
     if (!pin_row(out[i])) return unregister(), -1;
   uint64_t cl = std::max<uint64_t>(4 * kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
-  if (cl >= L) cl = (L + 3) & ~3ull;
+  if (cl >= L) cl = (L + 63) & ~63ull;  // row stride: 256 B aligned
   const uint64_t nch = (L + cl - 1) / cl;
   const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
   const size_t stage_words = (size_t)(nin + nout) * cl;

@@ -16,11 +16,11 @@ void go(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo
   hipLaunchKernelGGL((rs_apply_kernel<K, true, U, NTL, NTS, ROT>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo,
                      os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
 }
-template <int K, int U, bool NTL, bool NTS, bool MATH = true>
+template <int K, int U, bool NTL, bool NTS, int MODE = 0>
 void gp(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os, const uint32_t* coeff,
         const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy,
         hipStream_t s, uint32_t nseg) {
-  hipLaunchKernelGGL((rs_apply_pipe_kernel<K, U, NTL, NTS, MATH>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os,
+  hipLaunchKernelGGL((rs_apply_pipe_kernel<K, U, NTL, NTS, MODE>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os,
                      coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
 }
 }  // namespace
@@ -74,13 +74,23 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
     P(15, 3)
     // XOR stand-in math (wrong results by design): how much does the field math cost?
     case 16:
-      if (k == 8) gp<8, 3, true, true, false>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
-      else if (k == 10) gp<10, 3, true, true, false>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      if (k == 8) gp<8, 3, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else if (k == 10) gp<10, 3, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else return -2;
+      break;
+    case 18:  // read-only probe (U3): the loads of the product walk, no stores
+      if (k == 8) gp<8, 3, true, true, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else if (k == 10) gp<10, 3, true, true, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else return -2;
+      break;
+    case 19:  // write-only probe (U3): the stores of the product walk, no loads
+      if (k == 8) gp<8, 3, true, true, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else if (k == 10) gp<10, 3, true, true, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
       else return -2;
       break;
     case 17:
-      if (k == 8) gp<8, 2, true, true, false>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
-      else if (k == 10) gp<10, 2, true, true, false>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      if (k == 8) gp<8, 2, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else if (k == 10) gp<10, 2, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
       else return -2;
       break;
     default:

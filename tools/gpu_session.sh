@@ -293,4 +293,40 @@ if has mathcost; then  # pipelined kernel with XOR stand-in math: is the field m
   run mc_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,16 --blocks 256,512 --nseg 2
   run mc_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,16,14,17 --blocks 256,512 --nseg 8
 fi
+if has rwsplit; then  # the product walk split into its read-only and write-only halves
+  run rw_c3 300 python tools/apply_variants.py --variants 15,16,18,19 --blocks 256,512 --nseg 2
+  run rw_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,16,18,19 --blocks 256,512 --nseg 8
+fi
+if has linealign; then  # 10/14 (L = 26843546: shard bases 8 B off 16 B) with shard strides padded to 16/64/128/256 B
+  run la_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,18,19 --blocks 256 --nseg 8 --pad 0,2,6,22,38
+  run la_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 8 --pad 0,2,38
+fi
+if has pow2; then  # is 10/14 slow because of k, or because its shards are not power-of-two sized?
+  run p2_c3 300 python tools/apply_variants.py --variants 15,18,19 --blocks 256 --nseg 2
+  run p2_k8_25m 300 python tools/apply_variants.py --need 8 --total 12 --mib 800 --nobj 128 --variants 15,18,19 --blocks 256 --nseg 2
+  run p2_k10_128m 300 python tools/apply_variants.py --need 10 --total 14 --mib 1280 --nobj 32 --variants 15,18,19 --blocks 256 --nseg 8
+  run p2_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,18,19 --blocks 256 --nseg 8
+fi
+if has segalign; then  # column segments rounded to whole 1 KiB: 10/14 (odd splits) before/after, padded strides
+  run sa_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,18,19 --blocks 256 --nseg 1,2,4,8 --pad 0,2,38
+  run sa_c5dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 8 --pad 0,38
+  run sa_c3 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 2
+  B="--cpu-baseline 0 --host-path 0"
+  run sa_bench_c5_64 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 $B
+  run sa_bench_c5_32 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 32 --steps 5 $B
+  run sa_bench_c10_256 300 python bench.py --need 10 --total 14 --object-mib 256 --objects 128 --steps 5 $B
+  run sa_bench_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 $B
+  run sa_bench_c3 300 python bench.py --steps 5 $B
+fi
+if has shardalign; then  # bench with line-aligned shard strides (default) vs packed (--shard-align 1)
+  B="--cpu-baseline 0 --host-path 0 --bytes-path 0"
+  for al in 64 1; do
+    run al${al}_c5_64 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 64 --steps 3 --shard-align $al $B
+    run al${al}_c10_256 300 python bench.py --need 10 --total 14 --object-mib 256 --objects 128 --steps 5 --shard-align $al $B
+  done
+  run al64_c3 300 python bench.py --steps 5 $B
+  run al64_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --steps 5 $B
+  run al64_c4mixed 300 python bench.py --erase 0,3,8,11 --steps 5 $B
+  run al64_c3_sep 300 python bench.py --decode-dst separate --steps 5 $B
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
