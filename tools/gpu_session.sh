@@ -329,4 +329,9 @@ if has shardalign; then  # bench with line-aligned shard strides (default) vs pa
   run al64_c4mixed 300 python bench.py --erase 0,3,8,11 --steps 5 $B
   run al64_c3_sep 300 python bench.py --decode-dst separate --steps 5 $B
 fi
+if has pipe4; then  # 4 KiB tiles per wave per stream (pipe U4) against the product U3, C3 and C5
+  run p4_c3 300 python tools/apply_variants.py --variants 15,20 --blocks 256,512 --nseg 2 --rounds 4
+  run p4_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,20 --blocks 256 --nseg 2 --rounds 4
+  run p4_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,20 --blocks 256 --nseg 8 --pad 38 --rounds 4
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
