@@ -259,6 +259,36 @@ def test_plan_encode_vs_oracle(torch_dev, need, total, L, nobj):
         assert np.array_equal(h[o], ref), o
 
 
+@pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (20, 24)])
+@pytest.mark.parametrize("L", [4 * 262145, 4 * 262145 + 3])
+@pytest.mark.parametrize("align", [1, 64])
+def test_segment_rounding_empty_trailing_segments(torch_dev, need, total, L, align):
+    """One object of 262145+ vectors per shard: 256 column segments whose 1 KiB
+    rounding (segment_vectors, rs_apply_kernel.hpp) leaves the trailing
+    segments empty, plus tail columns past the last vector; packed and 256 B
+    shard strides (the recommended layout).  Encode and in-place repair of r
+    erased shards, bit-exact against the oracle."""
+    torch = torch_dev
+    from slime_amd import device as D
+    SS = (L + align - 1) // align * align
+    buf = torch.empty(total * SS, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, 0xE5E6 + need * 131 + L + align)
+    lay = D.layout_of(total, L, SS)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, 1, dst_offset=need * SS)
+    torch.cuda.synchronize()
+    h = buf.cpu().numpy().view(np.uint32).reshape(total, SS)[:, :L]
+    ref = np.ascontiguousarray(h.copy())
+    OC.encode_object(ref, need, total)
+    assert np.array_equal(h, ref)
+    erase = list(range(total - need - 1)) + [need]  # r erasures: data 0..r-2 and the first parity
+    have = [i for i in range(total) if i not in erase][:need]
+    buf.view(total, SS)[erase, :L] = 0
+    D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)(buf, lay, buf, lay, L, 1)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().view(np.uint32).reshape(total, SS)[:, :L]
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("need,total", [(4, 6), (8, 12)])
 def test_plan_reconstruct_every_pattern(torch_dev, need, total):
     torch = torch_dev
