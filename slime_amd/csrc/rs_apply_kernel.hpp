@@ -241,7 +241,7 @@ __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __res
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     uint4 r;
-    if constexpr (MODE == 0)
+    if constexpr (MODE == 0 || MODE == 4)
       r = dot4<K>(x[u], c);
     else
       r = xor4<K>(x[u], c);
@@ -265,7 +265,10 @@ __device__ __forceinline__ void store_tile(const uint4 (&x)[U][K], uint32_t* __r
 
 // MODE (tuning harness only; the product is MODE 0, the field math):
 //   1 swaps the field math for xor4, 2 also drops the stores (read-only),
-//   3 keeps xor4 and the stores but drops the loads (write-only).
+//   3 keeps xor4 and the stores but drops the loads (write-only),
+//   4 is the product math with an XCD-grouped work order (blocks are dispatched
+//     round-robin over the 8 XCDs; 4 gives XCD x the contiguous work items
+//     [x*gy/8, (x+1)*gy/8) instead of every 8th one).
 template <int K, int U, bool NTL, bool NTS, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
@@ -284,7 +287,10 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
   // scalar loop with scalar compares.
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+  uint32_t by = blockIdx.y;
+  if constexpr (MODE == 4)
+    if (gridDim.x == 1 && gridDim.y % 8 == 0) by = (blockIdx.y % 8) * (gridDim.y / 8) + blockIdx.y / 8;
+  for (uint64_t wi = by; wi < nwork; wi += gridDim.y) {
     const uint64_t obj = wi / nseg;
     const uint32_t seg = (uint32_t)(wi % nseg);
     const uint32_t* __restrict__ ib = in + obj * in_obj_stride;

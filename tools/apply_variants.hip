@@ -93,6 +93,11 @@ extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, 
       else if (k == 10) gp<10, 4, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
       else return -2;
       break;
+    case 21:  // product math, XCD-grouped work order
+      if (k == 8) gp<8, 3, true, true, 4>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else if (k == 10) gp<10, 3, true, true, 4>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
+      else return -2;
+      break;
     case 17:
       if (k == 8) gp<8, 2, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);
       else if (k == 10) gp<10, 2, true, true, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);

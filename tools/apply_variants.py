@@ -31,7 +31,7 @@ ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2
                 11: "U4 ntL ntS rot", 12: "U2 ntL ntS rot",
                 13: "pipe U1 ntL ntS", 14: "pipe U2 ntL ntS", 15: "pipe U3 ntL ntS",
                 16: "pipe U3 XOR-math (wrong by design)", 17: "pipe U2 XOR-math (wrong by design)",
-                18: "pipe U3 read-only probe", 19: "pipe U3 write-only probe", 20: "pipe U4 ntL ntS"}
+                18: "pipe U3 read-only probe", 19: "pipe U3 write-only probe", 20: "pipe U4 ntL ntS", 21: "pipe U3 XCD-grouped"}
 
 
 def main():

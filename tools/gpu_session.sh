@@ -334,4 +334,9 @@ if has pipe4; then  # 4 KiB tiles per wave per stream (pipe U4) against the prod
   run p4_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,20 --blocks 256 --nseg 2 --rounds 4
   run p4_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,20 --blocks 256 --nseg 8 --pad 38 --rounds 4
 fi
+if has xcd; then  # XCD-grouped work order against the product's round-robin one
+  run xcd_c3 300 python tools/apply_variants.py --variants 15,21 --blocks 256 --nseg 2 --rounds 5
+  run xcd_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,21 --blocks 256 --nseg 2 --rounds 5
+  run xcd_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,21 --blocks 256 --nseg 8 --pad 38 --rounds 5
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
