@@ -339,4 +339,11 @@ if has xcd; then  # XCD-grouped work order against the product's round-robin one
   run xcd_c3dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15,21 --blocks 256 --nseg 2 --rounds 5
   run xcd_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 32 --variants 15,21 --blocks 256 --nseg 8 --pad 38 --rounds 5
 fi
+if has slowtile; then  # tile size per wave on a slow-placement allocation (if the box gives one)
+  run st_slow 400 python tools/apply_variants.py --hunt slow --variants 15,20,14,13 --blocks 256,512 --nseg 2,8 --rounds 3
+fi
+if has slowrw; then  # read-only / write-only halves of the walk on slow vs fast allocations of one box
+  run srw_slow 400 python tools/apply_variants.py --hunt slow --variants 15,18,19 --blocks 256 --nseg 2 --rounds 3
+  run srw_fast 400 python tools/apply_variants.py --hunt fast --variants 15,18,19 --blocks 256 --nseg 2 --rounds 3
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
