@@ -346,4 +346,9 @@ if has slowrw; then  # read-only / write-only halves of the walk on slow vs fast
   run srw_slow 400 python tools/apply_variants.py --hunt slow --variants 15,18,19 --blocks 256 --nseg 2 --rounds 3
   run srw_fast 400 python tools/apply_variants.py --hunt fast --variants 15,18,19 --blocks 256 --nseg 2 --rounds 3
 fi
+if has slowpad; then  # shard-stride skew (256 B-aligned pads) on slow vs fast allocations, pipelined product kernel
+  P="0,64,1024,16384,262208,1048640,4194368"
+  run spad_slow 500 python tools/apply_variants.py --hunt slow --variants 15 --blocks 256 --nseg 2 --rounds 2 --pad $P
+  run spad_fast 500 python tools/apply_variants.py --hunt fast --variants 15 --blocks 256 --nseg 2 --rounds 2 --pad $P
+fi
 echo "=== session done" | tee -a "$OUT/session.log"
