@@ -12,12 +12,17 @@ OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_bytes.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 CXXTEST  := tests/cpp/rs_host_test
+CACHETEST := tests/cpp/plan_cache_test
 
-all: $(LIB) oracle $(CXXTEST)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST)
+
+# The plan cache (plan_cache.hpp) over the product's host matrix code, CPU only.
+$(CACHETEST): tests/cpp/plan_cache_test.cpp $(SRC)/plan_cache.hpp $(SRC)/rs_matrix.cpp $(SRC)/rs_matrix.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -I$(SRC) -o $@ tests/cpp/plan_cache_test.cpp $(SRC)/rs_matrix.cpp
 
 # C++ host mirror of the Go API (include/slime_rs.hpp) and its parity tests.
 $(CXXTEST): tests/cpp/rs_host_test.cpp include/slime_rs.hpp include/slime_rs.h $(LIB)
-	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
 	  -Wl,-rpath,'$$ORIGIN/../../slime_amd/lib'
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HDRS) | $(OBJ)
@@ -37,7 +42,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(CXXTEST)
+	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -66,34 +66,52 @@ def parse():
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
-    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="PMC-derived HBM bytes per launch (rocprofv3, see profiles/README.md)")
+    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
+                         "used only when its config and kernel source match this run)")
     return ap.parse_args()
 
 
-def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, seconds: float) -> dict:
-    """The reference's algorithm on host cores: the oracle's faithful C restatement
-    (uint64 products, `%`p twice per term, r CreateParity passes per object,
-    RecoverData recomputing all need rows), one object per thread as the
-    reference runs it, repeated until ~`seconds` of wall time have elapsed."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cgroup_cpus() -> float | None:
+    """CPU quota of this process's cgroup (cpu.max), in CPUs; None if unlimited/unknown."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_leg(OC, need: int, total: int, have: list[int], threads: int, sample_mib: int, seconds: float) -> dict:
+    """`threads` host threads, one object each, each running the reference's
+    per-object path until ~`seconds` of wall time: r CreateParity passes
+    (multi_store.go:528-531 -> vector.go:18-41) and one RecoverData recomputing
+    all need rows (vector.go:50-88, multi_store.go:237) on the oracle's C
+    restatement (uint64 products, `%`p twice per term, vector.go:97)."""
     import threading
 
     import numpy as np
 
-    from oracle import oracle_c as OC
-
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
     L = (sample_mib << 20) // 4 // need
     rng = np.random.default_rng(0x5113E)
-    objs = [rng.integers(0, 4294967291, size=(total, L), dtype=np.uint64).astype(np.uint32) for _ in range(threads)]
-    have = [i for i in range(total) if i not in erase][:need]
+    base = rng.integers(0, 4294967291, size=(total, L), dtype=np.uint64).astype(np.uint32)
+    objs = [base.copy() for _ in range(threads)]
     reps = [0] * threads
     deadline = time.perf_counter() + seconds
 
     def work(t, o):
         while True:
             OC.encode_object(o, need, total)
-            rc, _ = OC.recover_data([o[i] for i in have], have)  # vector.go:80-85: all need rows
+            rc, _ = OC.recover_data([o[i] for i in have], have)
             assert rc == 0
             reps[t] += 1
             if time.perf_counter() >= deadline:
@@ -107,11 +125,39 @@ def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, secon
         t.join()
     dt = time.perf_counter() - t0
     nbytes = 2 * sum(reps) * need * L * 4  # encode + decode of each object pass
-    return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{threads} threads x {sample_mib} MiB objects, need={need} total={total}: encode (r "
-                      f"CreateParity passes, multi_store.go:528-531) + RecoverData(erase {erase}); {sum(reps)} "
-                      f"object passes in {dt:.1f} s (oracle/rs_oracle.c, gcc -O2)",
-            "seconds": round(dt, 2)}
+    return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads, "object_mib": sample_mib,
+            "object_passes": sum(reps), "seconds": round(dt, 2)}
+
+
+def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, seconds: float) -> dict:
+    """The reference's algorithm on host cores: the oracle's
+    faithful C restatement, one object per thread as the reference runs it
+    (the RS math is single-threaded per object, multi_store.go:528-531), on 1
+    thread and on every core this process may run on (sched_getaffinity).
+    `value` is the all-core figure."""
+    from oracle import oracle_c as OC
+
+    have = [i for i in range(total) if i not in erase][:need]
+    # Every core this process may run on: its affinity set, capped by its
+    # cgroup's CPU quota when there is one (a 1-GPU share of the GPU box sees
+    # 256 CPUs but may use 16; more threads than that only time-slice).
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpus()
+    ncores = max(1, min(affinity, int(quota))) if quota else affinity
+    one = _cpu_leg(OC, need, total, have, 1, sample_mib, seconds * 0.4)
+    # Smaller objects when there are many cores keep the sample's memory and
+    # setup time bounded (threads x 1.5 x object bytes resident).
+    all_mib = sample_mib if ncores <= 16 else max(8, sample_mib // 4)
+    allc = _cpu_leg(OC, need, total, have, ncores, all_mib, seconds * 0.6)
+    return {"value": allc["value"], "unit": "GiB/s", "cores": ncores, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": affinity,
+            "cgroup_cpu_quota": quota,
+            "single_thread": one, "all_cores": allc,
+            "sample": f"need={need} total={total}: per object, r CreateParity passes (multi_store.go:528-531) + "
+                      f"RecoverData(erase {erase}) recomputing all need rows (vector.go:80-85); 1 thread on "
+                      f"{one['object_mib']} MiB objects ({one['object_passes']} passes in {one['seconds']} s) and "
+                      f"{ncores} threads on {all_mib} MiB objects ({allc['object_passes']} passes in "
+                      f"{allc['seconds']} s); oracle/rs_oracle.c, gcc -O2"}
 
 
 def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int) -> dict:
@@ -183,17 +229,26 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
 
 
 def host_leg(need, total, erase, obj_mib=64, reps=5):
-    """PCIe-inclusive object rate from host memory (HTTP bodies <= 64 MiB):
-    slime_rs_write_chunks and slime_rs_reconstruct on caller-reused buffers,
-    median of `reps`.  Reported beside the device-resident `value`, never as it."""
+    """PCIe-inclusive object rate from host memory (HTTP bodies <= 64 MiB), on
+    caller-reused buffers, median of `reps`.  Reported beside the
+    device-resident `value`, never as it.
+
+    Two callers are timed.  The fused object entry points (write_chunks /
+    reconstruct: one device pass each) need writeChunks/reconstruct to call
+    them.  The UNCHANGED caller (multi_store.go as it is) issues the Go API
+    call by call: MapToGF, splitVector, r CreateParity calls (each uploads all
+    need data shards again, :528-531) and a MapFromGF per chunk (:554) on
+    write; MapToGFWith per survivor (:224), RecoverData (:237) and MapFromGF
+    per data row (:239) on read."""
     import numpy as np
-    from slime_amd import objects
+    from slime_amd import gf, objects, rs
     rng = np.random.default_rng(0x5113E)
     data = rng.integers(0, 256, size=obj_mib << 20, dtype=np.uint8)
     cb = objects.chunk_size(data.size, need)
     chunks = [np.zeros(cb, dtype=np.uint8) for _ in range(total)]
     out = np.zeros(data.size, dtype=np.uint8)
     have = [i for i in range(total) if i not in erase][:need]
+    r = total - need
 
     def med(fn):
         fn()
@@ -209,29 +264,77 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     surv = [chunks[i] for i in have]
     t_r = med(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
     ok = bool(np.array_equal(out, data))
-    return {"write_chunks_gibs": round(data.size / GIB / t_w, 2), "reconstruct_gibs": round(data.size / GIB / t_r, 2),
+
+    # The unchanged caller, call by call (Go API mirrors, slime_amd.rs / .gf).
+    m, words = gf.MapToGF(data)
+    parts = objects.split_vector(words, need)
+    par = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
+    t_cp = med(lambda: [rs.CreateParity(parts, need + i, par[i]) for i in range(r)])
+
+    def unchanged_write():
+        mm, w = gf.MapToGF(data)
+        ps = objects.split_vector(w, need)
+        pv = [rs.CreateParity(ps, need + i) for i in range(r)]
+        return mm, [gf.MapFromGF(mm, p) for p in ps + pv]
+
+    t_uw = med(unchanged_write)
+    mm, ref_chunks = unchanged_write()
+    ok_w = mm == box["m"] and all(bytes(c) == rc for c, rc in zip(chunks, ref_chunks))
+    sym = [gf.MapToGFWith(chunks[i], m) for i in have]
+    rec = [np.zeros(sym[0].size, dtype=np.uint32) for _ in range(need)]
+    t_rd = med(lambda: rs.RecoverData(sym, have, rec))
+
+    def unchanged_read():
+        cs = [gf.MapToGFWith(chunks[i], m) for i in have]
+        vs = rs.RecoverData(cs, have)
+        return b"".join(gf.MapFromGF(m, v) for v in vs)[:data.size]
+
+    t_ur = med(unchanged_read)
+    ok_r = unchanged_read() == data.tobytes()
+    par2 = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
+    t_cps = med(lambda: rs.CreateParities(parts, total, par2))
+    g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
+    return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r),
+            "unchanged_caller": {
+                "write_gibs": g(t_uw), "read_gibs": g(t_ur),
+                "create_parity_x_r_gibs": g(t_cp), "create_parities_batched_gibs": g(t_cps),
+                "recover_data_gibs": g(t_rd), "verified": bool(ok_w and ok_r),
+                "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF "
+                        f"(write); {need} x MapToGFWith + RecoverData + {need} x MapFromGF (read); each call "
+                        "host->GPU->host"},
             "object_mib": obj_mib, "erased": erase, "verified": ok,
             "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
                     "PCIe-inclusive; not `value`"}
 
 
-def board_info(dev: int) -> dict | None:
-    """Board model and HBM vendor of `dev` (amd-smi), so a bench line can be
-    matched with the board it ran on (placement modes differ between boards,
-    DESIGN.md).  None when amd-smi is unavailable."""
-    import subprocess
-    try:
-        p = torch.cuda.get_device_properties(dev)
-        bdf = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}.0"
-        out = subprocess.run(["amd-smi", "static", "-g", bdf], capture_output=True, text=True, timeout=30).stdout
-    except Exception:  # noqa: BLE001 - diagnostics only
-        return None
-    info = {"bdf": bdf}
-    for line in out.splitlines():
-        key, _, val = line.strip().partition(": ")
-        if key in ("MODEL_NUMBER", "PRODUCT_NAME", "OAM_ID") or (key == "VENDOR" and "HBM" not in val and val):
-            info.setdefault(key.lower(), val.strip())
-    return info if len(info) > 1 else None
+def board_info(dev: int) -> dict:
+    """Board identity of `dev` read in-process from sysfs (amdgpu exposes
+    product_name / product_number / VRAM vendor under the PCI device), so a
+    bench line can be matched with the board it ran on.  Nothing is spawned:
+    this process has initialised the GPU (no exec after GPU init)."""
+    p = torch.cuda.get_device_properties(dev)
+    bdf = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}.0"
+    info = {"bdf": bdf, "name": p.name, "arch": getattr(p, "gcnArchName", None),
+            "hbm_gib": round(p.total_memory / GIB, 1), "cus": p.multi_processor_count}
+    for key, fname in (("product_name", "product_name"), ("model_number", "product_number"),
+                       ("vram_vendor", "mem_info_vram_vendor"), ("vbios", "vbios_version")):
+        try:
+            val = open(f"/sys/bus/pci/devices/{bdf}/{fname}").read().strip()
+        except OSError:
+            continue
+        if val:
+            info[key] = val
+    return info
+
+
+def kernel_source_id() -> str:
+    """Hash of the apply kernel's sources: PMC traffic measured on one build
+    is only replayed into a bench line of the same kernel source."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("rs_apply_kernel.hpp", "rs_apply.hip", "gfp.hpp"):
+        h.update(open(os.path.join(ROOT, "slime_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def main():
@@ -243,9 +346,14 @@ def main():
         # Control plane only (barrier + max-over-ranks timing): objects are
         # independent, the data path exchanges nothing between GPUs.
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    # One rank per GPU.  With fewer visible GPUs than local ranks (a 2-rank
-    # rehearsal on a 1-GPU box) ranks share devices round-robin.
-    dev = local % max(1, torch.cuda.device_count())
+    # One rank per GPU.  More ranks than visible GPUs would put two ranks on
+    # one device and overstate the scaling curve: refuse.
+    ndev = torch.cuda.device_count()
+    if world > ndev or local >= ndev:
+        print(f"bench.py: {world} ranks (local rank {local}) but {ndev} visible GPU(s); one rank per GPU",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    dev = local
     torch.cuda.set_device(dev)
 
     need, total = args.need, args.total
@@ -334,14 +442,24 @@ def main():
     # under 4 GiB, unless SLIME_RS_PIPE=0.
     kname = "rs_apply_pipe_kernel" if L < (1 << 30) and os.environ.get("SLIME_RS_PIPE", "1") != "0" \
         else "rs_apply_kernel"
-    traffic = None
+    # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
+    # --pmc passes of their own).  It is replayed from the summary of such
+    # passes only when they were taken on this config AND this kernel source,
+    # and the line says where it came from.
+    traffic, traffic_source = None, "not measured for this kernel source/config"
+    src_id = kernel_source_id()
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}" and tj.get("kernel") == kname:
+            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}" and tj.get("kernel") == kname \
+                    and tj.get("kernel_source") == src_id:
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_source = (f"replayed: {os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE / "
+                                  f"WRITE_SIZE passes, session {tj.get('session', '?')}, kernel source {src_id})")
         except (OSError, ValueError):
             traffic = None
+    # Distinct devices across ranks (n_gpus), by PCI address.
+    bdfs = batch.gather_strings(board_info(dev)["bdf"])
 
     bytes_path = None
     if args.bytes_path:
@@ -354,7 +472,7 @@ def main():
             "metric": "RS encode+decode GiB/s device-resident at need=8/total=12, 1/2/4/8 GPUs",
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": len(set(bdfs)),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
@@ -383,6 +501,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg},
             },
             "cpu_baseline": None,

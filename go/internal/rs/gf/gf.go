@@ -8,6 +8,7 @@ package gf
 /*
 #cgo LDFLAGS: -lslime_rs
 #include <stdint.h>
+#include <stdlib.h>
 #include "slime_rs.h"
 */
 import "C"
@@ -20,9 +21,31 @@ import (
 
 const MaxVal = 1<<32 - 5
 
-func check(rc C.int) {
+// Device is the GPU MapToGF / MapToGFWith / MapFromGF run on; -1
+// (C.SLIME_RS_ANY_DEVICE, the default) lets libslime_rs's device pool pick.
+var Device = -1
+
+const detailCap = 512
+
+// call carries the device into one C call and that call's failure detail
+// back out (see internal/rs: goroutines may change OS threads between cgo
+// calls, so no thread-local state is read afterwards).
+type call struct{ c *C.slime_rs_call_t }
+
+func newCall() call {
+	size := C.size_t(unsafe.Sizeof(C.slime_rs_call_t{}))
+	c := (*C.slime_rs_call_t)(C.calloc(1, size+detailCap))
+	c.device = C.int(Device)
+	c.detail = (*C.char)(unsafe.Add(unsafe.Pointer(c), size))
+	c.detail_cap = detailCap
+	return call{c}
+}
+
+func (k call) free() { C.free(unsafe.Pointer(k.c)) }
+
+func (k call) check(rc C.int) {
 	if rc != C.SLIME_RS_OK {
-		panic(fmt.Sprintf("slime_rs: %s: %s", C.GoString(C.slime_rs_status_string(rc)), C.GoString(C.slime_rs_last_error())))
+		panic(fmt.Sprintf("slime_rs: %s: %s", C.GoString(C.slime_rs_status_string(rc)), C.GoString(k.c.detail)))
 	}
 }
 
@@ -54,7 +77,9 @@ func MapToGF(in []byte) (uint32, []uint32) {
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	var n C.uint32_t
-	check(C.slime_gf_map_to_gf(bytesPtr(in, &pin), C.uint64_t(len(in)), &n, wordsPtr(out, &pin)))
+	k := newCall()
+	defer k.free()
+	k.check(C.slime_gf_map_to_gf_ex(k.c, bytesPtr(in, &pin), C.uint64_t(len(in)), &n, wordsPtr(out, &pin)))
 	return uint32(n), out
 }
 
@@ -63,7 +88,9 @@ func MapToGFWith(in []byte, n uint32) []uint32 {
 	out := make([]uint32, (len(in)+3)/4)
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	check(C.slime_gf_map_to_gf_with(bytesPtr(in, &pin), C.uint64_t(len(in)), C.uint32_t(n), wordsPtr(out, &pin)))
+	k := newCall()
+	defer k.free()
+	k.check(C.slime_gf_map_to_gf_with_ex(k.c, bytesPtr(in, &pin), C.uint64_t(len(in)), C.uint32_t(n), wordsPtr(out, &pin)))
 	return out
 }
 
@@ -73,6 +100,8 @@ func MapFromGF(inn uint32, inv []uint32) []byte {
 	out := make([]byte, len(inv)*4)
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	check(C.slime_gf_map_from_gf(C.uint32_t(inn), wordsPtr(inv, &pin), C.uint64_t(len(inv)), bytesPtr(out, &pin)))
+	k := newCall()
+	defer k.free()
+	k.check(C.slime_gf_map_from_gf_ex(k.c, C.uint32_t(inn), wordsPtr(inv, &pin), C.uint64_t(len(inv)), bytesPtr(out, &pin)))
 	return out
 }

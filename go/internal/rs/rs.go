@@ -27,18 +27,48 @@ import (
 	"unsafe"
 )
 
-// raise turns a C-ABI status into the reference's panic.
-func raise(rc C.int) {
+// Device is the GPU the data-path calls of this package run on.  The default,
+// C.SLIME_RS_ANY_DEVICE (-1), lets libslime_rs's device pool give each call
+// the visible GPU with the fewest calls in flight, so concurrent goroutines
+// (HTTP requests, main.go:107-109; scrubbers, multi.go:54-58) spread over
+// every GPU of the node.  Additive: the reference has no device to choose.
+var Device = -1
+
+const detailCap = 512
+
+// call is one C-allocated slime_rs_call_t with its detail buffer.  The
+// device goes in with the call and the failure detail of THAT call comes
+// back in the buffer, so nothing depends on which OS thread cgo runs the
+// call on: a goroutine may move between threads from one C call to the next,
+// which makes the library's thread-local state (the last-error string, the
+// per-thread device choice) unusable from Go.
+type call struct{ c *C.slime_rs_call_t }
+
+func newCall() call {
+	size := C.size_t(unsafe.Sizeof(C.slime_rs_call_t{}))
+	c := (*C.slime_rs_call_t)(C.calloc(1, size+detailCap))
+	c.device = C.int(Device)
+	c.detail = (*C.char)(unsafe.Add(unsafe.Pointer(c), size))
+	c.detail_cap = detailCap
+	return call{c}
+}
+
+func (k call) free() { C.free(unsafe.Pointer(k.c)) }
+
+// raise turns the status of the call made with k into the reference's panic.
+func (k call) raise(rc C.int) {
 	if rc == C.SLIME_RS_OK {
 		return
 	}
+	// Codes 1..7: the reference's own panic strings (static, thread-free).
 	if rc >= 1 && rc <= 7 {
 		panic(C.GoString(C.slime_rs_status_string(rc)))
 	}
-	if rc == C.SLIME_RS_ERR_INDEX_RANGE {
-		panic(C.GoString(C.slime_rs_last_error()))
+	detail := C.GoString(k.c.detail)
+	if rc == C.SLIME_RS_ERR_INDEX_RANGE && detail != "" {
+		panic(detail) // Go's runtime index-out-of-range text, as produced by this call
 	}
-	panic(fmt.Sprintf("slime_rs: %s: %s", C.GoString(C.slime_rs_status_string(rc)), C.GoString(C.slime_rs_last_error())))
+	panic(fmt.Sprintf("slime_rs: %s: %s", C.GoString(C.slime_rs_status_string(rc)), detail))
 }
 
 // vectors pins the backing arrays of vs and returns a C array of their data
@@ -127,7 +157,9 @@ func CreateParity(data [][]uint32, index int, out []uint32) []uint32 {
 		defer pin.Unpin()
 		op = (*C.uint32_t)(unsafe.Pointer(&out[0]))
 	}
-	raise(C.slime_rs_create_parity(m.ptrs, m.lens, C.int(len(data)), C.int(index), op))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_create_parity_ex(k.c, m.ptrs, m.lens, C.int(len(data)), C.int(index), op))
 	return out
 }
 
@@ -147,7 +179,9 @@ func CreateParities(data [][]uint32, total int) [][]uint32 {
 	defer m.free()
 	o := marshal(outs)
 	defer o.free()
-	raise(C.slime_rs_create_parities(m.ptrs, m.lens, C.int(len(data)), C.int(total), o.ptrs))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_create_parities_ex(k.c, m.ptrs, m.lens, C.int(len(data)), C.int(total), o.ptrs))
 	return outs
 }
 
@@ -174,14 +208,18 @@ func RecoverData(chunks [][]uint32, indices []int) [][]uint32 {
 	defer m.free()
 	o := marshal(data)
 	defer o.free()
-	raise(C.slime_rs_recover_data(m.ptrs, m.lens, C.int(len(chunks)), idx, C.int(len(indices)), o.ptrs))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_recover_data_ex(k.c, m.ptrs, m.lens, C.int(len(chunks)), idx, C.int(len(indices)), o.ptrs))
 	return data
 }
 
 // vandermondeMatrix: (d+p) x d, entry [i][j] = (j+1)^i mod p (host, exact).
 func vandermondeMatrix(d, p int) [][]uint32 {
 	buf := make([]C.uint32_t, (d+p)*d+1)
-	raise(C.slime_rs_vandermonde_matrix(C.int(d), C.int(p), &buf[0]))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_vandermonde_matrix_ex(k.c, C.int(d), C.int(p), &buf[0]))
 	return matrixFromC(&buf[0], d+p, d)
 }
 
@@ -189,7 +227,9 @@ func vandermondeMatrix(d, p int) [][]uint32 {
 // rows invertible), computed exactly on the host by libslime_rs.
 func ParityMatrix(d, p int) [][]uint32 {
 	buf := make([]C.uint32_t, (d+p)*d+1)
-	raise(C.slime_rs_parity_matrix(C.int(d), C.int(p), &buf[0]))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_parity_matrix_ex(k.c, C.int(d), C.int(p), &buf[0]))
 	return matrixFromC(&buf[0], d+p, d)
 }
 
@@ -210,11 +250,13 @@ func ParityMatrixCached(d, p int) [][]uint32 {
 // the identity; singular input panics with the reference's message.
 func solveSubIdentity(m [][]uint32) {
 	flat := flatten(m)
-	rc := C.slime_rs_solve_sub_identity((*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(len(m)), C.int(len(m[0])))
+	k := newCall()
+	defer k.free()
+	rc := C.slime_rs_solve_sub_identity_ex(k.c, (*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(len(m)), C.int(len(m[0])))
 	for i := range m {
 		copy(m[i], flat[i*len(m[0]):(i+1)*len(m[0])])
 	}
-	raise(rc)
+	k.raise(rc)
 }
 
 // cloneMatrix deep-copies m into rows that share one backing array.
@@ -233,7 +275,9 @@ func invertMatrix(m [][]uint32) [][]uint32 {
 	flat := flatten(m)
 	d := len(m[0])
 	inv := make([]C.uint32_t, d*d)
-	raise(C.slime_rs_invert_matrix((*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(d), &inv[0]))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_invert_matrix_ex(k.c, (*C.uint32_t)(unsafe.Pointer(&flat[0])), C.int(d), &inv[0]))
 	return matrixFromC(&inv[0], d, d)
 }
 
@@ -264,7 +308,9 @@ func WriteChunks(data []byte, need, total int) (uint32, [][]byte) {
 		in = (*C.uint8_t)(unsafe.Pointer(&data[0]))
 	}
 	var mapping C.uint32_t
-	raise(C.slime_rs_write_chunks(in, C.uint64_t(len(data)), C.int(need), C.int(total), ptrs, &mapping))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_write_chunks_ex(k.c, in, C.uint64_t(len(data)), C.int(need), C.int(total), ptrs, &mapping))
 	return uint32(mapping), chunks
 }
 
@@ -304,6 +350,8 @@ func ReconstructObject(chunks [][]byte, indices []int, mapping uint32, size int)
 		pinner.Pin(&out[0])
 		op = (*C.uint8_t)(unsafe.Pointer(&out[0]))
 	}
-	raise(C.slime_rs_reconstruct(ptrs, idx, C.int(n), C.uint64_t(cb), C.uint32_t(mapping), C.uint64_t(size), op))
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_reconstruct_ex(k.c, ptrs, idx, C.int(n), C.uint64_t(cb), C.uint32_t(mapping), C.uint64_t(size), op))
 	return out
 }

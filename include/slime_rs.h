@@ -50,14 +50,36 @@ enum slime_rs_status {
 
 /* Reference panic message (codes 1..8) or a short description. Static storage. */
 const char *slime_rs_status_string(int status);
-/* Detail of the last failure on the calling thread ("" if none). */
+/* Detail of the last failure on the calling thread ("" if none).  Meaningful
+ * only on the thread that made the failing call, before its next call: the
+ * *_ex forms return the detail of the call itself instead. */
 const char *slime_rs_last_error(void);
 /* Library version string. */
 const char *slime_rs_version(void);
 /* Number of visible HIP devices (0 without a GPU; never fails). */
 int slime_rs_device_count(void);
-/* Device the calling thread's Go-API entry points run on (default 0). */
+
+/* Device of a host-memory entry point (CreateParity ... reconstruct, the
+ * MapToGF codec).  SLIME_RS_ANY_DEVICE: the library's device pool picks the
+ * visible GPU with the fewest calls in flight (ties round-robin), so
+ * concurrent callers spread over every GPU of the node (objects are
+ * independent: no data exchange between GPUs). */
+#define SLIME_RS_ANY_DEVICE (-1)
+/* Pin the calling OS thread's host entry points to `device`
+ * (SLIME_RS_ANY_DEVICE, the default, returns them to the pool).  Thread-local:
+ * callers whose threads migrate between calls (Go) use the *_ex forms. */
 int slime_rs_select_device(int device);
+
+/* Per-call context of the *_ex entry points, for callers that must not depend
+ * on thread-local state between calls (cgo: a goroutine may run consecutive
+ * C calls on different OS threads, and concurrent goroutines share threads).
+ * Replaces, for these callers, slime_rs_select_device and
+ * slime_rs_last_error. */
+typedef struct slime_rs_call {
+  int device;        /* device ordinal, or SLIME_RS_ANY_DEVICE (the pool picks) */
+  char *detail;      /* optional: receives this call's failure detail, NUL-terminated ("" on success) */
+  size_t detail_cap; /* bytes at detail (0: no detail wanted) */
+} slime_rs_call_t;
 /* How the Go-API entry points (CreateParity/CreateParities/RecoverData) move
  * host rows to the GPU and back (process-wide; env SLIME_RS_HOST_PIPE sets
  * the initial value):
@@ -157,7 +179,9 @@ int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t *src, slime_rs_la
                           slime_rs_layout_t dst_layout, uint64_t L, uint64_t nobj, void *stream);
 /* Write output row i to dst shard out_shards[i] instead of shard i (e.g. a
  * repair that writes rebuilt shards back into their erased slots of the
- * source layout, which is also the faster placement on MI355X: DESIGN.md). */
+ * source layout, which is also the faster placement on MI355X: DESIGN.md).
+ * Only before the plan's first launch (SLIME_RS_ERR_INVALID_ARG after it:
+ * launches in flight read the table). */
 int slime_rs_plan_set_outputs(slime_rs_plan_t plan, const int *out_shards);
 /* Shape of a plan: rows written and inputs read per column. */
 int slime_rs_plan_shape(slime_rs_plan_t plan, int *rows, int *k);
@@ -206,13 +230,15 @@ uint64_t slime_rs_chunk_size(uint64_t size, int need);
  * in one device pass (fused byte kernels) with pinned, overlapped transfers.
  * chunks[0..total-1] each receive slime_rs_chunk_size(size, need) bytes;
  * *mapping receives MappingValue.  The random-mapping fallback draws from the
- * library's stream (slime_gf_seed).  need >= 1 and total > need;
- * size 0 gives mapping 0 and empty chunks.  Synchronous; thread-safe. */
+ * library's stream (slime_gf_seed).  need >= 1 and total >= need (total ==
+ * need: a store without parity, multi_config.go:36); size 0 gives mapping 0
+ * and empty chunks.  Synchronous; thread-safe. */
 int slime_rs_write_chunks(const uint8_t *data, uint64_t size, int need, int total, uint8_t *const *chunks,
                           uint32_t *mapping);
 
 /* The slow path of Multi.reconstruct (multi_store.go:215-241): the first
- * `need` available chunks (chunk_bytes each, a multiple of 4) with their
+ * `need` available chunks (chunk_bytes each; a length that is not a multiple
+ * of 4 is zero-padded to whole words as MapToGFWith does) with their
  * chunk indices, and the file's MappingValue -> the object's `size` bytes in
  * out:  chunk := MapToGFWith(data, mapping); RecoverData(chunks, indices);
  * MapFromGF each data row; data[:size].  Same panics as RecoverData for bad
@@ -226,13 +252,56 @@ int slime_rs_reconstruct(const uint8_t *const *chunks, const int *indices, int n
  * in a partial last word); if flags != NULL it is OR-ed with bit0 = some
  * unmapped word >= p, bit1 = some (word ^ 1<<31) >= p  (MapToGF's choice).
  * unpack: bytes = BE(words[i] ^ mapping). */
-int slime_gf_pack_device(const uint8_t *bytes, uint64_t len, uint32_t mapping, uint32_t *words, uint32_t *flags,
-                         void *stream);
-int slime_gf_unpack_device(const uint32_t *words, uint64_t count, uint32_t mapping, uint8_t *bytes, void *stream);
+int slime_gf_pack_device(int device, const uint8_t *bytes, uint64_t len, uint32_t mapping, uint32_t *words,
+                         uint32_t *flags, void *stream);
+int slime_gf_unpack_device(int device, const uint32_t *words, uint64_t count, uint32_t mapping, uint8_t *bytes,
+                           void *stream);
 
 /* Deterministic synthetic symbols (benchmarks/tests): word g of the buffer is
  * a pure function of (seed, g), uniform over [0, p). Asynchronous. */
 int slime_rs_fill_symbols(int device, uint32_t *dst, uint64_t count, uint64_t seed, void *stream);
+
+/* ==== *_ex forms: the entry points above with a per-call context ==========
+ * Same arguments and results as the plain forms; `call` gives the device and
+ * receives this call's failure detail (see slime_rs_call_t).  These are what
+ * the cgo shim binds. */
+int slime_rs_create_parity_ex(const slime_rs_call_t *call, const uint32_t *const *data, const uint64_t *lens,
+                              int ndata, int index, uint32_t *out);                       /* vector.go:18 */
+int slime_rs_create_parities_ex(const slime_rs_call_t *call, const uint32_t *const *data, const uint64_t *lens,
+                                int ndata, int total, uint32_t *const *out);              /* multi_store.go:528-531 */
+int slime_rs_recover_data_ex(const slime_rs_call_t *call, const uint32_t *const *chunks, const uint64_t *lens,
+                             int nchunks, const int *indices, int nindices, uint32_t *const *out); /* vector.go:50 */
+int slime_rs_write_chunks_ex(const slime_rs_call_t *call, const uint8_t *data, uint64_t size, int need, int total,
+                             uint8_t *const *chunks, uint32_t *mapping);                  /* multi_store.go:526-554 */
+int slime_rs_reconstruct_ex(const slime_rs_call_t *call, const uint8_t *const *chunks, const int *indices, int need,
+                            uint64_t chunk_bytes, uint32_t mapping, uint64_t size, uint8_t *out); /* :215-241 */
+int slime_gf_map_to_gf_ex(const slime_rs_call_t *call, const uint8_t *in, uint64_t len, uint32_t *mapping,
+                          uint32_t *out);                                                 /* map.go:15 */
+int slime_gf_map_to_gf_with_ex(const slime_rs_call_t *call, const uint8_t *in, uint64_t len, uint32_t n,
+                               uint32_t *out);                                            /* map.go:74 */
+int slime_gf_map_from_gf_ex(const slime_rs_call_t *call, uint32_t n, const uint32_t *in, uint64_t count,
+                            uint8_t *out);                                                /* map.go:103 */
+int slime_rs_parity_matrix_ex(const slime_rs_call_t *call, int d, int p, uint32_t *out);  /* matrix.go:27 */
+int slime_rs_vandermonde_matrix_ex(const slime_rs_call_t *call, int d, int p, uint32_t *out); /* matrix.go:8 */
+int slime_rs_solve_sub_identity_ex(const slime_rs_call_t *call, uint32_t *m, int rows, int cols); /* matrix.go:35 */
+int slime_rs_invert_matrix_ex(const slime_rs_call_t *call, const uint32_t *m, int d, uint32_t *inv); /* matrix.go:112 */
+
+/* ==== plan cache and device pool (host entry points) =====================
+ * Host entry points keep their device plans (coefficient tables; recovery
+ * plans keyed by survivor set, reference: vector.go:69-77) in one bounded LRU
+ * per process (default 256 plans, env SLIME_RS_PLAN_CACHE).  An evicted plan
+ * releases its device table once no call in flight still uses it. */
+typedef struct slime_rs_cache_stats {
+  uint64_t live;          /* plans cached now (<= capacity) */
+  uint64_t capacity;
+  uint64_t hits, misses, evictions;
+  uint64_t device_tables; /* plan tables allocated on devices and not yet freed (all plans, cached or not) */
+} slime_rs_cache_stats_t;
+int slime_rs_plan_cache_stats(slime_rs_cache_stats_t *stats);
+/* Set the cache capacity (>= 1); shrinking evicts at once. */
+int slime_rs_plan_cache_capacity(uint64_t capacity);
+/* Host calls the device pool has routed to `device` so far and calls in flight there. */
+int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
 
 #ifdef __cplusplus
 }

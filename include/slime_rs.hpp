@@ -38,17 +38,34 @@ struct NativeError : std::runtime_error {
   NativeError(int st, const std::string& msg) : std::runtime_error(msg), status(st) {}
 };
 
-namespace detail {
-inline void check(int rc) {
-  if (rc == SLIME_RS_OK) return;
-  const std::string last = slime_rs_last_error();
-  if (rc >= SLIME_RS_ERR_VARYING_LENGTH && rc <= SLIME_RS_ERR_INDEX_RANGE) {
-    std::string msg = slime_rs_status_string(rc);
-    if (rc == SLIME_RS_ERR_INDEX_RANGE && !last.empty()) msg = last;
-    throw Panic(rc, msg);
-  }
-  throw NativeError(rc, std::string("slime_rs error ") + std::to_string(rc) + ": " + last);
+// Device of the data-path calls below (process-wide; SLIME_RS_ANY_DEVICE,
+// the default, lets the library's device pool pick per call).
+inline int& Device() {
+  static int d = SLIME_RS_ANY_DEVICE;
+  return d;
 }
+
+namespace detail {
+// One call's context: the device goes in, that call's failure detail comes
+// back (the *_ex entry points), so no thread-local state is read afterwards.
+struct Call {
+  char buf[512] = {0};
+  slime_rs_call_t c{Device(), buf, sizeof(buf)};
+  Call() = default;
+  Call(const Call&) = delete;  // c points into this object's buffer
+  Call& operator=(const Call&) = delete;
+  const slime_rs_call_t* ptr() const { return &c; }
+  void check(int rc) const {
+    if (rc == SLIME_RS_OK) return;
+    const std::string last = buf;
+    if (rc >= SLIME_RS_ERR_VARYING_LENGTH && rc <= SLIME_RS_ERR_INDEX_RANGE) {
+      std::string msg = slime_rs_status_string(rc);
+      if (rc == SLIME_RS_ERR_INDEX_RANGE && !last.empty()) msg = last;
+      throw Panic(rc, msg);
+    }
+    throw NativeError(rc, std::string("slime_rs error ") + std::to_string(rc) + ": " + last);
+  }
+};
 }  // namespace detail
 
 namespace gf {
@@ -64,7 +81,8 @@ inline uint32_t Raise(uint32_t x, uint32_t n) { return slime_gf_raise(x, n); }
 inline std::pair<uint32_t, std::vector<uint32_t>> MapToGF(const std::vector<uint8_t>& in) {
   std::vector<uint32_t> out((in.size() + 3) / 4);
   uint32_t mapping = 0;
-  detail::check(slime_gf_map_to_gf(in.empty() ? nullptr : in.data(), in.size(), &mapping,
+  slime::detail::Call k;
+  k.check(slime_gf_map_to_gf_ex(k.ptr(), in.empty() ? nullptr : in.data(), in.size(), &mapping,
                                    out.empty() ? nullptr : out.data()));
   return {mapping, std::move(out)};
 }
@@ -72,7 +90,8 @@ inline std::pair<uint32_t, std::vector<uint32_t>> MapToGF(const std::vector<uint
 // gf.MapToGFWith (internal/rs/gf/map.go:74)
 inline std::vector<uint32_t> MapToGFWith(const std::vector<uint8_t>& in, uint32_t n) {
   std::vector<uint32_t> out((in.size() + 3) / 4);
-  detail::check(slime_gf_map_to_gf_with(in.empty() ? nullptr : in.data(), in.size(), n,
+  slime::detail::Call k;
+  k.check(slime_gf_map_to_gf_with_ex(k.ptr(), in.empty() ? nullptr : in.data(), in.size(), n,
                                         out.empty() ? nullptr : out.data()));
   return out;
 }
@@ -80,7 +99,8 @@ inline std::vector<uint32_t> MapToGFWith(const std::vector<uint8_t>& in, uint32_
 // gf.MapFromGF (internal/rs/gf/map.go:103)
 inline std::vector<uint8_t> MapFromGF(uint32_t inn, const std::vector<uint32_t>& inv) {
   std::vector<uint8_t> out(4 * inv.size());
-  detail::check(slime_gf_map_from_gf(inn, inv.empty() ? nullptr : inv.data(), inv.size(),
+  slime::detail::Call k;
+  k.check(slime_gf_map_from_gf_ex(k.ptr(), inn, inv.empty() ? nullptr : inv.data(), inv.size(),
                                      out.empty() ? nullptr : out.data()));
   return out;
 }
@@ -119,14 +139,16 @@ struct Rows {  // pointer + length arrays for the C-ABI (C never keeps them)
 // vandermondeMatrix (internal/rs/matrix.go:8): (d+p) x d, m[i][j] = (j+1)^i.
 inline Matrix vandermondeMatrix(int d, int p) {
   Vector f((size_t)(d + p) * (size_t)(d > 0 ? d : 0));
-  slime::detail::check(slime_rs_vandermonde_matrix(d, p, f.data()));
+  slime::detail::Call k;
+  k.check(slime_rs_vandermonde_matrix_ex(k.ptr(), d, p, f.data()));
   return detail::rows_of(f.data(), d + p, d);
 }
 
 // ParityMatrix (internal/rs/matrix.go:27): systematic (d+p) x d code matrix.
 inline Matrix ParityMatrix(int d, int p) {
   Vector f((size_t)(d + p) * (size_t)(d > 0 ? d : 0));
-  slime::detail::check(slime_rs_parity_matrix(d, p, f.data()));
+  slime::detail::Call k;
+  k.check(slime_rs_parity_matrix_ex(k.ptr(), d, p, f.data()));
   return detail::rows_of(f.data(), d + p, d);
 }
 
@@ -139,7 +161,7 @@ inline const Matrix& ParityMatrixCached(int d, int p) {
   auto it = cache.find({d, p});
   if (it != cache.end()) return *it->second;
   const uint32_t* flat = nullptr;
-  slime::detail::check(slime_rs_parity_matrix_cached(d, p, &flat));
+  slime::detail::Call().check(slime_rs_parity_matrix_cached(d, p, &flat));
   auto m = std::make_unique<Matrix>(detail::rows_of(flat, d + p, d));
   const Matrix& ref = *m;
   cache.emplace(std::make_pair(d, p), std::move(m));
@@ -150,7 +172,8 @@ inline const Matrix& ParityMatrixCached(int d, int p) {
 inline void solveSubIdentity(Matrix& m) {
   if (m.empty()) return;
   Vector f = detail::flat_of(m);
-  slime::detail::check(slime_rs_solve_sub_identity(f.data(), (int)m.size(), (int)m[0].size()));
+  slime::detail::Call k;
+  k.check(slime_rs_solve_sub_identity_ex(k.ptr(), f.data(), (int)m.size(), (int)m[0].size()));
   m = detail::rows_of(f.data(), (int)m.size(), (int)m[0].size());
 }
 
@@ -161,7 +184,8 @@ inline Matrix cloneMatrix(const Matrix& m) { return m; }
 inline Matrix invertMatrix(const Matrix& m) {
   const int d = (int)m.size();
   Vector f = detail::flat_of(m), inv((size_t)d * d);
-  slime::detail::check(slime_rs_invert_matrix(f.data(), d, inv.data()));
+  slime::detail::Call k;
+  k.check(slime_rs_invert_matrix_ex(k.ptr(), f.data(), d, inv.data()));
   return detail::rows_of(inv.data(), d, d);
 }
 
@@ -177,7 +201,8 @@ inline Vector CreateParity(const Matrix& data, int index, Vector out = {}) {
     if (out.capacity() < L) out = Vector();
     out.resize(L);
   }
-  slime::detail::check(slime_rs_create_parity(rows.ptrs.data(), rows.lens.data(), (int)data.size(), index,
+  slime::detail::Call k;
+  k.check(slime_rs_create_parity_ex(k.ptr(), rows.ptrs.data(), rows.lens.data(), (int)data.size(), index,
                                               same ? out.data() : nullptr));
   return out;
 }
@@ -191,7 +216,8 @@ inline Matrix CreateParities(const Matrix& data, int total) {
   Matrix out(r > 0 ? (size_t)r : 0, Vector(L));
   std::vector<uint32_t*> optrs;
   for (Vector& o : out) optrs.push_back(o.data());
-  slime::detail::check(slime_rs_create_parities(rows.ptrs.data(), rows.lens.data(), (int)data.size(), total,
+  slime::detail::Call k;
+  k.check(slime_rs_create_parities_ex(k.ptr(), rows.ptrs.data(), rows.lens.data(), (int)data.size(), total,
                                                 optrs.empty() ? nullptr : optrs.data()));
   return out;
 }
@@ -204,7 +230,8 @@ inline Matrix RecoverData(const Matrix& chunks, const std::vector<int>& indices)
   Matrix out(chunks.size(), Vector(L));
   std::vector<uint32_t*> optrs;
   for (Vector& o : out) optrs.push_back(o.data());
-  slime::detail::check(slime_rs_recover_data(rows.ptrs.data(), rows.lens.data(), (int)chunks.size(),
+  slime::detail::Call k;
+  k.check(slime_rs_recover_data_ex(k.ptr(), rows.ptrs.data(), rows.lens.data(), (int)chunks.size(),
                                              indices.empty() ? nullptr : indices.data(), (int)indices.size(),
                                              optrs.empty() ? nullptr : optrs.data()));
   return out;
@@ -219,7 +246,8 @@ inline std::pair<uint32_t, std::vector<std::vector<uint8_t>>> WriteChunks(const 
   std::vector<uint8_t*> ptrs;
   for (auto& c : chunks) ptrs.push_back(c.data());
   uint32_t mapping = 0;
-  slime::detail::check(slime_rs_write_chunks(data.empty() ? nullptr : data.data(), data.size(), need, total,
+  slime::detail::Call k;
+  k.check(slime_rs_write_chunks_ex(k.ptr(), data.empty() ? nullptr : data.data(), data.size(), need, total,
                                              ptrs.empty() ? nullptr : ptrs.data(), &mapping));
   return {mapping, std::move(chunks)};
 }
@@ -231,7 +259,8 @@ inline std::vector<uint8_t> ReconstructObject(const std::vector<std::vector<uint
   std::vector<const uint8_t*> ptrs;
   for (const auto& c : chunks) ptrs.push_back(c.data());
   std::vector<uint8_t> out(size);
-  slime::detail::check(slime_rs_reconstruct(ptrs.empty() ? nullptr : ptrs.data(),
+  slime::detail::Call k;
+  k.check(slime_rs_reconstruct_ex(k.ptr(), ptrs.empty() ? nullptr : ptrs.data(),
                                             indices.empty() ? nullptr : indices.data(), (int)chunks.size(),
                                             chunks.empty() ? 0 : chunks[0].size(), mapping, size,
                                             out.empty() ? nullptr : out.data()));

@@ -32,6 +32,20 @@ c_intp = ctypes.POINTER(ctypes.c_int)
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 
 
+class Call(ctypes.Structure):
+    """slime_rs_call_t: per-call device and failure-detail buffer (the *_ex forms)."""
+    _fields_ = [("device", ctypes.c_int), ("detail", ctypes.c_char_p), ("detail_cap", ctypes.c_size_t)]
+
+
+class CacheStats(ctypes.Structure):
+    """slime_rs_cache_stats_t."""
+    _fields_ = [("live", ctypes.c_uint64), ("capacity", ctypes.c_uint64), ("hits", ctypes.c_uint64),
+                ("misses", ctypes.c_uint64), ("evictions", ctypes.c_uint64), ("device_tables", ctypes.c_uint64)]
+
+
+ANY_DEVICE = -1
+
+
 class Layout(ctypes.Structure):
     """slime_rs_layout_t: shard s of object o at base + o*obj_stride + s*shard_stride."""
     _fields_ = [("obj_stride", ctypes.c_uint64), ("shard_stride", ctypes.c_uint64)]
@@ -92,11 +106,41 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
       ctypes.c_void_p]),
     ("slime_gf_pack_device", ctypes.c_int,
-     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+     [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p]),
     ("slime_gf_unpack_device", ctypes.c_int,
-     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+     [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_fill_symbols", ctypes.c_int,
      [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+    # *_ex forms (per-call context)
+    ("slime_rs_create_parity_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_create_parities_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_recover_data_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+      ctypes.c_void_p]),
+    ("slime_rs_write_chunks_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, c_u32p]),
+    ("slime_rs_reconstruct_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+      ctypes.c_uint64, ctypes.c_void_p]),
+    ("slime_gf_map_to_gf_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_uint64, c_u32p, ctypes.c_void_p]),
+    ("slime_gf_map_to_gf_with_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    ("slime_gf_map_from_gf_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    ("slime_rs_parity_matrix_ex", ctypes.c_int, [ctypes.POINTER(Call), ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_vandermonde_matrix_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("slime_rs_solve_sub_identity_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    ("slime_rs_invert_matrix_ex", ctypes.c_int, [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    # plan cache / device pool
+    ("slime_rs_plan_cache_stats", ctypes.c_int, [ctypes.POINTER(CacheStats)]),
+    ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
+    ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
 ]
 
 for _name, _res, _args in SIGNATURES:
@@ -154,3 +198,20 @@ def check(rc: int) -> None:
 
 def device_count() -> int:
     return int(lib.slime_rs_device_count())
+
+
+def plan_cache_stats() -> dict:
+    st = CacheStats()
+    check(lib.slime_rs_plan_cache_stats(ctypes.byref(st)))
+    return {f: int(getattr(st, f)) for f, _ in CacheStats._fields_}
+
+
+def set_plan_cache_capacity(cap: int) -> None:
+    check(lib.slime_rs_plan_cache_capacity(cap))
+
+
+def pool_calls(device: int) -> tuple[int, int]:
+    """(host calls routed to `device` by the device pool so far, calls in flight there)."""
+    c, f = ctypes.c_uint64(), ctypes.c_int()
+    check(lib.slime_rs_pool_calls(device, ctypes.byref(c), ctypes.byref(f)))
+    return int(c.value), int(f.value)

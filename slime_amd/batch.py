@@ -36,3 +36,12 @@ def max_over_ranks(values: Sequence[float]) -> list[float]:
 def barrier() -> None:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
+
+
+def gather_strings(s: str) -> list[str]:
+    """One string from every rank, in rank order ([s] when not distributed)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        out: list = [None] * dist.get_world_size()
+        dist.all_gather_object(out, s)
+        return [str(x) for x in out]
+    return [s]

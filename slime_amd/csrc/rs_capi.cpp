@@ -29,10 +29,14 @@
 #include "gfp_host.hpp"
 #include "host_copy.hpp"
 #include "kernels.hpp"
+#include "plan_cache.hpp"
 #include "rs_matrix.hpp"
 
 struct slime_rs_plan {
   int device = 0;
+  // Set by the first launch; slime_rs_plan_set_outputs refuses afterwards
+  // (its table rewrite is not ordered against launches in flight).
+  std::atomic<bool> executed{false};
   uint32_t rows = 0, k = 0;
   uint32_t out_max = 0;         // highest destination shard index
   std::vector<uint32_t> in_idx_host;  // input shard indices (host copy, bounds checks)
@@ -47,7 +51,13 @@ namespace slime {
 namespace {
 
 thread_local std::string t_error;
-thread_local int t_device = 0;
+// Device of the calling thread's host entry points after
+// slime_rs_select_device (-1: not selected, the device pool picks).
+thread_local int t_device = -1;
+// The per-call context of the *_ex entry points (explicit device, detail
+// buffer), active for the duration of that one call on this thread.
+thread_local const slime_rs_call_t* t_call = nullptr;
+std::atomic<int64_t> g_tables_live{0};  // device plan tables allocated and not yet freed
 
 int fail(Status st, std::string detail) {
   t_error = std::move(detail);
@@ -92,6 +102,60 @@ struct DeviceScope {
   }
 };
 
+// ---- device pool (host entry points) -------------------------------------------
+//
+// The reference's callers are concurrent (up to `parallel-requests` HTTP
+// goroutines, main.go:107-109, plus scrubbers, multi.go:54-58), and objects
+// are independent.  A host call that does not name a
+// device takes the visible GPU with the fewest calls in flight (ties: round
+// robin), so concurrent callers spread over every GPU of the node with no
+// data-path exchange.  Each device has its own workspaces and plans.
+struct DevicePool {
+  static constexpr int kMax = 64;
+  std::atomic<int> inflight[kMax] = {};
+  std::atomic<uint64_t> calls[kMax] = {};
+  std::atomic<uint64_t> next{0};
+  int pick() {
+    const int n = std::min(visible_devices(), kMax);
+    const int start = (int)(next.fetch_add(1, std::memory_order_relaxed) % (uint64_t)n);
+    int best = start;
+    for (int i = 1; i < n; ++i) {
+      const int d = (start + i) % n;
+      if (inflight[d].load(std::memory_order_relaxed) < inflight[best].load(std::memory_order_relaxed)) best = d;
+    }
+    return best;
+  }
+};
+DevicePool g_pool;
+
+// The device of one host call: the *_ex call's explicit device, else the
+// thread's selected device, else the pool's pick.  Holds the pool slot for
+// the life of the call.
+struct DeviceLease {
+  int device = -1;
+  bool pooled = false;
+  int acquire() {
+    int want = t_call ? t_call->device : SLIME_RS_ANY_DEVICE;
+    if (want == SLIME_RS_ANY_DEVICE && !t_call) want = t_device;
+    if (want != SLIME_RS_ANY_DEVICE) {
+      if (int rc = check_device(want)) return rc;
+      device = want;
+    } else {
+      if (int rc = check_device(0)) return rc;
+      device = g_pool.pick();
+    }
+    if (device < DevicePool::kMax) {
+      pooled = true;
+      g_pool.inflight[device].fetch_add(1, std::memory_order_relaxed);
+      g_pool.calls[device].fetch_add(1, std::memory_order_relaxed);
+    }
+    return 0;
+  }
+  ~DeviceLease() {
+    if (pooled) g_pool.inflight[device].fetch_sub(1, std::memory_order_relaxed);
+  }
+};
+
 // ---- plans -----------------------------------------------------------------
 
 int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, const std::vector<uint32_t>& in_idx,
@@ -120,6 +184,7 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
     return fail(Status::Hip, "plan table upload failed");
   }
   plan->table = (uint32_t*)p;
+  g_tables_live.fetch_add(1, std::memory_order_relaxed);
   plan->d_coeff = plan->table;
   plan->d_in_idx = plan->table + ncoef;
   plan->d_out_idx = plan->table + ncoef + n_in;
@@ -132,6 +197,7 @@ void destroy_plan(slime_rs_plan* plan) {
   if (plan->table) {
     DeviceScope ds(plan->device);
     (void)hipFree(plan->table);
+    g_tables_live.fetch_sub(1, std::memory_order_relaxed);
   }
   delete plan;
 }
@@ -162,29 +228,30 @@ int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, ui
   // vectorised.  16-byte aligned layouts are faster; pad strides where the
   // layout is yours to choose.
   a.vec_ok = aligned4(src) && aligned4(dst);
+  const_cast<slime_rs_plan*>(plan)->executed.store(true, std::memory_order_relaxed);
   DeviceScope ds(plan->device);
   HIP_TRY(launch_apply(a, stream));
   return 0;
 }
 
-// Plans the host entry points reuse, keyed by (device, kind, shape, indices).
+// Plans the host entry points reuse, keyed by (device, kind, shape, indices):
+// a bounded LRU (plan_cache.hpp).  Env SLIME_RS_PLAN_CACHE sets the capacity
+// (default 256 plans: at 20/40 a recovery plan's table is about 4 KiB).
 using PlanKey = std::tuple<int, char, int, int, std::vector<int>>;
-std::mutex g_plan_mu;
-std::map<PlanKey, slime_rs_plan*> g_plans;
+using PlanRef = std::shared_ptr<slime_rs_plan>;
+// Never destroyed: freeing device tables from a static destructor would run
+// after the HIP runtime may have shut down.
+LruCache<PlanKey, slime_rs_plan>& plans() {
+  static auto* c = new LruCache<PlanKey, slime_rs_plan>([] {
+    const char* e = getenv("SLIME_RS_PLAN_CACHE");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (size_t)v : (size_t)256;
+  }());
+  return *c;
+}
 
-int cached_plan(const PlanKey& key, slime_rs_plan** out,
-                int (*make)(const PlanKey&, slime_rs_plan**)) {
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_plans.find(key);
-  if (it != g_plans.end()) {
-    *out = it->second;
-    return 0;
-  }
-  slime_rs_plan* p = nullptr;
-  if (int rc = make(key, &p)) return rc;
-  g_plans[key] = p;
-  *out = p;
-  return 0;
+int cached_plan(const PlanKey& key, PlanRef* out, int (*make)(const PlanKey&, slime_rs_plan**)) {
+  return plans().get(key, out, make, destroy_plan);
 }
 
 // ---- per-call device workspaces (host entry points) ----------------------------
@@ -676,7 +743,8 @@ int slime_rs_host_pipeline(int mode) {
 }
 
 int slime_rs_select_device(int device) {
-  if (int rc = check_device(device)) return rc;
+  if (device != SLIME_RS_ANY_DEVICE)
+    if (int rc = check_device(device)) return rc;
   t_device = device;
   return 0;
 }
@@ -802,6 +870,11 @@ int slime_rs_plan_execute(slime_rs_plan_t plan, const uint32_t* src, slime_rs_la
 
 int slime_rs_plan_set_outputs(slime_rs_plan_t plan, const int* out_shards) {
   if (!plan || !out_shards) return fail(Status::InvalidArg, "plan_set_outputs: bad args");
+  // The table rewrite below is a synchronous copy that nothing orders against
+  // launches of this plan still in flight on other streams: only before the
+  // plan's first launch.
+  if (plan->executed.load(std::memory_order_relaxed))
+    return fail(Status::InvalidArg, "plan_set_outputs: plan already launched; build a new plan for other outputs");
   std::vector<uint32_t> idx(plan->rows);
   for (uint32_t i = 0; i < plan->rows; ++i) {
     if (out_shards[i] < 0) return fail(Status::InvalidArg, "plan_set_outputs: negative shard index");
@@ -850,6 +923,7 @@ static int check_slots(const slime_rs_plan* plan, const uint8_t* slots, uint64_t
 
 static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
                                 uint64_t S, uint64_t nobj, int phase, uint32_t* flags, const uint32_t* mapping) {
+  const_cast<slime_rs_plan*>(plan)->executed.store(true, std::memory_order_relaxed);
   BytesLaunch a;
   a.slots = slots;
   a.slot_stride = slot_stride;
@@ -960,19 +1034,22 @@ extern "C" int slime_rs_decode_objects(slime_rs_plan_t plan, uint8_t* slots, uin
 
 // ---- device codec / fill ------------------------------------------------------------
 
-int slime_gf_pack_device(const uint8_t* bytes, uint64_t len, uint32_t mapping, uint32_t* words, uint32_t* flags,
-                         void* stream) {
+int slime_gf_pack_device(int device, const uint8_t* bytes, uint64_t len, uint32_t mapping, uint32_t* words,
+                         uint32_t* flags, void* stream) {
   if (len == 0) return 0;
   if (!bytes || !words) return fail(Status::InvalidArg, "pack_device: null buffer");
-  if (int rc = check_device(0)) return rc;
+  if (int rc = check_device(device)) return rc;
+  DeviceScope ds(device);
   HIP_TRY(launch_map_pack(bytes, len, mapping, words, flags, (hipStream_t)stream));
   return 0;
 }
 
-int slime_gf_unpack_device(const uint32_t* words, uint64_t count, uint32_t mapping, uint8_t* bytes, void* stream) {
+int slime_gf_unpack_device(int device, const uint32_t* words, uint64_t count, uint32_t mapping, uint8_t* bytes,
+                           void* stream) {
   if (count == 0) return 0;
   if (!bytes || !words) return fail(Status::InvalidArg, "unpack_device: null buffer");
-  if (int rc = check_device(0)) return rc;
+  if (int rc = check_device(device)) return rc;
+  DeviceScope ds(device);
   HIP_TRY(launch_map_unpack(words, count, mapping, bytes, (hipStream_t)stream));
   return 0;
 }
@@ -1005,11 +1082,11 @@ static int make_rows_plan(const PlanKey& key, slime_rs_plan** out) {
 
 static int run_rows(int need, const std::vector<int>& rows, const uint32_t* const* data, uint64_t L,
                     uint32_t* const* out) {
-  const int dev = t_device;
-  if (int rc = check_device(dev)) return rc;
-  slime_rs_plan* plan = nullptr;
-  if (int rc = cached_plan(PlanKey{dev, 'P', need, 0, rows}, &plan, make_rows_plan)) return rc;
-  return host_apply(plan, data, out, L);
+  DeviceLease dl;
+  if (int rc = dl.acquire()) return rc;
+  PlanRef plan;
+  if (int rc = cached_plan(PlanKey{dl.device, 'P', need, 0, rows}, &plan, make_rows_plan)) return rc;
+  return host_apply(plan.get(), data, out, L);
 }
 
 int slime_rs_create_parity(const uint32_t* const* data, const uint64_t* lens, int ndata, int index, uint32_t* out) {
@@ -1103,12 +1180,12 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   for (int i = 0; i < need; ++i)
     if (!chunks[i] || !out[i]) return fail(Status::InvalidArg, "RecoverData: null buffer");
 
-  const int dev = t_device;
-  if (int rc = check_device(dev)) return rc;
+  DeviceLease dl;
+  if (int rc = dl.acquire()) return rc;
   std::vector<int> have(indices, indices + nindices);
-  slime_rs_plan* plan = nullptr;
-  if (int rc = cached_plan(PlanKey{dev, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
-  return host_apply(plan, chunks, out, L);
+  PlanRef plan;
+  if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
+  return host_apply(plan.get(), chunks, out, L);
 }
 
 // ---- object entry points (host memory): writeChunks / reconstruct ------------------
@@ -1134,20 +1211,64 @@ static int make_object_recover_plan(const PlanKey& key, slime_rs_plan** out) {
 
 uint64_t slime_rs_chunk_size(uint64_t size, int need) { return need > 0 ? 4 * slot_L(size, (uint32_t)need) : 0; }
 
+// writeChunks of a code with no parity (need == total; checkConfig admits it,
+// multi_config.go:36, and the reference's own tests run 1-of-1 stores,
+// multi_test.go:179,257): only MapToGF's mapping depends on the data, so it
+// is chosen on the device (pick_mapping) and the chunks are then written on
+// the host.  Chunk j = MapFromGF(m, part j): the object's own bytes (the
+// mapping cancels, map.go:15-33,103-113), zero low bytes in the object's
+// partial last word, then splitVector's zero padding symbols, which
+// serialise as BE(m) (multi_store.go:279-296).
+static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, uint32_t* d_words,
+                        uint32_t* d_scratch, uint32_t* mapping);
+
+static int write_data_chunks(int dev, const uint8_t* data, uint64_t size, int need, uint8_t* const* chunks,
+                             uint32_t* mapping) {
+  const uint64_t L = slot_L(size, (uint32_t)need), chunk = 4 * L, nw = (size + 3) / 4;
+  WsLease lease;
+  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+  Workspace* ws = lease.ws;
+  DeviceScope ds(dev);
+  const size_t bbytes = round16(size), wbytes = round16(nw * 4);
+  if (int rc = ws->reserve(bbytes + wbytes + 4 * (4 + 2 * 64))) return rc;
+  uint8_t* d_bytes = ws->dbuf;
+  uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
+  HIP_TRY(hipMemcpyAsync(d_bytes, data, size, hipMemcpyHostToDevice, ws->stream));
+  uint32_t m = 0;
+  if (int rc = pick_mapping(ws->stream, d_bytes, size, d_words, (uint32_t*)(ws->dbuf + bbytes + wbytes), &m))
+    return rc;
+  const uint8_t pad[4] = {(uint8_t)(m >> 24), (uint8_t)(m >> 16), (uint8_t)(m >> 8), (uint8_t)m};
+  const uint64_t word_end = 4 * nw;  // end of the object's last (possibly partial) word
+  for (int j = 0; j < need; ++j) {
+    const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk;
+    uint8_t* c = chunks[j];
+    const uint64_t body = size > lo ? std::min(size, hi) - lo : 0;
+    if (body) memcpy(c, data + lo, body);
+    const uint64_t zero_end = word_end > lo ? std::min(word_end, hi) - lo : 0;
+    if (zero_end > body) memset(c + body, 0, zero_end - body);
+    for (uint64_t o = std::max(body, zero_end); o < chunk; o += 4) memcpy(c + o, pad, 4);
+  }
+  *mapping = m;
+  return 0;
+}
+
 int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
                           uint32_t* mapping) {
   if (!mapping) return fail(Status::InvalidArg, "write_chunks: null mapping");
   *mapping = 0;
-  if (need < 1 || total <= need) return fail(Status::InvalidArg, "write_chunks: need must be >= 1 and total > need");
+  if (need < 1 || total < need) return fail(Status::InvalidArg, "write_chunks: need must be >= 1 and total >= need");
   const uint64_t L = slot_L(size, (uint32_t)need);
   if (L == 0) return 0;  // MapToGF(empty) = (0, []): every chunk is empty
   if (!data || !chunks) return fail(Status::InvalidArg, "write_chunks: null buffer");
   for (int i = 0; i < total; ++i)
     if (!chunks[i]) return fail(Status::InvalidArg, "write_chunks: null chunk buffer");
-  const int dev = t_device;
-  if (int rc = check_device(dev)) return rc;
-  slime_rs_plan* plan = nullptr;
-  if (int rc = cached_plan(PlanKey{dev, 'E', need, total, {}}, &plan, make_encode_plan)) return rc;
+  DeviceLease dl;
+  if (int rc = dl.acquire()) return rc;
+  const int dev = dl.device;
+  if (total == need) return write_data_chunks(dev, data, size, need, chunks, mapping);
+  PlanRef plan_ref;
+  if (int rc = cached_plan(PlanKey{dev, 'E', need, total, {}}, &plan_ref, make_encode_plan)) return rc;
+  slime_rs_plan* const plan = plan_ref.get();
   WsLease lease;
   if (int rc = acquire_ws(dev, &lease.ws)) return rc;
   Workspace* ws = lease.ws;
@@ -1226,8 +1347,24 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   if (need == 0) return status_of(Status::Empty, "RecoverData");
   if (!chunks || !indices) return fail(Status::InvalidArg, "reconstruct: bad args");
   if (int rc = check_survivors(need, indices)) return rc;
-  if (chunk_bytes % 4) return fail(Status::InvalidArg, "reconstruct: chunk_bytes must be a multiple of 4");
   if (size && !out) return fail(Status::InvalidArg, "reconstruct: null out");
+  if (chunk_bytes % 4) {
+    // Chunks of a length no writer produces (truncated or corrupt stored
+    // chunks).  MapToGFWith packs a partial last word with zero low bytes
+    // (map.go:16-33,74-98), so each survivor is its bytes zero-padded to
+    // 4*ceil(chunk_bytes/4), and each recovered data row is that long too
+    // (RecoverData, vector.go:80-85; MapFromGF, map.go:103-113).  Rare and
+    // never on the fast path: stage padded copies and run the normal path.
+    const uint64_t padded = (chunk_bytes + 3) & ~(uint64_t)3;
+    std::vector<std::vector<uint8_t>> copy((size_t)need, std::vector<uint8_t>(padded, 0));
+    std::vector<const uint8_t*> ptrs((size_t)need);
+    for (int q = 0; q < need; ++q) {
+      if (!chunks[q]) return fail(Status::InvalidArg, "reconstruct: null chunk");
+      memcpy(copy[q].data(), chunks[q], chunk_bytes);
+      ptrs[q] = copy[q].data();
+    }
+    return slime_rs_reconstruct(ptrs.data(), indices, need, padded, mapping, size, out);
+  }
   const uint64_t L = chunk_bytes / 4, body_bytes = (uint64_t)need * chunk_bytes, got = std::min(size, body_bytes);
   // data[:f.Size] of a make([]byte, 0, Size+16) buffer (multi_store.go:203,241):
   // bytes past the recovered ones are the zeroed capacity.
@@ -1235,11 +1372,13 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   if (got == 0) return 0;
   for (int q = 0; q < need; ++q)
     if (!chunks[q]) return fail(Status::InvalidArg, "reconstruct: null chunk");
-  const int dev = t_device;
-  if (int rc = check_device(dev)) return rc;
+  DeviceLease dl;
+  if (int rc = dl.acquire()) return rc;
+  const int dev = dl.device;
   std::vector<int> have(indices, indices + need);
-  slime_rs_plan* plan = nullptr;
-  if (int rc = cached_plan(PlanKey{dev, 'O', need, 0, have}, &plan, make_object_recover_plan)) return rc;
+  PlanRef plan_ref;
+  if (int rc = cached_plan(PlanKey{dev, 'O', need, 0, have}, &plan_ref, make_object_recover_plan)) return rc;
+  slime_rs_plan* const plan = plan_ref.get();
   WsLease lease;
   if (int rc = acquire_ws(dev, &lease.ws)) return rc;
   Workspace* ws = lease.ws;
@@ -1281,10 +1420,9 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
 
 // ---- gf codec (host memory) -----------------------------------------------------------
 
-static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease) {
-  const int dev = t_device;
-  if (int rc = check_device(dev)) return rc;
-  if (int rc = acquire_ws(dev, &lease.ws)) return rc;
+static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease, DeviceLease& dl) {
+  if (int rc = dl.acquire()) return rc;
+  if (int rc = acquire_ws(dl.device, &lease.ws)) return rc;
   *wsp = lease.ws;
   return (*wsp)->reserve(bytes_needed);
 }
@@ -1296,7 +1434,8 @@ int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t bbytes = round16(len);
-  if (int rc = codec_setup(bbytes + round16(nw * 4), &ws, lease)) return rc;
+  DeviceLease dl;
+  if (int rc = codec_setup(bbytes + round16(nw * 4), &ws, lease, dl)) return rc;
   DeviceScope ds(ws->device);
   uint8_t* d_bytes = ws->dbuf;
   uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
@@ -1305,6 +1444,48 @@ int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_
   HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
   HIP_TRY(hipStreamSynchronize(ws->stream));
   return 0;
+}
+
+// gf.MapToGF's choice of mapping (map.go:35-66) for `len` bytes already on
+// the device: pack them (mapping 0) into d_words, OR-reduce the two flags,
+// then 0, else 1<<31, else the first fitting value of the library's random
+// candidate stream (64 per device probe pass).  d_scratch holds 4 + 2*64 words.
+static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, uint32_t* d_words,
+                        uint32_t* d_scratch, uint32_t* mapping) {
+  constexpr uint32_t kCand = 64;
+  const uint64_t nw = (len + 3) / 4;
+  uint32_t* d_flags = d_scratch;
+  uint32_t* d_cand = d_flags + 4;
+  uint32_t* d_bad = d_cand + kCand;
+  uint32_t flags = 0;
+  HIP_TRY(hipMemsetAsync(d_flags, 0, 4, st));
+  HIP_TRY(launch_map_pack(d_bytes, len, 0, d_words, d_flags, st));
+  HIP_TRY(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *mapping = 0;
+  if (!(flags & 1u)) return 0;
+  if (!(flags & 2u)) {
+    *mapping = 1u << 31;  // map.go:47: try just switching the high bit first
+    return 0;
+  }
+  for (int round = 0; round < (1 << 16); ++round) {  // map.go:64-66
+    uint32_t cand[kCand], bad[kCand];
+    {
+      std::lock_guard<std::mutex> lk(g_rng_mu);
+      for (uint32_t c = 0; c < kCand; ++c) cand[c] = (uint32_t)(g_rng() >> 32);
+    }
+    HIP_TRY(hipMemcpyAsync(d_cand, cand, sizeof(cand), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(bad), st));
+    HIP_TRY(launch_mapping_probe(d_words, nw, d_cand, kCand, d_bad, st));
+    HIP_TRY(hipMemcpyAsync(bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (uint32_t c = 0; c < kCand; ++c)
+      if (!bad[c]) {
+        *mapping = cand[c];
+        return 0;
+      }
+  }
+  return status_of(Status::MappingFallback, "MapToGF");
 }
 
 int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
@@ -1316,49 +1497,16 @@ int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint3
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t bbytes = round16(len), wbytes = round16(nw * 4);
-  constexpr uint32_t kCand = 64;
-  if (int rc = codec_setup(bbytes + wbytes + 16 + 2 * kCand * 4, &ws, lease)) return rc;
+  DeviceLease dl;
+  if (int rc = codec_setup(bbytes + wbytes + 4 * (4 + 2 * 64), &ws, lease, dl)) return rc;
   DeviceScope ds(ws->device);
   uint8_t* d_bytes = ws->dbuf;
   uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
-  uint32_t* d_flags = (uint32_t*)(ws->dbuf + bbytes + wbytes);
-  uint32_t* d_cand = d_flags + 4;
-  uint32_t* d_bad = d_cand + kCand;
-  uint32_t flags = 0;
+  uint32_t* d_scratch = (uint32_t*)(ws->dbuf + bbytes + wbytes);
   HIP_TRY(hipMemcpyAsync(d_bytes, in, len, hipMemcpyHostToDevice, ws->stream));
-  HIP_TRY(hipMemsetAsync(d_flags, 0, 4, ws->stream));
-  HIP_TRY(launch_map_pack(d_bytes, len, 0, d_words, d_flags, ws->stream));
-  HIP_TRY(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
   uint32_t m = 0;
-  if (flags & 1u) {
-    if (!(flags & 2u)) {
-      m = 1u << 31;  // map.go:47: try just switching the high bit first
-    } else {
-      // map.go:64-66: random candidates until one fits; 64 per device pass.
-      bool found = false;
-      for (int round = 0; round < (1 << 16) && !found; ++round) {
-        uint32_t cand[kCand], bad[kCand];
-        {
-          std::lock_guard<std::mutex> lk(g_rng_mu);
-          for (uint32_t c = 0; c < kCand; ++c) cand[c] = (uint32_t)(g_rng() >> 32);
-        }
-        HIP_TRY(hipMemcpyAsync(d_cand, cand, sizeof(cand), hipMemcpyHostToDevice, ws->stream));
-        HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(bad), ws->stream));
-        HIP_TRY(launch_mapping_probe(d_words, nw, d_cand, kCand, d_bad, ws->stream));
-        HIP_TRY(hipMemcpyAsync(bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, ws->stream));
-        HIP_TRY(hipStreamSynchronize(ws->stream));
-        for (uint32_t c = 0; c < kCand; ++c)
-          if (!bad[c]) {
-            m = cand[c];
-            found = true;
-            break;
-          }
-      }
-      if (!found) return status_of(Status::MappingFallback, "MapToGF");
-    }
-    HIP_TRY(launch_xor_words(d_words, nw, m, ws->stream));
-  }
+  if (int rc = pick_mapping(ws->stream, d_bytes, len, d_words, d_scratch, &m)) return rc;
+  if (m) HIP_TRY(launch_xor_words(d_words, nw, m, ws->stream));
   HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
   HIP_TRY(hipStreamSynchronize(ws->stream));
   *mapping = m;
@@ -1371,7 +1519,8 @@ int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t wbytes = round16(count * 4);
-  if (int rc = codec_setup(2 * wbytes, &ws, lease)) return rc;
+  DeviceLease dl;
+  if (int rc = codec_setup(2 * wbytes, &ws, lease, dl)) return rc;
   DeviceScope ds(ws->device);
   uint32_t* d_words = (uint32_t*)ws->dbuf;
   uint8_t* d_bytes = ws->dbuf + wbytes;
@@ -1379,6 +1528,131 @@ int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t
   HIP_TRY(launch_map_unpack(d_words, count, n, d_bytes, ws->stream));
   HIP_TRY(hipMemcpyAsync(out, d_bytes, count * 4, hipMemcpyDeviceToHost, ws->stream));
   HIP_TRY(hipStreamSynchronize(ws->stream));
+  return 0;
+}
+
+// ---- per-call context entry points (cgo) ------------------------------------------
+//
+// A goroutine can move to another OS thread between two cgo calls, so the
+// shim must not read thread-local state in a second call: each *_ex entry
+// point takes the device explicitly and returns the failure detail of THIS
+// call in the caller's buffer.
+
+namespace {
+struct CallScope {
+  const slime_rs_call_t* prev;
+  const slime_rs_call_t* call;
+  explicit CallScope(const slime_rs_call_t* c) : prev(t_call), call(c) {
+    t_call = c;
+    t_error.clear();
+  }
+  int done(int rc) {
+    if (call && call->detail && call->detail_cap) {
+      const std::string& d = rc ? t_error : std::string();
+      const size_t n = std::min(d.size(), call->detail_cap - 1);
+      memcpy(call->detail, d.data(), n);
+      call->detail[n] = 0;
+    }
+    t_call = prev;
+    return rc;
+  }
+};
+int bad_call(const slime_rs_call_t* call) {
+  if (!call) return fail(Status::InvalidArg, "null call context");
+  if (call->device != SLIME_RS_ANY_DEVICE && call->device < 0)
+    return fail(Status::InvalidArg, "call context: device must be >= 0 or SLIME_RS_ANY_DEVICE");
+  return 0;
+}
+}  // namespace
+
+#define SLIME_EX(call, expr)                      \
+  do {                                            \
+    CallScope cs_(call);                          \
+    if (int rc_ = bad_call(call)) return cs_.done(rc_); \
+    return cs_.done(expr);                        \
+  } while (0)
+
+int slime_rs_create_parity_ex(const slime_rs_call_t* call, const uint32_t* const* data, const uint64_t* lens,
+                              int ndata, int index, uint32_t* out) {
+  SLIME_EX(call, slime_rs_create_parity(data, lens, ndata, index, out));
+}
+
+int slime_rs_create_parities_ex(const slime_rs_call_t* call, const uint32_t* const* data, const uint64_t* lens,
+                                int ndata, int total, uint32_t* const* out) {
+  SLIME_EX(call, slime_rs_create_parities(data, lens, ndata, total, out));
+}
+
+int slime_rs_recover_data_ex(const slime_rs_call_t* call, const uint32_t* const* chunks, const uint64_t* lens,
+                             int nchunks, const int* indices, int nindices, uint32_t* const* out) {
+  SLIME_EX(call, slime_rs_recover_data(chunks, lens, nchunks, indices, nindices, out));
+}
+
+int slime_rs_write_chunks_ex(const slime_rs_call_t* call, const uint8_t* data, uint64_t size, int need, int total,
+                             uint8_t* const* chunks, uint32_t* mapping) {
+  SLIME_EX(call, slime_rs_write_chunks(data, size, need, total, chunks, mapping));
+}
+
+int slime_rs_reconstruct_ex(const slime_rs_call_t* call, const uint8_t* const* chunks, const int* indices, int need,
+                            uint64_t chunk_bytes, uint32_t mapping, uint64_t size, uint8_t* out) {
+  SLIME_EX(call, slime_rs_reconstruct(chunks, indices, need, chunk_bytes, mapping, size, out));
+}
+
+int slime_gf_map_to_gf_ex(const slime_rs_call_t* call, const uint8_t* in, uint64_t len, uint32_t* mapping,
+                          uint32_t* out) {
+  SLIME_EX(call, slime_gf_map_to_gf(in, len, mapping, out));
+}
+
+int slime_gf_map_to_gf_with_ex(const slime_rs_call_t* call, const uint8_t* in, uint64_t len, uint32_t n,
+                               uint32_t* out) {
+  SLIME_EX(call, slime_gf_map_to_gf_with(in, len, n, out));
+}
+
+int slime_gf_map_from_gf_ex(const slime_rs_call_t* call, uint32_t n, const uint32_t* in, uint64_t count,
+                            uint8_t* out) {
+  SLIME_EX(call, slime_gf_map_from_gf(n, in, count, out));
+}
+
+int slime_rs_parity_matrix_ex(const slime_rs_call_t* call, int d, int p, uint32_t* out) {
+  SLIME_EX(call, slime_rs_parity_matrix(d, p, out));
+}
+
+int slime_rs_vandermonde_matrix_ex(const slime_rs_call_t* call, int d, int p, uint32_t* out) {
+  SLIME_EX(call, slime_rs_vandermonde_matrix(d, p, out));
+}
+
+int slime_rs_solve_sub_identity_ex(const slime_rs_call_t* call, uint32_t* m, int rows, int cols) {
+  SLIME_EX(call, slime_rs_solve_sub_identity(m, rows, cols));
+}
+
+int slime_rs_invert_matrix_ex(const slime_rs_call_t* call, const uint32_t* m, int d, uint32_t* inv) {
+  SLIME_EX(call, slime_rs_invert_matrix(m, d, inv));
+}
+#undef SLIME_EX
+
+// ---- plan cache / device pool introspection ---------------------------------------
+
+int slime_rs_plan_cache_stats(slime_rs_cache_stats_t* st) {
+  if (!st) return fail(Status::InvalidArg, "plan_cache_stats: null");
+  LruCache<PlanKey, slime_rs_plan>& c = plans();
+  st->live = c.size();
+  st->capacity = c.capacity();
+  st->hits = c.hits();
+  st->misses = c.misses();
+  st->evictions = c.evictions();
+  st->device_tables = (uint64_t)std::max<int64_t>(0, g_tables_live.load());
+  return 0;
+}
+
+int slime_rs_plan_cache_capacity(uint64_t capacity) {
+  if (capacity == 0) return fail(Status::InvalidArg, "plan_cache_capacity: must be >= 1");
+  plans().set_capacity((size_t)capacity);
+  return 0;
+}
+
+int slime_rs_pool_calls(int device, uint64_t* calls, int* inflight) {
+  if (device < 0 || device >= DevicePool::kMax) return fail(Status::InvalidArg, "pool_calls: device out of range");
+  if (calls) *calls = g_pool.calls[device].load();
+  if (inflight) *inflight = g_pool.inflight[device].load();
   return 0;
 }
 

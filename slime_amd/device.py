@@ -134,7 +134,9 @@ def pack_bytes(src: torch.Tensor, mapping: int, words: torch.Tensor, flags: Opti
     if words.numel() < (src.numel() + 3) // 4:
         raise ValueError("words tensor too small")
     fp = ctypes.c_void_p(flags.data_ptr()) if flags is not None else None
-    N.check(lib.slime_gf_pack_device(ctypes.c_void_p(src.data_ptr()), src.numel(), mapping & 0xFFFFFFFF,
+    if _dev_index(words) != dev or (flags is not None and _dev_index(flags) != dev):
+        raise ValueError("pack_bytes: tensors on different devices")
+    N.check(lib.slime_gf_pack_device(dev, ctypes.c_void_p(src.data_ptr()), src.numel(), mapping & 0xFFFFFFFF,
                                      ctypes.c_void_p(words.data_ptr()), fp, _stream_handle(dev, stream)))
 
 
@@ -144,7 +146,9 @@ def unpack_words(words: torch.Tensor, mapping: int, dst: torch.Tensor,
     dev = _dev_index(words)
     if dst.numel() < 4 * words.numel():
         raise ValueError("byte tensor too small")
-    N.check(lib.slime_gf_unpack_device(ctypes.c_void_p(words.data_ptr()), words.numel(), mapping & 0xFFFFFFFF,
+    if _dev_index(dst) != dev:
+        raise ValueError("unpack_words: tensors on different devices")
+    N.check(lib.slime_gf_unpack_device(dev, ctypes.c_void_p(words.data_ptr()), words.numel(), mapping & 0xFFFFFFFF,
                                        ctypes.c_void_p(dst.data_ptr()), _stream_handle(dev, stream)))
 
 
@@ -170,8 +174,8 @@ def encode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, object_siz
     _, _, need_bytes = slot_geometry(object_size, plan.k, plan.k + plan.rows)
     dev = _check_slots(slots, slot_stride, nobj, need_bytes)
     for t in (mapping, status):
-        if t.numel() < nobj or t.dtype not in (torch.int32, torch.uint32):
-            raise ValueError("mapping/status need nobj int32 words")
+        if t.numel() < nobj or t.dtype not in (torch.int32, torch.uint32) or _dev_index(t) != dev:
+            raise ValueError("mapping/status need nobj int32 words on the slots' device")
     N.check(lib.slime_rs_encode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, object_size, nobj,
                                         ctypes.c_void_p(mapping.data_ptr()), ctypes.c_void_p(status.data_ptr()),
                                         _stream_handle(dev, stream)))
@@ -196,5 +200,7 @@ def decode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, L: int, no
     """Device reconstruct: rebuild the plan's output chunks from its input chunks in every slot."""
     hi = max(plan.in_max, plan.rows - 1 if plan.out_max is None else plan.out_max)
     dev = _check_slots(slots, slot_stride, nobj, 4 * L * (hi + 1))
+    if mapping.numel() < nobj or mapping.dtype not in (torch.int32, torch.uint32) or _dev_index(mapping) != dev:
+        raise ValueError("mapping needs nobj int32 words on the slots' device")
     N.check(lib.slime_rs_decode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, L, nobj,
                                         ctypes.c_void_p(mapping.data_ptr()), _stream_handle(dev, stream)))

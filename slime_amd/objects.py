@@ -25,6 +25,23 @@ def chunk_size(size: int, need: int) -> int:
     return int(lib.slime_rs_chunk_size(size, need))
 
 
+def split_vector(data: np.ndarray, count: int) -> list[np.ndarray]:
+    """The caller's splitVector (multi_store.go:271-299), for callers that keep
+    the reference's call-by-call path: `count` parts of ceil(len/count)
+    symbols, views into `data` where whole, a zero-padded copy for the short
+    tail part and any empty trailing parts."""
+    per = -(-data.size // count)
+    parts = []
+    for i in range(count):
+        p = data[i * per:(i + 1) * per]
+        if p.size != per:
+            q = np.zeros(per, dtype=np.uint32)
+            q[:p.size] = p
+            p = q
+        parts.append(p)
+    return parts
+
+
 def _bytes_view(data) -> np.ndarray:
     if isinstance(data, np.ndarray):
         return np.ascontiguousarray(data).view(np.uint8).reshape(-1)

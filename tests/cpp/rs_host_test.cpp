@@ -13,6 +13,7 @@
 //   cpu: host-only tests (matrices, scalars, validation panics) -- no device
 //   gpu: data-path tests through the HIP kernels (needs an MI355X)
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -21,6 +22,7 @@
 #include <random>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "slime_rs.hpp"
@@ -269,7 +271,131 @@ TEST_CPU(TestValidationPanics) {  // vector.go:19-23, :51-57 -- reached before a
   EXPECT(panic_text([] { rs::RecoverData({}, {}); }) == "RecoverData: len(chunks) == 0");
 }
 
+// The cgo contract: each *_ex call returns its own
+// failure detail, whatever other threads fail with meanwhile, so a goroutine
+// that changes OS threads between calls still panics with its own text
+// (vector.go:18-88's panics, concurrent callers as at main.go:107-109).
+TEST_CPU(TestCallDetailPerCall) {
+  std::atomic<int> bad{0};
+  std::vector<std::thread> ts;
+  ts.emplace_back([&] {  // CreateParity index -k: Go's index-out-of-range text (code 8)
+    const uint32_t x[2] = {1, 2};
+    const uint32_t* d[2] = {x, x};
+    const uint64_t lens[2] = {2, 2};
+    for (int it = 0; it < 3000; ++it) {
+      char buf[256];
+      slime_rs_call_t c{SLIME_RS_ANY_DEVICE, buf, sizeof(buf)};
+      const int index = -(1 + it % 7);
+      const int rc = slime_rs_create_parity_ex(&c, d, lens, 2, index, nullptr);
+      if (rc != SLIME_RS_ERR_INDEX_RANGE ||
+          std::string(buf) != "runtime error: index out of range [" + std::to_string(index) + "]")
+        ++bad;
+    }
+  });
+  ts.emplace_back([&] {  // RecoverData with a short chunk: a different code-8 text per call
+    const uint32_t x[3] = {1, 2, 3};
+    const uint32_t* d[2] = {x, x};
+    const int idx[2] = {0, 1};
+    for (int it = 0; it < 3000; ++it) {
+      char buf[256];
+      slime_rs_call_t c{SLIME_RS_ANY_DEVICE, buf, sizeof(buf)};
+      const uint64_t short_len = (uint64_t)(it % 3);
+      const uint64_t lens[2] = {3, short_len};
+      const int rc = slime_rs_recover_data_ex(&c, d, lens, 2, idx, 2, nullptr);
+      const std::string want = "runtime error: index out of range [" + std::to_string(short_len) + "] with length " +
+                               std::to_string(short_len);
+      if (rc != SLIME_RS_ERR_INDEX_RANGE || std::string(buf) != want) ++bad;
+    }
+  });
+  ts.emplace_back([&] {  // varying lengths: code 1, its own detail
+    const uint32_t x[3] = {1, 2, 3};
+    const uint32_t* d[2] = {x, x};
+    const uint64_t lens[2] = {3, 2};
+    for (int it = 0; it < 3000; ++it) {
+      char buf[256];
+      slime_rs_call_t c{SLIME_RS_ANY_DEVICE, buf, sizeof(buf)};
+      const int rc = slime_rs_create_parity_ex(&c, d, lens, 2, 2, nullptr);
+      if (rc != SLIME_RS_ERR_VARYING_LENGTH || std::string(buf).find("varying length") == std::string::npos) ++bad;
+    }
+  });
+  ts.emplace_back([&] {  // successes report an empty detail
+    std::vector<uint32_t> m(12 * 8);
+    for (int it = 0; it < 3000; ++it) {
+      char buf[256] = "stale";
+      slime_rs_call_t c{SLIME_RS_ANY_DEVICE, buf, sizeof(buf)};
+      if (slime_rs_parity_matrix_ex(&c, 8, 4, m.data()) != SLIME_RS_OK || buf[0] != 0) ++bad;
+    }
+  });
+  for (auto& t : ts) t.join();
+  EXPECT(bad.load() == 0);
+  // A detail longer than the caller's buffer is truncated, still NUL-terminated.
+  char tiny[8];
+  slime_rs_call_t c{SLIME_RS_ANY_DEVICE, tiny, sizeof(tiny)};
+  const uint32_t x[1] = {1};
+  const uint32_t* d[1] = {x};
+  const uint64_t lens[1] = {1};
+  EXPECT(slime_rs_create_parity_ex(&c, d, lens, 1, -5, nullptr) == SLIME_RS_ERR_INDEX_RANGE);
+  EXPECT(std::string(tiny) == "runtime");
+  // A bad context is refused before anything runs.
+  slime_rs_call_t neg{-7, tiny, sizeof(tiny)};
+  EXPECT(slime_rs_parity_matrix_ex(&neg, 4, 2, nullptr) == SLIME_RS_ERR_INVALID_ARG);
+}
+
+// checkConfig admits need == total (multi_config.go:36; the reference's own
+// multi-store tests run 1-of-1, multi_test.go:179,257): writeChunks must not
+// reject it.  total < need is a caller error.
+TEST_CPU(TestWriteChunksConfigChecks) {
+  const std::vector<uint8_t> obj(1000, 7);
+  std::vector<std::vector<uint8_t>> chunks(3, std::vector<uint8_t>(slime_rs_chunk_size(obj.size(), 3)));
+  std::vector<uint8_t*> ptrs;
+  for (auto& ch : chunks) ptrs.push_back(ch.data());
+  uint32_t m = 0;
+  char buf[256];
+  slime_rs_call_t c{SLIME_RS_ANY_DEVICE, buf, sizeof(buf)};
+  const int rc = slime_rs_write_chunks_ex(&c, obj.data(), obj.size(), 3, 3, ptrs.data(), &m);
+  EXPECT(rc == SLIME_RS_OK || rc == SLIME_RS_ERR_NO_DEVICE);  // never INVALID_ARG
+  EXPECT(slime_rs_write_chunks_ex(&c, obj.data(), obj.size(), 3, 2, ptrs.data(), &m) == SLIME_RS_ERR_INVALID_ARG);
+}
+
 // ---------------------------------------------------------------- data path
+TEST_GPU(TestWriteChunksNoParity) {  // need == total: chunks are MapFromGF(m, splitVector parts)
+  std::mt19937_64 rng(11);
+  for (int need : {1, 3}) {
+    for (size_t size : {(size_t)1, (size_t)5, (size_t)4099, (size_t)100003}) {
+      for (int force_high : {0, 1}) {
+        std::vector<uint8_t> obj(size);
+        for (uint8_t& b : obj) b = (uint8_t)rng();
+        if (force_high && size >= 4) obj[0] = obj[1] = obj[2] = obj[3] = 0xFF;  // a word >= p: mapping != 0
+        const auto [m, chunks] = rs::WriteChunks(obj, need, need);
+        const auto [m_ref, words] = gf::MapToGF(obj);
+        EXPECT(m == m_ref);
+        EXPECT(force_high == 0 || size < 4 || m != 0);
+        const size_t L = chunks[0].size() / 4;
+        Matrix parts((size_t)need, Vector(L, 0));
+        for (size_t w = 0; w < words.size(); ++w) parts[w / L][w % L] = words[w];
+        for (int i = 0; i < need; ++i) EXPECT(gf::MapFromGF(m, parts[i]) == chunks[i]);
+      }
+    }
+  }
+}
+
+TEST_GPU(TestDevicePool) {  // calls without a pinned device go through the pool (one GPU here)
+  const int n = slime_rs_device_count();
+  EXPECT(n >= 1);
+  std::vector<uint64_t> before(n);
+  for (int d = 0; d < n; ++d) EXPECT(slime_rs_pool_calls(d, &before[d], nullptr) == SLIME_RS_OK);
+  for (int i = 0; i < 10; ++i) EXPECT(rs::CreateParity({{0, 0, 0}, {1, 2, 3}}, 2) == Vector({3, 6, 9}));
+  uint64_t routed = 0;
+  for (int d = 0; d < n; ++d) {
+    uint64_t now = 0;
+    int inflight = -1;
+    EXPECT(slime_rs_pool_calls(d, &now, &inflight) == SLIME_RS_OK);
+    EXPECT(inflight == 0);
+    routed += now - before[d];
+  }
+  EXPECT(routed == 10);
+}
+
 TEST_GPU(TestCreateParity) {  // vector_test.go:24-63
   for (const Json& c : kats()["create_parity"].arr)
     EXPECT(rs::CreateParity(c["data"].mat(), (int)c["index"].u()) == c["out"].vec());

@@ -24,12 +24,27 @@ def _run(group: str) -> str:
 def test_cpp_host_mirror_host_only():
     out = _run("cpu")
     for name in ("TestVandermonde", "TestParityMatrix", "TestParityMatrixInvertible", "TestMInverse",
-                 "TestValidationPanics"):
+                 "TestValidationPanics", "TestCallDetailPerCall", "TestWriteChunksConfigChecks"):
         assert f"ok   {name}" in out
 
 
 @pytest.mark.gpu
 def test_cpp_host_mirror_data_path():
     out = _run("gpu")
-    for name in ("TestCreateParity", "TestRecovery", "TestMapTrivial", "TestMapTricky", "TestWriteChunksRoundTrip"):
+    for name in ("TestCreateParity", "TestRecovery", "TestMapTrivial", "TestMapTricky", "TestWriteChunksRoundTrip",
+                 "TestWriteChunksNoParity", "TestDevicePool"):
         assert f"ok   {name}" in out
+
+
+CACHE_BIN = os.path.join(ROOT, "tests", "cpp", "plan_cache_test")
+
+
+def test_plan_cache_is_bounded_and_safe_under_eviction():
+    """slime_amd/csrc/plan_cache.hpp over the product's host matrix code:
+    10,000 distinct 20/40 survivor sets keep the live plan count at the cap
+    and release every evicted table; held plans survive concurrent eviction."""
+    subprocess.run(["make", "-C", ROOT, "tests/cpp/plan_cache_test"], check=True, capture_output=True)
+    r = subprocess.run([CACHE_BIN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestPlanCacheBounded", "TestPlanCacheFailedBuild", "TestPlanCacheConcurrent"):
+        assert f"ok   {name}" in r.stdout

@@ -1,0 +1,199 @@
+"""Full-symbol parity at BASELINE sizes: every output symbol of the HIP path
+against the C oracle (oracle/rs_oracle.c, the reference's arithmetic), not a
+sample and not a round trip.
+
+  C3: need=8 total=12, 256 MiB objects -- encode (all parity rows,
+      internal/rs/vector.go:90-102 via CreateParity x r, multi_store.go:528-531)
+  C4: the same objects, data shards {0,1,2,3} erased, and the mixed set
+      {0,3,8,11} (RecoverData, vector.go:50-88, + CreateParity for parity rows)
+  C5: need=10 total=14, 1 GiB objects (L = 26843546, 4 padding symbols)
+and the fused byte path (writeChunks / reconstruct framing,
+multi_store.go:526-557 and :194-242) at C3 and C5, including objects mapped
+with 1<<31 (map.go:47-62).  The oracle runs threaded over column ranges
+(every output column is independent), so a 1 GiB object checks in seconds.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from slime_amd import rs
+from oracle import oracle_c as OC
+from oracle import oracle_py as OP
+
+pytestmark = pytest.mark.gpu
+
+P = 4294967291
+NTHREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch
+
+
+def _threads(n_cols: int, fn):
+    """fn(c0, c1) over NTHREADS contiguous column ranges, in parallel (ctypes drops the GIL)."""
+    step = -(-n_cols // NTHREADS)
+    ts = [threading.Thread(target=fn, args=(c0, min(n_cols, c0 + step))) for c0 in range(0, n_cols, step)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+
+
+def oracle_apply(mat, ins):
+    """out[i] = sum_j mat[i][j] * ins[j] mod p (oracle_apply_matrix, vector.go:90-102), threaded."""
+    mat = np.ascontiguousarray(mat, dtype=np.uint32)
+    rows, k = mat.shape
+    L = ins[0].size
+    assert all(x.flags.c_contiguous and x.size == L for x in ins)
+    outs = [np.empty(L, dtype=np.uint32) for _ in range(rows)]
+
+    def work(c0, c1):
+        ip = (ctypes.c_void_p * k)(*[x.ctypes.data + 4 * c0 for x in ins])
+        op = (ctypes.c_void_p * rows)(*[o.ctypes.data + 4 * c0 for o in outs])
+        OC.lib.oracle_apply_matrix(mat.ctypes.data, rows, k, ip, op, c1 - c0)
+
+    _threads(L, work)
+    return outs
+
+
+def oracle_recover(chunks, have):
+    """RecoverData(chunks, have) (oracle_recover_data, vector.go:50-88), threaded over columns."""
+    n = len(chunks)
+    L = chunks[0].size
+    outs = [np.empty(L, dtype=np.uint32) for _ in range(n)]
+    idx = (ctypes.c_int * n)(*have)
+    rcs = []
+
+    def work(c0, c1):
+        ip = (ctypes.c_void_p * n)(*[x.ctypes.data + 4 * c0 for x in chunks])
+        op = (ctypes.c_void_p * n)(*[o.ctypes.data + 4 * c0 for o in outs])
+        lens = (ctypes.c_uint64 * n)(*([c1 - c0] * n))
+        rcs.append(OC.lib.oracle_recover_data(ip, lens, idx, n, n, op))
+
+    _threads(L, work)
+    assert rcs and all(rc == 0 for rc in rcs)
+    return outs
+
+
+def _symbol_case(torch, need, total, mib, nobj, check_obj):
+    from slime_amd import device as D
+    L = -(-(-(-(mib << 20) // 4)) // need)
+    SS = -(-L // 64) * 64  # bench.py's device layout (256 B shard stride)
+    lay = D.layout_of(total, L, SS)
+    buf = torch.empty(nobj * total * SS, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, 0xF011 + need)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * SS)
+    torch.cuda.synchronize()
+    h = buf.view(nobj, total, SS)[check_obj, :, :L].cpu().numpy().view(np.uint32)
+    shards = [np.ascontiguousarray(h[s]) for s in range(total)]
+    del h
+    # encode: every parity symbol
+    pm = rs.ParityMatrix(need, total - need)[need:]
+    ref = oracle_apply(pm, shards[:need])
+    for i in range(total - need):
+        assert np.array_equal(shards[need + i], ref[i]), f"parity row {need + i}"
+    del ref
+    # decode: two erasure sets, rebuilt into a separate buffer
+    for erase in ([0, 1, 2, 3], [0, 3, need, total - 1]):
+        have = [i for i in range(total) if i not in erase][:need]
+        out = torch.empty(nobj * len(erase) * SS, dtype=torch.int32, device="cuda")
+        D.Plan.reconstruct(need, total, have, erase)(buf, lay, out, D.layout_of(len(erase), L, SS), L, nobj)
+        torch.cuda.synchronize()
+        got = out.view(nobj, len(erase), SS)[check_obj, :, :L].cpu().numpy().view(np.uint32)
+        del out
+        data = oracle_recover([shards[i] for i in have], have)  # all need data rows, as the reference computes
+        par = oracle_apply(pm, data)
+        for i, t in enumerate(erase):
+            want = data[t] if t < need else par[t - need]
+            assert np.array_equal(got[i], want), (erase, t)
+            assert np.array_equal(got[i], shards[t]), (erase, t)
+    del buf
+    torch.cuda.empty_cache()
+
+
+def test_c3_c4_every_symbol_vs_oracle(torch_dev):
+    """C3 encode + C4 decode of one whole 256 MiB object (object 1 of 2 in the batch)."""
+    _symbol_case(torch_dev, 8, 12, 256, 2, 1)
+
+
+def test_c5_every_symbol_vs_oracle(torch_dev):
+    """C5 (10/14, 1 GiB object, L = 26843546) encode + two decodes, every symbol."""
+    _symbol_case(torch_dev, 10, 14, 1024, 1, 0)
+
+
+# ------------------------------------------------------------ fused byte path
+
+def _oracle_chunks_threaded(obj: bytes, need: int, total: int, cands=()):
+    """writeChunks' framing (multi_store.go:526-554) via the oracle, parity threaded."""
+    rc, m, words = OC.map_to_gf(obj, list(cands))
+    assert rc == 0
+    parts = [np.ascontiguousarray(p) for p in OP.split_vector(words, need)]
+    parity = oracle_apply(rs.ParityMatrix(need, total - need)[need:], parts)
+    return m, [OC.map_from_gf(m, p) for p in parts + parity]
+
+
+def _bytes_case(torch, need, total, mib):
+    from slime_amd import device as D
+    S = mib << 20
+    L, chunk, slot = D.slot_geometry(S, need, total)
+    rng = np.random.default_rng(mib * 131 + need)
+    objs = [rng.integers(0, 256, size=S, dtype=np.uint8) for _ in range(2)]
+    # Object 1: a word >= p and no word that 1<<31 would map to >= p, so
+    # MapToGF picks 1<<31 (map.go:47-62).  Object 0 stays uniform random (at
+    # 1 GiB about a quarter of such objects need 1<<31 or the random fallback).
+    w = objs[1].view(">u4")
+    w[(w >= 0x7FFFFFFB) & (w <= 0x7FFFFFFF)] = 0x12345678
+    w[0] = 0xFFFFFFFF
+    host = np.zeros(2 * slot, dtype=np.uint8)
+    for o in range(2):
+        host[o * slot: o * slot + S] = objs[o]
+    slots = torch.from_numpy(host).cuda()
+    del host
+    enc = D.Plan.encode(need, total)
+    mapping = torch.empty(2, dtype=torch.int32, device="cuda")
+    status = torch.empty(2, dtype=torch.int32, device="cuda")
+    D.encode_objects(enc, slots, slot, S, 2, mapping, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().tolist()
+    assert st[1] == 0
+    if st[0]:  # MapToGF's random fallback (map.go:64-66): resolved on the device
+        assert D.resolve_fallbacks(enc, slots, slot, S, 2, mapping, status) == 1
+    ms = mapping.cpu().numpy().view(np.uint32).tolist()
+    for o in range(2):
+        cands = [ms[o]] if ms[o] not in (0, 1 << 31) else []
+        m, want = _oracle_chunks_threaded(objs[o].tobytes(), need, total, cands)
+        assert ms[o] == m, o
+        got = slots[o * slot: (o + 1) * slot].cpu().numpy()
+        for c in range(total):
+            assert got[c * chunk:(c + 1) * chunk].tobytes() == want[c], (o, c)
+        if o == 1:
+            assert m == 1 << 31
+        truth = want
+    # repair (C4 erasures) of both objects; compare the rebuilt chunk bytes of object 1
+    for erase in ([0, 1, 2, 3], [0, 3, need, total - 1]):
+        have = [i for i in range(total) if i not in erase][:need]
+        rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+        v = slots.view(2, slot)[:, : total * chunk].view(2, total, chunk)
+        v[:, erase, :] = 0x5A
+        D.decode_objects(rec, slots, slot, L, 2, mapping)
+        torch.cuda.synchronize()
+        got = slots[slot: 2 * slot].cpu().numpy()
+        for c in erase:
+            assert got[c * chunk:(c + 1) * chunk].tobytes() == truth[c], (erase, c)
+    del slots
+    torch.cuda.empty_cache()
+
+
+def test_c3_bytes_every_byte_vs_oracle(torch_dev):
+    _bytes_case(torch_dev, 8, 12, 256)
+
+
+def test_c5_bytes_every_byte_vs_oracle(torch_dev):
+    _bytes_case(torch_dev, 10, 14, 1024)

@@ -7,6 +7,7 @@ KATs, and size-independent properties at full BASELINE sizes (encode -> erase
 empty and ragged vectors, non-canonical symbols (x >= p, 0xFFFFFFFF), every
 erasure pattern at 4/6, unaligned layouts, k > 16 (generic kernel).
 """
+import ctypes
 import itertools
 import random
 
@@ -783,3 +784,103 @@ def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
             outs[(pipe, off)] = h.copy()
     for off in (0, 1):
         assert np.array_equal(outs[("0", off)], outs[("1", off)])
+
+
+# ------------------------------------------------- round-2 boundary behaviour
+
+@pytest.mark.parametrize("need", [1, 3, 8])
+@pytest.mark.parametrize("S", [1, 5, 4096, 100003])
+@pytest.mark.parametrize("kind", ["plain", "high", "fallback"])
+def test_write_chunks_without_parity_vs_oracle(need, S, kind):
+    """need == total (checkConfig, multi_config.go:36; 1-of-1 in multi_test.go:179):
+    chunks are the reference's MapFromGF(m, splitVector parts) and the object
+    reconstructs from them."""
+    from slime_amd import objects
+    rng = np.random.default_rng(S * 7 + need)
+    obj = _obj_bytes(rng, S, kind)
+    m, chunks = objects.write_chunks(obj, need, need)
+    m_ref, want = _oracle_chunks(obj, need, need, [m] if kind == "fallback" and S >= 8 else [])
+    assert m == m_ref
+    assert [c.tobytes() for c in chunks] == want
+    assert objects.reconstruct(chunks, list(range(need)), m, S).tobytes() == obj
+
+
+@pytest.mark.parametrize("cut", [1, 2, 3])
+def test_reconstruct_partial_word_chunks_vs_oracle(cut):
+    """Survivors whose length is not a multiple of 4 (truncated stored chunks):
+    MapToGFWith zero-pads the partial word (map.go:16-33) and every recovered
+    row is that long (vector.go:80-85), as the reference computes."""
+    from slime_amd import objects
+    rng = np.random.default_rng(cut)
+    need, total, S = 4, 6, 40000
+    obj = _obj_bytes(rng, S, "high")
+    m, chunks = objects.write_chunks(obj, need, total)
+    have = [1, 2, 4, 5]
+    surv = [chunks[i][:-cut].tobytes() for i in have]
+    for size in (S, S + 100):
+        got = objects.reconstruct(surv, have, m, size).tobytes()
+        assert got == _oracle_reconstruct(surv, have, m, need, size)
+
+
+def test_plan_cache_stays_bounded_on_device():
+    """RecoverData over many distinct survivor sets (20/40): the host plan cache
+    stays at its capacity and evicted plans free their device tables
+    (vector.go:69-77 inverts per survivor set)."""
+    import itertools as it
+    rng = np.random.default_rng(2040)
+    N.set_plan_cache_capacity(8)
+    try:
+        need, total, L = 20, 40, 37
+        data = rand_vecs(rng, need, L, canonical=True, edges=False)
+        code = data + [OC.create_parity(data, need + i)[1] for i in range(total - need)]
+        base = N.plan_cache_stats()
+        seen = 0
+        for have in it.islice(it.combinations(range(total), need), 0, 100000, 997):
+            got = rs.RecoverData([code[i] for i in have], list(have))
+            assert all(np.array_equal(g, d) for g, d in zip(got, data))
+            seen += 1
+        st = N.plan_cache_stats()
+        assert seen >= 60
+        assert st["live"] <= 8 and st["capacity"] == 8
+        assert st["evictions"] - base["evictions"] >= seen - 8
+        assert st["device_tables"] <= base["device_tables"] + 8
+    finally:
+        N.set_plan_cache_capacity(256)
+
+
+def test_set_outputs_refused_after_launch(torch_dev):
+    """A plan's output table is fixed once it has launched (launches in flight read it)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, L = 4, 6, 1024
+    buf = _objects(torch, 1, total, L, seed=3)
+    lay = D.layout_of(total, L)
+    rec = D.Plan.reconstruct(need, total, [2, 3, 4, 5], [0, 1]).set_outputs([0, 1])  # before: fine
+    rec(buf, lay, buf, lay, L, 1)
+    torch.cuda.synchronize()
+    with pytest.raises(slime_amd.NativeError) as e:
+        rec.set_outputs([1, 0])
+    assert e.value.code == N.ERR_INVALID_ARG
+
+
+def test_device_pool_routes_unpinned_calls():
+    """Host calls that name no device go through the device pool; on a 1-GPU box
+    every call lands on device 0 (8-GPU behaviour: DESIGN.md, unmeasured)."""
+    n = N.device_count()
+    before = [N.pool_calls(d)[0] for d in range(n)]
+    for _ in range(6):
+        assert rs.CreateParity([[0, 0, 0], [1, 2, 3]], 2).tolist() == [3, 6, 9]
+    after = [N.pool_calls(d) for d in range(n)]
+    assert sum(a[0] - b for a, b in zip(after, before)) == 6
+    assert all(a[1] == 0 for a in after)
+    if n == 1:
+        assert after[0][0] - before[0] == 6
+    # a pinned call bypasses the pool's choice but still counts on its device
+    buf = ctypes.create_string_buffer(128)
+    call = N.Call(0, ctypes.cast(buf, ctypes.c_char_p), 128)
+    x = np.array([1, 2, 3], dtype=np.uint32)
+    out = np.zeros(3, dtype=np.uint32)
+    ptrs = (ctypes.c_void_p * 2)(x.ctypes.data, x.ctypes.data)
+    lens = (ctypes.c_uint64 * 2)(3, 3)
+    assert N.lib.slime_rs_create_parity_ex(ctypes.byref(call), ptrs, lens, 2, 2, out.ctypes.data) == 0
+    assert buf.value == b"" and out.tolist() == OC.create_parity([x, x], 2)[1].tolist()

@@ -158,10 +158,57 @@ def test_object_entry_points_validate_like_reference():
     with pytest.raises(slime_amd.Panic) as e:  # duplicate survivors -> singular
         objects.reconstruct([b"\0" * 8, b"\0" * 8], [1, 1], 0, 16)
     assert "Couldn't ensure" in str(e.value)
-    with pytest.raises(slime_amd.NativeError):
-        objects.write_chunks(b"abc", 4, 4)  # total must exceed need
+    with pytest.raises(slime_amd.NativeError) as e:
+        objects.write_chunks(b"abc", 4, 3)  # total < need: a caller error
+    assert e.value.code == N.ERR_INVALID_ARG
+    # need == total is a valid config (multi_config.go:36; multi_test.go:179 runs 1-of-1)
+    if not HAS_GPU:
+        with pytest.raises(slime_amd.NativeError) as e:
+            objects.write_chunks(b"abc", 4, 4)
+        assert e.value.code == N.ERR_NO_DEVICE
     m, chunks = objects.write_chunks(b"", 4, 6)
     assert m == 0 and all(c.size == 0 for c in chunks)
+    m, chunks = objects.write_chunks(b"", 3, 3)
+    assert m == 0 and all(c.size == 0 for c in chunks)
+
+
+def test_reconstruct_pads_size_past_the_chunks_with_zeros():
+    """data[:f.Size] of make([]byte, 0, Size+16) (multi_store.go:203,241) never
+    panics: bytes past the recovered rows are the zeroed capacity.  Zero-length
+    chunks reach that before any device work."""
+    out = np.full(10, 0xAB, dtype=np.uint8)
+    got = objects.reconstruct([b"", b""], [0, 1], 0, 10, out=out)
+    assert got.tolist() == [0] * 10
+
+
+def test_ex_entry_points_return_this_calls_detail():
+    """The *_ex forms (what the cgo shim binds) hand back the failure detail
+    of the call itself, in the caller's buffer, from any thread."""
+    import threading
+    bad = []
+
+    def create_parity(index):
+        buf = ctypes.create_string_buffer(256)
+        call = N.Call(N.ANY_DEVICE, ctypes.cast(buf, ctypes.c_char_p), 256)
+        x = np.array([1, 2], dtype=np.uint32)
+        ptrs = (ctypes.c_void_p * 2)(x.ctypes.data, x.ctypes.data)
+        lens = (ctypes.c_uint64 * 2)(2, 2)
+        rc = N.lib.slime_rs_create_parity_ex(ctypes.byref(call), ptrs, lens, 2, index, None)
+        return rc, buf.value.decode()
+
+    def worker(base):
+        for i in range(300):
+            index = -(base + i % 5)
+            rc, detail = create_parity(index)
+            if rc != N.ERR_INDEX_RANGE or detail != f"runtime error: index out of range [{index}]":
+                bad.append((index, rc, detail))
+
+    ts = [threading.Thread(target=worker, args=(b,)) for b in (1, 10, 100, 1000)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not bad, bad[:3]
 
 
 def test_status_strings_are_reference_panics():
@@ -239,16 +286,36 @@ def _call_args(src, start):
     raise AssertionError("unbalanced call")
 
 
+# Entry points whose result or detail depends on the call: the shim must
+# bind their *_ex forms (device and detail travel with the call).
+EX_BOUND = ["slime_rs_create_parity", "slime_rs_create_parities", "slime_rs_recover_data", "slime_rs_write_chunks",
+            "slime_rs_reconstruct", "slime_gf_map_to_gf", "slime_gf_map_to_gf_with", "slime_gf_map_from_gf",
+            "slime_rs_parity_matrix", "slime_rs_vandermonde_matrix", "slime_rs_solve_sub_identity",
+            "slime_rs_invert_matrix"]
+
+
 def test_go_shim_keeps_the_reference_api_and_binds_the_header():
     """The cgo shim (compile-unverified: no Go toolchain here) declares the
     reference's Go API verbatim and calls only C entry points the header
-    declares, each with the header's argument count."""
+    declares, each with the header's argument count.  It reads no
+    thread-local state across cgo calls: no slime_rs_last_error or
+    slime_rs_select_device (a goroutine may change OS threads between calls),
+    only the *_ex forms, whose detail comes back from the same call."""
     arity = _header_arity()
     for path, decls in GO_API.items():
         src = open(os.path.join(ROOT, path)).read()
         for d in decls:
             assert d in src, (path, d)
+        called = set()
         for m in re.finditer(r"\bC\.(slime_\w+)\(", src):
             name = m.group(1)
+            called.add(name)
             assert name in arity, (path, name)
             assert _call_args(src, m.end() - 1) == arity[name], (path, name)
+        assert "slime_rs_last_error" not in src, path
+        assert "slime_rs_select_device" not in src, path
+        for name in EX_BOUND:
+            assert name not in called, (path, f"{name}: bind {name}_ex")
+    shim = "".join(open(os.path.join(ROOT, p)).read() for p in GO_API)
+    for name in EX_BOUND:
+        assert f"C.{name}_ex(" in shim, name

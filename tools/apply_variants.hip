@@ -23,7 +23,251 @@ void gp(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo
   hipLaunchKernelGGL((rs_apply_pipe_kernel<K, U, NTL, NTS, MODE>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os,
                      coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, nseg);
 }
+// ---- time-phased walk (read/write turnaround experiment, round 2) ----------
+// Every wave of the chip reads only inside the first `rwin` ticks of each
+// `period` ticks of the 100 MHz s_memrealtime clock and writes only after
+// them, so the DRAM sees chip-wide read bursts and write bursts instead of a
+// 2:1 mix at every instant.  Per period a wave loads T tiles of U KiB per
+// shard (T register sets), computes all R output rows into registers, waits
+// for the write window and stores them.  R = 4 rows (C3 encode / C4 decode).
+__device__ __forceinline__ void wait_phase(uint32_t period, uint32_t lo, uint32_t hi) {
+  for (;;) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime() % period;
+    if (t >= lo && t < hi) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+template <int K, int U, int R>
+__global__ __launch_bounds__(kBlock) void phased_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                        uint64_t in_obj_stride, uint64_t in_shard,
+                                                        uint64_t out_obj_stride, uint64_t out_shard,
+                                                        const uint32_t* __restrict__ coeff,
+                                                        const uint32_t* __restrict__ in_idx,
+                                                        const uint32_t* __restrict__ out_idx, uint64_t ncols,
+                                                        uint32_t nobj, uint32_t nseg, uint32_t period, uint32_t rwin) {
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = ib + (uint64_t)in_idx[j] * in_shard;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    for (uint32_t step = wave; step < ntiles; step += nwaves) {
+      const uint32_t g0 = v0 + step * (64 * U) + lane;
+      uint4 x[U][K];
+      wait_phase(period, 0, rwin);
+      load_tile<K, U, true>(x, sb, g0, v1);
+      uint4 y[R][U];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[i][u] = dot4<K>(x[u], c);
+      }
+      wait_phase(period, rwin, period);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (g0 + 64 * u < v1) st16<true>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), y[i][u]);
+      }
+    }
+  }
+}
+// ---- LDS-staged write bursts (round 2) --------------------------------------
+// The product's software pipeline, but a wave parks each tile's R x U output
+// vectors in LDS and stores T tiles' worth as one burst every T tiles, so the
+// wave's store stream reaches the memory system in runs of T x R x U KiB.
+template <int K, int U, int R, int T>
+__global__ __launch_bounds__(kBlock) void burst_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       uint64_t in_obj_stride, uint64_t in_shard,
+                                                       uint64_t out_obj_stride, uint64_t out_shard,
+                                                       const uint32_t* __restrict__ coeff,
+                                                       const uint32_t* __restrict__ in_idx,
+                                                       const uint32_t* __restrict__ out_idx, uint64_t ncols,
+                                                       uint32_t nobj, uint32_t nseg) {
+  __shared__ uint4 stage[kWaves][T][R][U][64];
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * kWaves + wv;
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = ib + (uint64_t)in_idx[j] * in_shard;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    uint4 xa[U][K];
+    uint32_t step = wave, slot = 0, first = wave;
+    auto flush = [&](uint32_t nslots) {
+      for (uint32_t t = 0; t < nslots; ++t) {
+        const uint32_t g0 = v0 + (first + t * nwaves) * (64 * U) + lane;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (g0 + 64 * u < v1) st16<true>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), stage[wv][t][i][u][lane]);
+        }
+      }
+    };
+    if (step < ntiles) load_tile<K, U, true>(xa, sb, v0 + step * (64 * U) + lane, v1);
+    while (step < ntiles) {
+      const uint32_t next = step + nwaves;
+      uint4 xb[U][K];
+      load_tile<K, U, true>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) stage[wv][slot][i][u][lane] = dot4<K>(xa[u], c);
+      }
+      if (++slot == T || next >= ntiles) {
+        flush(slot);
+        slot = 0;
+        first = next;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < K; ++j) xa[u][j] = xb[u][j];
+      step = next;
+    }
+  }
+}
+// The product's software pipeline with every output row of a tile computed
+// into registers first and the tile's R x U stores issued back to back
+// (the product interleaves each row's stores with the next row's math).
+template <int K, int U, int R>
+__global__ __launch_bounds__(kBlock) void batched_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                         uint64_t in_obj_stride, uint64_t in_shard,
+                                                         uint64_t out_obj_stride, uint64_t out_shard,
+                                                         const uint32_t* __restrict__ coeff,
+                                                         const uint32_t* __restrict__ in_idx,
+                                                         const uint32_t* __restrict__ out_idx, uint64_t ncols,
+                                                         uint32_t nobj, uint32_t nseg) {
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = ib + (uint64_t)in_idx[j] * in_shard;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    auto tile = [&](const uint4(&x)[U][K], uint32_t g0) {
+      uint4 y[R][U];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[i][u] = dot4<K>(x[u], c);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (g0 + 64 * u < v1) st16<true>(reinterpret_cast<uint32_t*>(orow + ((g0 + 64 * u) << 4)), y[i][u]);
+      }
+    };
+    uint4 xa[U][K], xb[U][K];
+    uint32_t step = wave;
+    if (step < ntiles) load_tile<K, U, true>(xa, sb, v0 + step * (64 * U) + lane, v1);
+    while (step < ntiles) {
+      uint32_t next = step + nwaves;
+      load_tile<K, U, true>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      tile(xa, v0 + step * (64 * U) + lane);
+      step = next;
+      if (step >= ntiles) break;
+      next = step + nwaves;
+      load_tile<K, U, true>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      tile(xb, v0 + step * (64 * U) + lane);
+      step = next;
+    }
+  }
+}
 }  // namespace
+
+extern "C" int av_launch_batched(int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
+                                 uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                                 uint64_t ncols, uint32_t nobj, uint32_t gx, uint32_t gy, void* stream,
+                                 uint32_t nseg) {
+  hipStream_t s = (hipStream_t)stream;
+  if (U == 2)
+    hipLaunchKernelGGL((batched_kernel<8, 2, 4>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg);
+  else if (U == 3)
+    hipLaunchKernelGGL((batched_kernel<8, 3, 4>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int av_launch_burst(int T, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
+                               uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                               uint64_t ncols, uint32_t nobj, uint32_t gx, uint32_t gy, void* stream, uint32_t nseg) {
+  hipStream_t s = (hipStream_t)stream;
+  if (T == 1)
+    hipLaunchKernelGGL((burst_kernel<8, 3, 4, 1>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg);
+  else if (T == 2)
+    hipLaunchKernelGGL((burst_kernel<8, 3, 4, 2>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg);
+  else if (T == 3)
+    hipLaunchKernelGGL((burst_kernel<8, 3, 4, 3>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Phased walk launch (k = 8, 4 rows): U in {3, 6}.
+extern "C" int av_launch_phased(int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
+                                uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                                uint64_t ncols, uint32_t nobj, uint32_t gx, uint32_t gy, void* stream, uint32_t nseg,
+                                uint32_t period, uint32_t rwin) {
+  hipStream_t s = (hipStream_t)stream;
+  if (period == 0 || rwin == 0 || rwin >= period) return -4;
+  if (U == 3)
+    hipLaunchKernelGGL((phased_kernel<8, 3, 4>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg, period, rwin);
+  else if (U == 6)
+    hipLaunchKernelGGL((phased_kernel<8, 6, 4>), dim3(gx, gy), dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii,
+                       oi, ncols, nobj, nseg, period, rwin);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 extern "C" int av_launch(int variant, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is,
                          uint64_t oo, uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,

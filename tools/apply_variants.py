@@ -26,6 +26,9 @@ import torch  # noqa: E402
 
 from slime_amd import device as D  # noqa: E402
 
+BATCHED: dict = {}  # variant id -> U
+BURST: dict = {}  # variant id -> tiles per store burst
+PHASED: dict = {}  # variant id -> (U, period ticks, read-window ticks)
 ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain",
                 6: "U2 ntL ntS", 7: "U2 ntS", 8: "U4 ntL ntS", 9: "U4 ntL", 10: "U3 ntL ntS",
                 11: "U4 ntL ntS rot", 12: "U2 ntL ntS rot",
@@ -49,11 +52,39 @@ def main():
     ap.add_argument("--pad", type=str, default="0", help="shard stride = L + pad symbols (comma list)")
     ap.add_argument("--hunt", choices=["any", "slow", "fast"], default="any",
                     help="re-allocate until the product encode runs in the given placement mode")
+    ap.add_argument("--phased", type=str, default="",
+                    help="time-phased walks U:period:rwin (100 MHz ticks), comma list, e.g. 3:700:460,6:1400:930")
+    ap.add_argument("--batched", type=str, default="", help="register-batched stores: U list (2,3)")
+    ap.add_argument("--burst", type=str, default="", help="LDS-staged write bursts: tiles per burst, comma list (1..3)")
     ap.add_argument("--separate", type=int, default=-1,
                     help="1: write to a separate buffer, 0: in place (default: encode in place, decode separate)")
     args = ap.parse_args()
-    VARIANTS = {int(v): ALL_VARIANTS[int(v)] for v in args.variants.split(",")}
+    VARIANTS = {int(v): ALL_VARIANTS[int(v)] for v in args.variants.split(",") if v}
+    PHASED.clear()
+    for i, spec in enumerate(x for x in args.phased.split(",") if x):
+        u, per, rw = (int(t) for t in spec.split(":"))
+        assert rw >= 50 and per - rw >= 50, "phase windows must be >= 50 ticks"
+        PHASED[100 + i] = (u, per, rw)
+        VARIANTS[100 + i] = f"phased U{u} period {per} read {rw} ticks"
+    for t in (int(x) for x in args.burst.split(",") if x):
+        BURST[200 + t] = t
+        VARIANTS[200 + t] = f"pipe U3 + LDS-staged store bursts of {t} tiles"
+    for u in (int(x) for x in args.batched.split(",") if x):
+        BATCHED[300 + u] = u
+        VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
+    lib.av_launch_batched.restype = ctypes.c_int
+    lib.av_launch_batched.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_void_p, ctypes.c_uint32]
+    lib.av_launch_burst.restype = ctypes.c_int
+    lib.av_launch_burst.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_void_p, ctypes.c_uint32]
+    lib.av_launch_phased.restype = ctypes.c_int
+    lib.av_launch_phased.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     lib.av_launch.restype = ctypes.c_int
     lib.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -132,6 +163,27 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
     def launch(v, gx, gy, nseg=1):
+        if v in BATCHED:
+            assert r == 4 and need == 8, "batched walk is built for 8/12 (4 rows)"
+            rc = lib.av_launch_batched(BATCHED[v], buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
+                                       ii.data_ptr(), oi.data_ptr(), L, nobj, gx, gy, ctypes.c_void_p(s.cuda_stream),
+                                       nseg)
+            assert rc == 0, rc
+            return
+        if v in BURST:
+            assert r == 4 and need == 8, "burst walk is built for 8/12 (4 rows)"
+            rc = lib.av_launch_burst(BURST[v], buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
+                                     ii.data_ptr(), oi.data_ptr(), L, nobj, gx, gy, ctypes.c_void_p(s.cuda_stream),
+                                     nseg)
+            assert rc == 0, rc
+            return
+        if v in PHASED:
+            assert r == 4 and need == 8, "phased walk is built for 8/12 (4 rows)"
+            u, per, rw = PHASED[v]
+            rc = lib.av_launch_phased(u, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(), ii.data_ptr(),
+                                      oi.data_ptr(), L, nobj, gx, gy, ctypes.c_void_p(s.cuda_stream), nseg, per, rw)
+            assert rc == 0, rc
+            return
         rc = lib.av_launch(v, need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                            ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream), nseg)
         assert rc == 0, rc

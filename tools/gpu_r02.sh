@@ -1,0 +1,57 @@
+#!/usr/bin/env bash
+# Round-2 GPU-box session: every GPU step under its own time limit; the first
+# crash/abort/timeout ends the session (nothing more runs on the GPU).
+# Usage (repo root, on the box):  bash tools/gpu_r02.sh <step> [<step>...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # run <name> <limit-seconds> <command...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then
+    echo "!!! $name ended with rc=$rc: stopping the session" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+}
+
+nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+for step in "$@"; do
+  case "$step" in
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    bench_nocpu) run bench_nocpu 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
+            python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    pmc_fetch) run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    pmc_write) run pmc_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    phased_enc) run phased_enc 400 python tools/apply_variants.py --variants 15 --blocks 256 --rounds 3 \
+            --phased 3:700:460,3:800:530,3:900:600,6:1300:860,6:1500:1000 ;;
+    phased_dec) run phased_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 \
+            --rounds 3 --phased 3:800:530,6:1400:930 ;;
+    phased_slow) run phased_slow 600 python tools/apply_variants.py --hunt slow --variants 15,18,19 --blocks 256 \
+            --rounds 3 --phased 3:700:460,3:800:530,3:900:600,6:1300:860,6:1500:1000 ;;
+    burst) run burst 400 python tools/apply_variants.py --variants 15 --blocks 256 --rounds 3 --burst 1,2,3 ;;
+    burst_dec) run burst_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 \
+            --rounds 3 --burst 1,2,3 ;;
+    burst_slow) run burst_slow 600 python tools/apply_variants.py --hunt slow --variants 15 --blocks 256 --rounds 3 \
+            --burst 1,2,3 ;;
+    stage) run stage 400 python tools/apply_variants.py --variants 14,15 --blocks 256,512 --rounds 3 --burst 1 --batched 2,3 ;;
+    stage_dec) run stage_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 14,15 --blocks 256,512 \
+            --rounds 3 --burst 1 --batched 2,3 ;;
+    stage_fast) run stage_fast 600 python tools/apply_variants.py --hunt fast --variants 15 --blocks 256,512 --rounds 3 \
+            --burst 1 --batched 2,3 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session done" | tee -a "$OUT/session.log"

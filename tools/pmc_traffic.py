@@ -5,12 +5,27 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): counters are in KiB; FETCH_SIZE
 reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
 so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r02/pmc_traffic.json
+
+`kernel_source` (hash of the apply kernel sources, as bench.py's
+kernel_source_id) ties the summary to the build it was measured on: bench.py
+replays `hbm_bytes_per_launch` only into lines of the same kernel source.
 """
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_source_id() -> str:
+    h = hashlib.sha256()
+    for f in ("rs_apply_kernel.hpp", "rs_apply.hip", "gfp.hpp"):
+        h.update(open(os.path.join(ROOT, "slime_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 KERNELS = ("rs_apply_pipe_kernel", "rs_apply_kernel")  # product apply kernels (rs_apply.hip)
@@ -29,6 +44,7 @@ def per_dispatch(d, counter):
 
 def main():
     fetch_dir, write_dir, config = sys.argv[1:4]
+    session = sys.argv[4] if len(sys.argv) > 4 else "?"
     f, fk = per_dispatch(fetch_dir, "FETCH_SIZE")
     w, wk = per_dispatch(write_dir, "WRITE_SIZE")
     assert len(fk | wk) == 1, f"expected one apply kernel, saw {fk | wk}"
@@ -38,6 +54,8 @@ def main():
     write_bytes = write_kib * 1024
     print(json.dumps({
         "config": config,
+        "session": session,
+        "kernel_source": kernel_source_id(),
         "kernel": (fk | wk).pop(),
         "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
         "fetch_size_kib_avg": fetch_kib,
