@@ -439,8 +439,8 @@ def main():
     launch_ms = (enc_ms + dec_ms) / 2
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
     # The product dispatch (rs_apply.hip): the pipelined kernel for shards
-    # under 4 GiB, unless SLIME_RS_PIPE=0.
-    kname = "rs_apply_pipe_kernel" if L < (1 << 30) and os.environ.get("SLIME_RS_PIPE", "1") != "0" \
+    # under 4 GiB, unless the kernel form was switched (slime_rs_kernel_pipeline).
+    kname = "rs_apply_pipe_kernel" if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1 \
         else "rs_apply_kernel"
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such

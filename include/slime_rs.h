@@ -93,6 +93,11 @@ typedef struct slime_rs_call {
  * SLIME_RS_ERR_INVALID_ARG for an unknown mode.  No reference counterpart:
  * the Go implementation computes in place on host memory. */
 int slime_rs_host_pipeline(int mode);
+/* Kernel form for shards/chunks under 4 GiB (process-wide; env SLIME_RS_PIPE=0
+ * sets the initial value): 1 = software-pipelined kernels (default), 0 = the
+ * non-pipelined forms that larger shards always take.  mode < 0 queries.
+ * Results are identical; the parity tests run both. */
+int slime_rs_kernel_pipeline(int mode);
 
 /* ==== internal/rs/gf ===================================================== */
 

@@ -34,6 +34,11 @@ inline uint32_t coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 
+// Kernel form for shards/chunks under 4 GiB: software-pipelined (default) or
+// not (the form larger ones always take).  Process-wide; see rs_apply.hip.
+bool pipelined_kernels();
+void set_pipelined_kernels(bool on);
+
 // Column segments per object for a launch over nobj objects of ncols
 // columns (the apply and byte kernels cut each object into this many
 // contiguous segments scheduled like separate objects).

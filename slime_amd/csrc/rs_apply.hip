@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "kernels.hpp"
 #include "rs_apply_kernel.hpp"
 
@@ -137,14 +139,25 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+}  // namespace
+
+// Kernel form (process-wide): the software-pipelined kernels (default) or
+// the non-pipelined forms that shards/chunks of 4 GiB and more always take.
+// Env SLIME_RS_PIPE=0 sets the initial value (read once, not per launch);
+// slime_rs_kernel_pipeline() switches it (the parity tests cover both forms
+// in one process).
+static std::atomic<int> g_pipelined{[] {
+  const char* e = getenv("SLIME_RS_PIPE");
+  return e && e[0] == '0' ? 0 : 1;
+}()};
+bool pipelined_kernels() { return g_pipelined.load(std::memory_order_relaxed) != 0; }
+void set_pipelined_kernels(bool on) { g_pipelined.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+namespace {
 // The pipelined kernel addresses a shard with 32-bit byte offsets: it needs
 // ncols * 4 < 2^32 (shards under 4 GiB -- objects under 4 GiB x need).
-// Larger shards, and SLIME_RS_PIPE=0 (tuning; read per launch so the parity
-// tests can cover the fallback kernel in-process), take rs_apply_kernel.
-bool pipe_ok(const ApplyLaunch& a) {
-  const char* e = getenv("SLIME_RS_PIPE");
-  return !(e && e[0] == '0') && a.ncols < (1ull << 30);
-}
+// Larger shards take rs_apply_kernel.
+bool pipe_ok(const ApplyLaunch& a) { return pipelined_kernels() && a.ncols < (1ull << 30); }
 
 template <int K>
 hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {

@@ -31,8 +31,9 @@ dim3 grid_for(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t target = 51
 }
 
 // Software-pipelined forms (rs_bytes_kernel.hpp), the product for need <= 16
-// when a chunk is under 4 GiB (32-bit offsets) unless SLIME_RS_PIPE=0 (read
-// per launch, as in rs_apply.hip).  Geometry as the pipelined apply kernel.
+// when a chunk is under 4 GiB (32-bit offsets) and the kernel form is
+// pipelined (slime_rs_kernel_pipeline, rs_apply.hip).  Geometry as the
+// pipelined apply kernel.
 template <int K>
 constexpr int pipe_unroll() {
   return K == 1 ? 4 : K == 2 ? 2 : K <= 4 ? 1 : K <= 12 ? 3 : 1;
@@ -41,10 +42,7 @@ template <int K>
 constexpr uint64_t pipe_blocks() {
   return K <= 12 ? 256 : 1024;
 }
-bool pipe_ok(const BytesLaunch& a) {
-  const char* e = getenv("SLIME_RS_PIPE");
-  return !(e && e[0] == '0') && a.L < (1ull << 30);
-}
+bool pipe_ok(const BytesLaunch& a) { return pipelined_kernels() && a.L < (1ull << 30); }
 
 // The encode keeps its flags and the edge-tile path live beside the two
 // register sets: U = 2 up to need 8, 1 above (no spills to scratch).

@@ -742,6 +742,13 @@ int slime_rs_host_pipeline(int mode) {
   return 0;
 }
 
+int slime_rs_kernel_pipeline(int mode) {
+  if (mode < 0) return pipelined_kernels() ? 1 : 0;
+  if (mode > 1) return fail(Status::InvalidArg, "kernel_pipeline: mode must be 0 or 1");
+  set_pipelined_kernels(mode == 1);
+  return 0;
+}
+
 int slime_rs_select_device(int device) {
   if (device != SLIME_RS_ANY_DEVICE)
     if (int rc = check_device(device)) return rc;

@@ -523,11 +523,13 @@ def _make_slots(torch, objs, need, total, extra=0):
 
 
 @pytest.fixture(params=["1", "0"], ids=["pipelined", "fallback"])
-def kernel_form(request, monkeypatch):
+def kernel_form(request):
     """Byte kernels: the pipelined product form and the non-pipelined form
-    (chunks >= 4 GiB), selected per launch by SLIME_RS_PIPE."""
-    monkeypatch.setenv("SLIME_RS_PIPE", request.param)
-    return request.param
+    (chunks >= 4 GiB), selected process-wide by slime_rs_kernel_pipeline."""
+    before = N.lib.slime_rs_kernel_pipeline(-1)
+    assert N.lib.slime_rs_kernel_pipeline(int(request.param)) == 0
+    yield request.param
+    N.lib.slime_rs_kernel_pipeline(before)
 
 
 @pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20), (17, 20), (33, 50)])
@@ -751,7 +753,7 @@ def test_fuzz_random_shapes_and_layouts(torch_dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20), (20, 24), (17, 30), (40, 56)])
-def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
+def test_fallback_kernel_vs_oracle(torch_dev, need, total):
     """The non-pipelined apply kernel (shards >= 4 GiB; SLIME_RS_PIPE=0) at
     small sizes: encode in place, misaligned bases, reconstruct into a
     separate buffer -- and the pipelined product form on the same inputs."""
@@ -764,8 +766,9 @@ def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
     have = [i for i in range(total) if i not in erase][:need]
     rec = D.Plan.reconstruct(need, total, have, erase)
     outs = {}
+    before = N.lib.slime_rs_kernel_pipeline(-1)
     for pipe in ("0", "1"):
-        monkeypatch.setenv("SLIME_RS_PIPE", pipe)
+        N.lib.slime_rs_kernel_pipeline(int(pipe))
         for off in (0, 1):
             buf = torch.empty(off + nobj * total * L, dtype=torch.int32, device="cuda")
             D.fill_symbols(buf, seed=need * 31 + off)
@@ -782,6 +785,7 @@ def test_fallback_kernel_vs_oracle(torch_dev, need, total, monkeypatch):
                 for i, t in enumerate(erase):
                     assert np.array_equal(got[o, i], h[o, t]), (pipe, off, o, t)
             outs[(pipe, off)] = h.copy()
+    N.lib.slime_rs_kernel_pipeline(before)
     for off in (0, 1):
         assert np.array_equal(outs[("0", off)], outs[("1", off)])
 
