@@ -1434,6 +1434,35 @@ static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease, D
   return (*wsp)->reserve(bytes_needed);
 }
 
+// The codec's host entry points stream through the same pinned 3-stage ring
+// as the object entry points (run_windows): the caller's buffers stay
+// pageable, each window's H2D / kernel / D2H overlaps the host copies of the
+// others, and fresh (never touched) output pages are faulted in by the
+// ring's host copy instead of by a DMA (the direct pageable copy of round 1
+// fell to 0.5 GiB/s into fresh pages, DESIGN.md "End-to-end").
+constexpr uint64_t kCodecWindowBytes = 8u << 20;  // input bytes per window (+ as many out)
+
+// Bytes -> words windows of MapToGF(With): window c packs input bytes
+// [c*W, c*W + W) into words [c*W/4, ...) on the device (mapping n, flags
+// OR-reduced if given) and streams the words back to `out`.
+static int pack_windows(Workspace* ws, const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out,
+                        uint8_t* d_bytes, uint32_t* d_words, uint32_t* d_flags) {
+  const uint64_t W = kCodecWindowBytes, nwin = (len + W - 1) / W;
+  uint8_t* const base = ws->dbuf;
+  return run_windows(
+      "codec_pack", ws, base, nwin, 2 * W,
+      [&](uint64_t c, int, Window& w) {
+        const uint64_t b0 = c * W, nb = std::min(W, len - b0);
+        w.in.push_back({const_cast<uint8_t*>(in) + b0, (uint64_t)(d_bytes - base) + b0, nb});
+        w.out.push_back({(uint8_t*)out + b0, (uint64_t)((uint8_t*)d_words - base) + b0, 4 * ((nb + 3) / 4)});
+      },
+      [&](uint64_t c, int, hipStream_t st) -> int {
+        const uint64_t b0 = c * W, nb = std::min(W, len - b0);
+        HIP_TRY(launch_map_pack(d_bytes + b0, nb, n, d_words + b0 / 4, d_flags, st));
+        return 0;
+      });
+}
+
 int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out) {
   const uint64_t nw = (len + 3) / 4;
   if (nw == 0) return 0;
@@ -1444,29 +1473,23 @@ int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_
   DeviceLease dl;
   if (int rc = codec_setup(bbytes + round16(nw * 4), &ws, lease, dl)) return rc;
   DeviceScope ds(ws->device);
-  uint8_t* d_bytes = ws->dbuf;
-  uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
-  HIP_TRY(hipMemcpyAsync(d_bytes, in, len, hipMemcpyHostToDevice, ws->stream));
-  HIP_TRY(launch_map_pack(d_bytes, len, n, d_words, nullptr, ws->stream));
-  HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
-  return 0;
+  const int rc = pack_windows(ws, in, len, n, out, ws->dbuf, (uint32_t*)(ws->dbuf + bbytes), nullptr);
+  if (rc) drain_stages(ws);
+  return rc;
 }
 
-// gf.MapToGF's choice of mapping (map.go:35-66) for `len` bytes already on
-// the device: pack them (mapping 0) into d_words, OR-reduce the two flags,
-// then 0, else 1<<31, else the first fitting value of the library's random
-// candidate stream (64 per device probe pass).  d_scratch holds 4 + 2*64 words.
-static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, uint32_t* d_words,
-                        uint32_t* d_scratch, uint32_t* mapping) {
+// gf.MapToGF's choice of mapping (map.go:35-66) from the two flags already
+// OR-reduced into d_scratch[0] while packing the nw words at d_words with
+// mapping 0: 0, else 1<<31, else the first fitting value of the library's
+// random candidate stream (64 per device probe pass).  d_scratch holds
+// 4 + 2*64 words.
+static int choose_mapping(hipStream_t st, const uint32_t* d_words, uint64_t nw, uint32_t* d_scratch,
+                          uint32_t* mapping) {
   constexpr uint32_t kCand = 64;
-  const uint64_t nw = (len + 3) / 4;
   uint32_t* d_flags = d_scratch;
   uint32_t* d_cand = d_flags + 4;
   uint32_t* d_bad = d_cand + kCand;
   uint32_t flags = 0;
-  HIP_TRY(hipMemsetAsync(d_flags, 0, 4, st));
-  HIP_TRY(launch_map_pack(d_bytes, len, 0, d_words, d_flags, st));
   HIP_TRY(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   *mapping = 0;
@@ -1495,6 +1518,14 @@ static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, ui
   return status_of(Status::MappingFallback, "MapToGF");
 }
 
+// pack (mapping 0, flags) + choose_mapping for `len` bytes already on the device.
+static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, uint32_t* d_words,
+                        uint32_t* d_scratch, uint32_t* mapping) {
+  HIP_TRY(hipMemsetAsync(d_scratch, 0, 4, st));
+  HIP_TRY(launch_map_pack(d_bytes, len, 0, d_words, d_scratch, st));
+  return choose_mapping(st, d_words, (len + 3) / 4, d_scratch, mapping);
+}
+
 int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
   if (!mapping) return fail(Status::InvalidArg, "MapToGF: null mapping");
   const uint64_t nw = (len + 3) / 4;
@@ -1510,14 +1541,27 @@ int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint3
   uint8_t* d_bytes = ws->dbuf;
   uint32_t* d_words = (uint32_t*)(ws->dbuf + bbytes);
   uint32_t* d_scratch = (uint32_t*)(ws->dbuf + bbytes + wbytes);
-  HIP_TRY(hipMemcpyAsync(d_bytes, in, len, hipMemcpyHostToDevice, ws->stream));
-  uint32_t m = 0;
-  if (int rc = pick_mapping(ws->stream, d_bytes, len, d_words, d_scratch, &m)) return rc;
-  if (m) HIP_TRY(launch_xor_words(d_words, nw, m, ws->stream));
-  HIP_TRY(hipMemcpyAsync(out, d_words, nw * 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
-  *mapping = m;
-  return 0;
+  auto body = [&]() -> int {
+    // Speculative mapping 0 (map.go:35-45): the words stream back while the
+    // flags of every window accumulate on the device; 1<<31 (map.go:47-62,
+    // about 2% of uniform 64 MiB bodies) or the random fallback (:64-66)
+    // re-map the words on the device and send them again.
+    HIP_TRY(hipMemsetAsync(d_scratch, 0, 4, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    if (int rc = pack_windows(ws, in, len, 0, out, d_bytes, d_words, d_scratch)) return rc;
+    uint32_t m = 0;
+    if (int rc = choose_mapping(ws->stream, d_words, nw, d_scratch, &m)) return rc;
+    if (m) {
+      HIP_TRY(launch_xor_words(d_words, nw, m, ws->stream));
+      const Span sp{(uint8_t*)out, (uint64_t)((uint8_t*)d_words - ws->dbuf), nw * 4};
+      if (int rc = staged_d2h(ws, ws->dbuf, &sp, 1)) return rc;
+    }
+    *mapping = m;
+    return 0;
+  };
+  const int rc = body();
+  if (rc) drain_stages(ws);
+  return rc;
 }
 
 int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t* out) {
@@ -1531,11 +1575,21 @@ int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t
   DeviceScope ds(ws->device);
   uint32_t* d_words = (uint32_t*)ws->dbuf;
   uint8_t* d_bytes = ws->dbuf + wbytes;
-  HIP_TRY(hipMemcpyAsync(d_words, in, count * 4, hipMemcpyHostToDevice, ws->stream));
-  HIP_TRY(launch_map_unpack(d_words, count, n, d_bytes, ws->stream));
-  HIP_TRY(hipMemcpyAsync(out, d_bytes, count * 4, hipMemcpyDeviceToHost, ws->stream));
-  HIP_TRY(hipStreamSynchronize(ws->stream));
-  return 0;
+  const uint64_t W = kCodecWindowBytes / 4, nwin = (count + W - 1) / W;  // words per window
+  const int rc = run_windows(
+      "codec_unpack", ws, ws->dbuf, nwin, 2 * kCodecWindowBytes,
+      [&](uint64_t c, int, Window& w) {
+        const uint64_t w0 = c * W, nwd = std::min(W, count - w0);
+        w.in.push_back({(uint8_t*)(in + w0), 4 * w0, 4 * nwd});
+        w.out.push_back({out + 4 * w0, wbytes + 4 * w0, 4 * nwd});
+      },
+      [&](uint64_t c, int, hipStream_t st) -> int {
+        const uint64_t w0 = c * W, nwd = std::min(W, count - w0);
+        HIP_TRY(launch_map_unpack(d_words + w0, nwd, n, d_bytes + 4 * w0, st));
+        return 0;
+      });
+  if (rc) drain_stages(ws);
+  return rc;
 }
 
 // ---- per-call context entry points (cgo) ------------------------------------------

@@ -50,13 +50,15 @@ def MapToGFWith(data, n: int) -> np.ndarray:
     return out
 
 
-def MapFromGF(n: int, v) -> bytes:
-    """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v))."""
+def MapFromGF(n: int, v) -> bytearray:
+    """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v)); a
+    bytearray, Go's mutable []byte, written in place by the library."""
     words = np.ascontiguousarray(v, dtype=np.uint32)
-    out = np.zeros(words.size * 4, dtype=np.uint8)
+    out = bytearray(words.size * 4)
+    ptr = (ctypes.c_char * len(out)).from_buffer(out) if out else None
     N.check(lib.slime_gf_map_from_gf(n & 0xFFFFFFFF, words.ctypes.data if words.size else None, words.size,
-                                     out.ctypes.data if out.size else None))
-    return out.tobytes()
+                                     ctypes.addressof(ptr) if ptr is not None else None))
+    return out
 
 
 def Seed(seed: int) -> None:

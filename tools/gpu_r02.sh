@@ -51,6 +51,8 @@ for step in "$@"; do
             --rounds 3 --burst 1 --batched 2,3 ;;
     stage_fast) run stage_fast 600 python tools/apply_variants.py --hunt fast --variants 15 --blocks 256,512 --rounds 3 \
             --burst 1 --batched 2,3 ;;
+    hostbd) run hostbd 300 python tools/host_breakdown.py ;;
+    hostbd16) run hostbd16 300 python tools/host_breakdown.py --mib 16 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
