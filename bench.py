@@ -294,7 +294,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     par2 = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
-    return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r),
+    return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "link": link_probe(obj_mib),
             "unchanged_caller": {
                 "write_gibs": g(t_uw), "read_gibs": g(t_ur),
                 "create_parity_x_r_gibs": g(t_cp), "create_parities_batched_gibs": g(t_cps),
@@ -305,6 +305,46 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
             "object_mib": obj_mib, "erased": erase, "verified": ok,
             "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
                     "PCIe-inclusive; not `value`"}
+
+
+def link_probe(mib: int) -> dict:
+    """The host side's own ceilings in this process, beside the host-path rates
+    (their run-to-run spread, DESIGN.md "End-to-end"): pinned DMA each way and
+    a single-thread host memcpy, median of 5, GB/s."""
+    import numpy as np
+    n = mib << 20
+    pin = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    src = np.ones(n, dtype=np.uint8)
+    dst = np.empty(n, dtype=np.uint8)
+    dst[:] = 0
+
+    def dma(h2d: bool) -> float:
+        ts = []
+        for _ in range(6):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            if h2d:
+                dev.copy_(pin, non_blocking=True)
+            else:
+                pin.copy_(dev, non_blocking=True)
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) * 1e-3)
+        return sorted(ts[1:])[2]
+
+    def memcpy() -> float:
+        ts = []
+        for _ in range(6):
+            t0 = time.perf_counter()
+            np.copyto(dst, src)
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts[1:])[2]
+
+    out = {"h2d_pinned_gbs": round(n / dma(True) / 1e9, 1), "d2h_pinned_gbs": round(n / dma(False) / 1e9, 1),
+           "host_memcpy_1thread_gbs": round(n / memcpy() / 1e9, 1), "bytes": n}
+    del pin, dev
+    return out
 
 
 def board_info(dev: int) -> dict:
@@ -325,6 +365,12 @@ def board_info(dev: int) -> dict:
         if val:
             info[key] = val
     return info
+
+
+def shape_label(need: int, total: int, mib: int) -> str:
+    """BASELINE.json's config name for a shape, if it is one of them."""
+    return {(8, 12, 256): "C3+C4: ", (4, 6, 64): "C2: ", (10, 14, 1024): "C5: ",
+            (8, 12, 512): "north-star 64 MiB shards: "}.get((need, total, mib), "")
 
 
 def kernel_source_id() -> str:
@@ -418,8 +464,10 @@ def main():
     batch.barrier()
     elapsed = time.perf_counter() - t0
 
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    enc_all = [e[0].elapsed_time(e[1]) for e in events]
+    dec_all = [e[1].elapsed_time(e[2]) for e in events]
+    enc_ms = sum(enc_all) / args.steps
+    dec_ms = sum(dec_all) / args.steps
 
     # Correctness of what was timed: every rebuilt shard equals the true one.
     got = buf.view(nobj, total, SS)[:, erase, :L] if args.decode_dst == "inplace" \
@@ -482,8 +530,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic (splitmix64 symbols in [0,p), seeded per rank; MapToGF domain)",
             "config": {
-                "workload": f"C3+C4: need={need} total={total}, {args.object_mib} MiB objects x {nobj} per GPU; "
-                            f"encode all parity + decode erased {erase}",
+                "workload": f"{shape_label(need, total, args.object_mib)}need={need} total={total}, "
+                            f"{args.object_mib} MiB objects x {nobj} per GPU; encode all parity + decode erased {erase}",
                 "need": need, "total": total, "object_mib": args.object_mib, "objects_per_gpu": nobj,
                 "symbols_per_shard": L, "shard_stride_symbols": SS, "erased": erase, "decode_dst": args.decode_dst,
                 "parallelism": f"object-partition x{world} (no RCCL)",
@@ -491,7 +539,9 @@ def main():
             "encode_gibs": round(obj_bytes / GIB / (enc_ms * 1e-3), 2),
             "decode_gibs": round(obj_bytes / GIB / (dec_ms * 1e-3), 2),
             "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4),
-                          "encode_max_rank": round(enc_ms_max, 4), "decode_max_rank": round(dec_ms_max, 4)},
+                          "encode_max_rank": round(enc_ms_max, 4), "decode_max_rank": round(dec_ms_max, 4),
+                          "encode_min_max": [round(min(enc_all), 4), round(max(enc_all), 4)],
+                          "decode_min_max": [round(min(dec_all), 4), round(max(dec_all), 4)]},
             "verified": bad == 0.0,
             "roofline": {
                 "bound": "hbm",

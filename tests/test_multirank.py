@@ -48,7 +48,11 @@ def _worker(rank, world, port, q):
         elapsed, objs = batch.max_over_ranks([1.0 + rank, float(count)])
         t = torch.tensor([float(count)], dtype=torch.float64)
         dist.all_reduce(t)
-        q.put((rank, start, count, elapsed, objs, t.item()))
+        # bench.py's n_gpus: distinct device addresses over ranks (two ranks
+        # reporting one PCI address count as one GPU)
+        bdfs = batch.gather_strings(f"0000:{rank:02x}:00.0")
+        shared = batch.gather_strings("0000:5d:00.0")
+        q.put((rank, start, count, elapsed, objs, t.item(), len(set(bdfs)), len(set(shared)), bdfs))
     finally:
         dist.destroy_process_group()
 
@@ -67,3 +71,5 @@ def test_gloo_world2_partition_and_max_timing():
     assert [(r[1], r[2]) for r in res] == [(0, 32), (32, 32)]
     assert all(r[3] == 2.0 for r in res)  # max over ranks
     assert all(r[5] == 64.0 for r in res)  # every object once
+    assert all(r[6] == 2 and r[7] == 1 for r in res)  # n_gpus counts distinct devices
+    assert all(r[8] == ["0000:00:00.0", "0000:01:00.0"] for r in res)  # rank order

@@ -53,6 +53,10 @@ for step in "$@"; do
             --burst 1 --batched 2,3 ;;
     hostbd) run hostbd 300 python tools/host_breakdown.py ;;
     hostbd16) run hostbd16 300 python tools/host_breakdown.py --mib 16 ;;
+    shapes) run shape_64mib 300 python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+            run shape_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 &&
+            run shape_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 &&
+            run shape_c3_again 300 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
