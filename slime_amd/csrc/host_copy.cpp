@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -18,6 +19,14 @@ namespace {
 
 constexpr size_t kPiece = 512u << 10;  // bytes per work piece
 constexpr size_t kSerialBelow = 2u << 20;  // small copies: not worth a wake-up
+// After a job a worker spins this long for the next one before it sleeps.
+// A host call posts one job per window (8-16 MiB, a fraction of a ms of
+// copying); a worker that went to sleep between windows can take longer to
+// wake than the caller needs to copy the whole window alone.  That is what
+// the slow runs of the object entry points were: the same rate as with no
+// workers at all (10 / 7 GiB/s against 28 / 24, tools/host_diag.py,
+// profiles/r02/s8_hostdiag).
+constexpr std::chrono::microseconds kSpin{3000};
 
 struct Job {
   const CopyItem* pieces = nullptr;
@@ -84,7 +93,7 @@ class Pool {
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+      stop_.store(true);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -103,6 +112,7 @@ class Pool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       cur_ = &j;
+      posted_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     const size_t did = drain(&j);
@@ -114,10 +124,28 @@ class Pool {
 
  private:
   void worker() {
-    std::unique_lock<std::mutex> lk(mu_);
+    uint64_t seen = 0;
     for (;;) {
-      cv_.wait(lk, [&] { return stop_ || (cur_ && cur_->next.load(std::memory_order_relaxed) < cur_->n); });
-      if (stop_) return;
+      // Hot wait: poll the job counter (pool state only, never a job) for kSpin.
+      const auto deadline = std::chrono::steady_clock::now() + kSpin;
+      bool timed_out = false;
+      for (uint32_t it = 1; posted_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed);
+           ++it) {
+        _mm_pause();
+        if ((it & 255) == 0 && std::chrono::steady_clock::now() > deadline) {
+          timed_out = true;
+          break;
+        }
+      }
+      std::unique_lock<std::mutex> lk(mu_);
+      auto ready = [&] { return stop_.load() || (cur_ && cur_->next.load(std::memory_order_relaxed) < cur_->n); };
+      if (!timed_out && !ready()) {  // a job came and went while this worker spun up: keep spinning
+        seen = posted_.load(std::memory_order_relaxed);
+        continue;
+      }
+      cv_.wait(lk, ready);
+      if (stop_.load()) return;
+      seen = posted_.load(std::memory_order_relaxed);
       Job* j = cur_;
       ++j->active;
       lk.unlock();
@@ -133,7 +161,8 @@ class Pool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   Job* cur_ = nullptr;
-  bool stop_ = false;
+  std::atomic<uint64_t> posted_{0};  // jobs posted so far (the spinners' signal)
+  std::atomic<bool> stop_{false};
   std::vector<std::thread> th_;
 };
 

@@ -1440,14 +1440,23 @@ static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease, D
 // others, and fresh (never touched) output pages are faulted in by the
 // ring's host copy instead of by a DMA (the direct pageable copy of round 1
 // fell to 0.5 GiB/s into fresh pages, DESIGN.md "End-to-end").
-constexpr uint64_t kCodecWindowBytes = 8u << 20;  // input bytes per window (+ as many out)
+constexpr uint64_t kCodecWindowBytes = 8u << 20;  // largest window: input bytes (+ as many out)
+
+// Input bytes per codec window: at least 4 windows per call when the input
+// allows (so H2D, kernel and D2H of one call overlap across the ring's 3
+// stages: an 8 MiB chunk in one window runs them back to back), between
+// 512 KiB and 8 MiB, a multiple of 64 KiB.
+static uint64_t codec_window(uint64_t len) {
+  const uint64_t quarter = ((len / 4) + 65535) & ~(uint64_t)65535;
+  return std::min<uint64_t>(kCodecWindowBytes, std::max<uint64_t>(512u << 10, quarter));
+}
 
 // Bytes -> words windows of MapToGF(With): window c packs input bytes
 // [c*W, c*W + W) into words [c*W/4, ...) on the device (mapping n, flags
 // OR-reduced if given) and streams the words back to `out`.
 static int pack_windows(Workspace* ws, const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out,
                         uint8_t* d_bytes, uint32_t* d_words, uint32_t* d_flags) {
-  const uint64_t W = kCodecWindowBytes, nwin = (len + W - 1) / W;
+  const uint64_t W = codec_window(len), nwin = (len + W - 1) / W;
   uint8_t* const base = ws->dbuf;
   return run_windows(
       "codec_pack", ws, base, nwin, 2 * W,
@@ -1575,7 +1584,7 @@ int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t
   DeviceScope ds(ws->device);
   uint32_t* d_words = (uint32_t*)ws->dbuf;
   uint8_t* d_bytes = ws->dbuf + wbytes;
-  const uint64_t W = kCodecWindowBytes / 4, nwin = (count + W - 1) / W;  // words per window
+  const uint64_t W = codec_window(4 * count) / 4, nwin = (count + W - 1) / W;  // words per window
   const int rc = run_windows(
       "codec_unpack", ws, ws->dbuf, nwin, 2 * kCodecWindowBytes,
       [&](uint64_t c, int, Window& w) {

@@ -57,6 +57,13 @@ for step in "$@"; do
             run shape_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 &&
             run shape_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 &&
             run shape_c3_again 300 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    hostdiag) run hostdiag 600 python tools/host_diag.py ;;
+    hostdiag4) run hostdiag4 600 python tools/host_diag.py --threads 4,8 --pre bench &&
+               run hostdiag5 600 python tools/host_diag.py --threads 0,2,4 --pre none &&
+               run bench_host 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
+    hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
+               run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
+               run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
