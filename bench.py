@@ -63,6 +63,11 @@ def parse():
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
     ap.add_argument("--host-path", type=int, default=1,
                     help="rank 0 at N=1: PCIe-inclusive writeChunks/reconstruct from host memory (never `value`)")
+    ap.add_argument("--host-order", choices=["before-free", "after-free"], default="before-free",
+                    help="run the host leg before the device buffers are freed (default) or after the bytes leg "
+                         "freed them: the driver then wipes the freed VRAM with the same DMA engines the host "
+                         "path uses, which slows its transfers for seconds (DESIGN.md, End-to-end)")
+    ap.add_argument("--host-delay", type=float, default=0.0, help="seconds to wait before the host leg")
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
@@ -509,11 +514,23 @@ def main():
     # Distinct devices across ranks (n_gpus), by PCI address.
     bdfs = batch.gather_strings(board_info(dev)["bdf"])
 
+    host = None
+    want_host = rank == 0 and world == 1 and args.host_path
+
+    def run_host_leg():
+        if args.host_delay > 0:
+            time.sleep(args.host_delay)
+        return dict(host_leg(need, total, erase), order=args.host_order, delay_s=args.host_delay)
+
+    if want_host and args.host_order == "before-free":
+        host = run_host_leg()
     bytes_path = None
     if args.bytes_path:
         del buf, rec  # rec aliases buf for in-place repair
         torch.cuda.empty_cache()
         bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj)
+    if want_host and args.host_order == "after-free":
+        host = run_host_leg()
 
     if rank == 0:
         line = {
@@ -558,8 +575,8 @@ def main():
             "object_bytes_path": bytes_path,
         }
         line["device"] = board_info(dev)
-        if world == 1 and args.host_path:
-            line["host_path"] = host_leg(need, total, erase)
+        if host is not None:
+            line["host_path"] = host
         if world == 1 and args.cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib, args.cpu_seconds)
         print(json.dumps(line), flush=True)

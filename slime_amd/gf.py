@@ -28,7 +28,10 @@ def Raise(x: int, n: int) -> int:
 
 
 def _bytes(b) -> np.ndarray:
-    return np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b, np.uint8)
+    """A uint8 view of b (bytes, bytearray, memoryview, ndarray) without copying it."""
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(b).cast("B"), dtype=np.uint8) if len(b) else np.zeros(0, dtype=np.uint8)
 
 
 def MapToGF(data) -> tuple[int, np.ndarray]:

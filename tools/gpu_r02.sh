@@ -61,6 +61,14 @@ for step in "$@"; do
     hostdiag4) run hostdiag4 600 python tools/host_diag.py --threads 4,8 --pre bench &&
                run hostdiag5 600 python tools/host_diag.py --threads 0,2,4 --pre none &&
                run bench_host 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
+    hosttrace) run trace_bytes 300 env SLIME_RS_PIPE_TRACE=1 python bench.py --cpu-baseline 0 &&
+               run trace_nobytes 300 env SLIME_RS_PIPE_TRACE=1 python bench.py --cpu-baseline 0 --bytes-path 0 &&
+               run trace_bytes2 300 env SLIME_RS_PIPE_TRACE=1 python bench.py --cpu-baseline 0 ;;
+    hostorder) run order_before 300 python bench.py --cpu-baseline 0 &&
+               run order_after 300 python bench.py --cpu-baseline 0 --host-order after-free &&
+               run order_after_10s 300 python bench.py --cpu-baseline 0 --host-order after-free --host-delay 10 ;;
+    sdma) run order_after_nosdma 300 env HSA_ENABLE_SDMA=0 python bench.py --cpu-baseline 0 --host-order after-free &&
+          run order_before_nosdma 300 env HSA_ENABLE_SDMA=0 python bench.py --cpu-baseline 0 ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;

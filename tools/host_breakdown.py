@@ -55,8 +55,17 @@ def main():
     code = parts + rs.CreateParities(parts, total)
     sym = [code[i] for i in have]
     rec = [np.zeros(L, dtype=np.uint32) for _ in range(need)]
+    import ctypes
+    from slime_amd import _native as N
+    reused = np.zeros(words.size, dtype=np.uint32)
+    mv = ctypes.c_uint32()
+
+    def map_reused():
+        N.check(N.lib.slime_gf_map_to_gf(data.ctypes.data, data.size, ctypes.byref(mv), reused.ctypes.data))
+
     t = {
         "MapToGF(object)": med(lambda: gf.MapToGF(data), a.reps),
+        "MapToGF(object, reused output)": med(map_reused, a.reps),
         "CreateParity(1 row)": med(lambda: rs.CreateParity(parts, need, par[0]), a.reps),
         "MapFromGF(1 chunk)": med(lambda: gf.MapFromGF(m, parts[0]), a.reps),
         "MapToGFWith(1 chunk)": med(lambda: gf.MapToGFWith(chunk, m), a.reps),
