@@ -69,6 +69,10 @@ for step in "$@"; do
                run order_after_10s 300 python bench.py --cpu-baseline 0 --host-order after-free --host-delay 10 ;;
     sdma) run order_after_nosdma 300 env HSA_ENABLE_SDMA=0 python bench.py --cpu-baseline 0 --host-order after-free &&
           run order_before_nosdma 300 env HSA_ENABLE_SDMA=0 python bench.py --cpu-baseline 0 ;;
+    c2sweep) for g in 256 512 1024 2048; do for sg in 8 16 32; do
+               run c2_g${g}_s${sg} 120 env SLIME_RS_GRID_TARGET=$g SLIME_RS_SEGMENTS=$sg python bench.py --need 4 --total 6 \
+                 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 || exit $?
+             done; done ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
