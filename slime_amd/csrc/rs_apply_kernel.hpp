@@ -369,9 +369,21 @@ __device__ __forceinline__ void wide_load16(uint4 (&x)[16], const uint32_t* __re
   }
 }
 
-// acc = (acc + sum_j c[j] * x[j]) mod p, exact, one fold.
+// acc = (acc + sum_j c[j] * x[j]) mod p, exact, one fold.  MATH = false is
+// the tuning harness's XOR stand-in (wrong results by design; see xor4).
+template <bool MATH = true>
 __device__ __forceinline__ void wide_mac16(const uint4 (&x)[16], const uint32_t* __restrict__ crow, uint4& acc) {
   const u32x16 c = *reinterpret_cast<const u32x16*>(crow);
+  if constexpr (!MATH) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc.x ^= x[j].x + c[j];
+      acc.y ^= x[j].y + c[j];
+      acc.z ^= x[j].z + c[j];
+      acc.w ^= x[j].w + c[j];
+    }
+    return;
+  }
   uint64_t lo0 = acc.x, lo1 = acc.y, lo2 = acc.z, lo3 = acc.w;
   uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
 #pragma unroll
@@ -380,7 +392,7 @@ __device__ __forceinline__ void wide_mac16(const uint4 (&x)[16], const uint32_t*
 }
 
 // One item's math (and the row block's stores after its last chunk).
-template <int RB, bool NTS>
+template <int RB, bool NTS, bool MATH = true>
 __device__ __forceinline__ void wide_item(const uint4 (&x)[16], uint4 (&acc)[RB], const WideItem& it, uint32_t nch,
                                           uint32_t rows, uint32_t cs, const uint32_t* __restrict__ coeff,
                                           const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ ob,
@@ -391,10 +403,10 @@ __device__ __forceinline__ void wide_item(const uint4 (&x)[16], uint4 (&acc)[RB]
   }
   const uint32_t r0 = it.rb * RB;
   const uint32_t* const c0 = coeff + (uint64_t)r0 * cs + it.jc * 16;
-  wide_mac16(x, c0, acc[0]);
+  wide_mac16<MATH>(x, c0, acc[0]);
 #pragma unroll
   for (int i = 1; i < RB; ++i)
-    if (r0 + i < rows) wide_mac16(x, c0 + (uint64_t)i * cs, acc[i]);
+    if (r0 + i < rows) wide_mac16<MATH>(x, c0 + (uint64_t)i * cs, acc[i]);
   if (it.jc == nch - 1 && g < v1) {
 #pragma unroll
     for (int i = 0; i < RB; ++i)
@@ -405,7 +417,7 @@ __device__ __forceinline__ void wide_item(const uint4 (&x)[16], uint4 (&acc)[RB]
   }
 }
 
-template <int RB, bool NTL, bool NTS>
+template <int RB, bool NTL, bool NTS, bool MATH = true>
 __global__ __launch_bounds__(kBlock) void rs_apply_wide_pipe_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
@@ -437,14 +449,14 @@ __global__ __launch_bounds__(kBlock) void rs_apply_wide_pipe_kernel(
       wide_next(nx, nch, nrb, nwaves);
       const WideItem& ld = nx.tile < ntiles ? nx : it;
       wide_load16<NTL>(xb, ib, in_idx, in_shard, k, ld.jc, v0 + ld.tile * 64 + lane, v1);
-      wide_item<RB, NTS>(xa, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
+      wide_item<RB, NTS, MATH>(xa, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
       it = nx;
       if (it.tile >= ntiles) break;
       nx = it;
       wide_next(nx, nch, nrb, nwaves);
       const WideItem& ld2 = nx.tile < ntiles ? nx : it;
       wide_load16<NTL>(xa, ib, in_idx, in_shard, k, ld2.jc, v0 + ld2.tile * 64 + lane, v1);
-      wide_item<RB, NTS>(xb, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
+      wide_item<RB, NTS, MATH>(xb, acc, it, nch, rows, cs, coeff, out_idx, ob, out_shard, v0 + it.tile * 64 + lane, v1);
       it = nx;
     }
     if (seg == nseg - 1)

@@ -251,6 +251,26 @@ extern "C" int av_launch_burst(int T, const uint32_t* in, uint32_t* out, uint64_
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// Wide-k pipelined kernel (the product's rs_apply_wide_pipe_kernel) with the
+// field math or the XOR stand-in: how much of a wide launch is VALU?
+extern "C" int av_launch_wide(int math, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
+                              uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                              uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, uint32_t gx, uint32_t gy,
+                              void* stream, uint32_t nseg) {
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(gx, gy), b(kBlock);
+#define W(RB, M) \
+  hipLaunchKernelGGL((rs_apply_wide_pipe_kernel<RB, true, true, M>), g, b, 0, s, in, out, io, is, oo, os, coeff, ii, oi, \
+                     ncols, nobj, rows, k, nseg)
+  if (rows <= 8) {
+    if (math) W(8, true); else W(8, false);
+  } else {
+    if (math) W(16, true); else W(16, false);
+  }
+#undef W
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // Phased walk launch (k = 8, 4 rows): U in {3, 6}.
 extern "C" int av_launch_phased(int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                 uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,

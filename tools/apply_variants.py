@@ -54,6 +54,7 @@ def main():
                     help="re-allocate until the product encode runs in the given placement mode")
     ap.add_argument("--phased", type=str, default="",
                     help="time-phased walks U:period:rwin (100 MHz ticks), comma list, e.g. 3:700:460,6:1400:930")
+    ap.add_argument("--wide", type=int, default=0, help="k > 16: time the wide kernel with field math (500) and XOR (501)")
     ap.add_argument("--batched", type=str, default="", help="register-batched stores: U list (2,3)")
     ap.add_argument("--burst", type=str, default="", help="LDS-staged write bursts: tiles per burst, comma list (1..3)")
     ap.add_argument("--separate", type=int, default=-1,
@@ -69,10 +70,18 @@ def main():
     for t in (int(x) for x in args.burst.split(",") if x):
         BURST[200 + t] = t
         VARIANTS[200 + t] = f"pipe U3 + LDS-staged store bursts of {t} tiles"
+    if args.wide:
+        VARIANTS.clear()
+        VARIANTS[500] = "wide pipe, field math (product)"
+        VARIANTS[501] = "wide pipe, XOR stand-in (wrong by design)"
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
+    lib.av_launch_wide.restype = ctypes.c_int
+    lib.av_launch_wide.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
     lib.av_launch_batched.restype = ctypes.c_int
     lib.av_launch_batched.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -136,7 +145,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     shards = lambda: buf.view(nobj, total, SS)[:, :, :L]  # noqa: E731
     ref = shards()[:, need:, :].clone()
 
-    coeff = np.zeros((r, 16), dtype=np.uint32)
+    coeff = np.zeros((r, max(16, -(-need // 16) * 16)), dtype=np.uint32)
     s = torch.cuda.current_stream()
     separate = args.separate if args.separate >= 0 else int(bool(args.decode))
     if args.decode:
@@ -163,6 +172,12 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
     def launch(v, gx, gy, nseg=1):
+        if v in (500, 501):
+            rc = lib.av_launch_wide(int(v == 500), buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
+                                    ii.data_ptr(), oi.data_ptr(), L, nobj, r, need, gx, gy,
+                                    ctypes.c_void_p(s.cuda_stream), nseg)
+            assert rc == 0, rc
+            return
         if v in BATCHED:
             assert r == 4 and need == 8, "batched walk is built for 8/12 (4 rows)"
             rc = lib.av_launch_batched(BATCHED[v], buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
@@ -208,6 +223,8 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     # correctness of every variant and segment count
     bad = []
     for v in VARIANTS:
+        if v == 501:
+            continue  # wrong by design
         for ns in segs:
             view().zero_()
             launch(v, 4, 8, ns)

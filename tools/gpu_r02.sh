@@ -73,6 +73,9 @@ for step in "$@"; do
                run c2_g${g}_s${sg} 120 env SLIME_RS_GRID_TARGET=$g SLIME_RS_SEGMENTS=$sg python bench.py --need 4 --total 6 \
                  --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 || exit $?
              done; done ;;
+    widemath) run wide_20_24 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --blocks 256,1024 &&
+              run wide_32_40 300 python tools/apply_variants.py --need 32 --total 40 --nobj 32 --wide 1 --blocks 256,1024 &&
+              run wide_64_80 300 python tools/apply_variants.py --need 64 --total 80 --nobj 16 --wide 1 --blocks 256,1024 ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
