@@ -888,3 +888,59 @@ def test_device_pool_routes_unpinned_calls():
     lens = (ctypes.c_uint64 * 2)(3, 3)
     assert N.lib.slime_rs_create_parity_ex(ctypes.byref(call), ptrs, lens, 2, 2, out.ctypes.data) == 0
     assert buf.value == b"" and out.tolist() == OC.create_parity([x, x], 2)[1].tolist()
+
+
+def test_concurrent_host_callers_match_oracle():
+    """The reference's callers are concurrent (25 HTTP goroutines by default,
+    main.go:107-109; scrubbers, multi.go:54-58).  Eight threads run the object
+    entry points and the Go-API data path at once, on mixed shapes and survivor
+    sets, with the plan cache capped below the number of live survivor sets, so
+    workspaces, the copy pool, the device pool and plan eviction all run under
+    contention.  Every result is checked against the oracle's framing."""
+    import threading
+    from slime_amd import objects
+    N.set_plan_cache_capacity(4)
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(1000 + t)
+            for it in range(6):
+                need = int(rng.choice([2, 4, 8, 10, 17]))
+                total = need + int(rng.integers(0, 5))
+                S = int(rng.choice([5, 4096, 100003, 3 << 20]))
+                obj = _obj_bytes(rng, S, "high" if it % 3 == 0 else "plain")
+                m, chunks = objects.write_chunks(obj, need, total)
+                m_ref, want = _oracle_chunks(obj, need, total)
+                if m != m_ref or [c.tobytes() for c in chunks] != want:
+                    errors.append(("write_chunks", t, it, need, total, S))
+                    continue
+                have = sorted(rng.choice(total, size=need, replace=False).tolist())
+                got = objects.reconstruct([chunks[i] for i in have], have, m, S)
+                if got.tobytes() != obj:
+                    errors.append(("reconstruct", t, it, need, total, S, have))
+                L = 1 + int(rng.integers(0, 5000))
+                data = rand_vecs(rng, need, L)
+                idx = need + int(rng.integers(0, max(1, total - need) + 1))
+                if not np.array_equal(rs.CreateParity(data, idx), OC.create_parity(data, idx)[1]):
+                    errors.append(("CreateParity", t, it, need, idx))
+                code = [np.ascontiguousarray(OC.create_parity(data, i)[1]) for i in range(need + 3)]
+                hv = sorted(rng.choice(need + 3, size=need, replace=False).tolist())
+                rec = rs.RecoverData([code[i] for i in hv], hv)
+                ref = OC.recover_data([code[i] for i in hv], hv)[1]
+                if not all(np.array_equal(a, b) for a, b in zip(rec, ref)):
+                    errors.append(("RecoverData", t, it, need, hv))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(("exception", t, repr(e)))
+
+    try:
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+    finally:
+        N.set_plan_cache_capacity(256)
+    assert not errors, errors[:5]
+    st = N.plan_cache_stats()
+    assert st["live"] <= 256
