@@ -264,10 +264,20 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
             ts.append(time.perf_counter() - t0)
         return sorted(ts)[len(ts) // 2]
 
+    from slime_amd import _native as N
+
+    def split(st):  # ms per call of the windowed pipeline, from slime_rs_host_stats
+        c = max(1, st["calls"])
+        return {k[:-3] + "_ms": round(st[k] / 1e3 / c, 3) for k in ("copy_in_us", "enqueue_us", "wait_us",
+                                                                      "copy_out_us", "total_us")}
+
     box = {}
+    N.host_stats(reset=True)
     t_w = med(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
+    split_w = split(N.host_stats(reset=True))
     surv = [chunks[i] for i in have]
     t_r = med(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
+    split_r = split(N.host_stats(reset=True))
     ok = bool(np.array_equal(out, data))
 
     # The unchanged caller, call by call (Go API mirrors, slime_amd.rs / .gf).
@@ -300,6 +310,9 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
     return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "link": link_probe(obj_mib),
+            "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
+                               "what": "mean per call: host copies in/out, launches, waits on the device/link side "
+                                       "(a large wait with normal copies = DMA contention, DESIGN.md End-to-end)"},
             "unchanged_caller": {
                 "write_gibs": g(t_uw), "read_gibs": g(t_ur),
                 "create_parity_x_r_gibs": g(t_cp), "create_parities_batched_gibs": g(t_cps),

@@ -305,6 +305,16 @@ typedef struct slime_rs_cache_stats {
 int slime_rs_plan_cache_stats(slime_rs_cache_stats_t *stats);
 /* Set the cache capacity (>= 1); shrinking evicts at once. */
 int slime_rs_plan_cache_capacity(uint64_t capacity);
+/* Where the host entry points' windowed pipeline spends its wall time (all
+ * threads, since the start or the last reset; microseconds): copy_in = host
+ * copies into pinned staging, enqueue = DMA/kernel launches, wait = waiting
+ * for a stage's transfers and kernels (device and link side), copy_out = host
+ * copies out of pinned staging.  reset != 0 zeroes the counters after reading. */
+typedef struct slime_rs_host_stats {
+  uint64_t calls, windows;
+  uint64_t copy_in_us, enqueue_us, wait_us, copy_out_us, total_us;
+} slime_rs_host_stats_t;
+int slime_rs_host_stats(slime_rs_host_stats_t *stats, int reset);
 /* Host calls the device pool has routed to `device` so far and calls in flight there. */
 int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
 

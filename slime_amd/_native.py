@@ -46,6 +46,12 @@ class CacheStats(ctypes.Structure):
 ANY_DEVICE = -1
 
 
+class HostStats(ctypes.Structure):
+    """slime_rs_host_stats_t."""
+    _fields_ = [(f, ctypes.c_uint64) for f in ("calls", "windows", "copy_in_us", "enqueue_us", "wait_us",
+                                                "copy_out_us", "total_us")]
+
+
 class Layout(ctypes.Structure):
     """slime_rs_layout_t: shard s of object o at base + o*obj_stride + s*shard_stride."""
     _fields_ = [("obj_stride", ctypes.c_uint64), ("shard_stride", ctypes.c_uint64)]
@@ -142,6 +148,7 @@ SIGNATURES = [
     ("slime_rs_plan_cache_stats", ctypes.c_int, [ctypes.POINTER(CacheStats)]),
     ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
     ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
+    ("slime_rs_host_stats", ctypes.c_int, [ctypes.POINTER(HostStats), ctypes.c_int]),
 ]
 
 for _name, _res, _args in SIGNATURES:
@@ -209,6 +216,13 @@ def plan_cache_stats() -> dict:
 
 def set_plan_cache_capacity(cap: int) -> None:
     check(lib.slime_rs_plan_cache_capacity(cap))
+
+
+def host_stats(reset: bool = False) -> dict:
+    """Split of the host pipeline's wall time (microseconds) since start / last reset."""
+    st = HostStats()
+    check(lib.slime_rs_host_stats(ctypes.byref(st), int(reset)))
+    return {f: int(getattr(st, f)) for f, _ in HostStats._fields_}
 
 
 def pool_calls(device: int) -> tuple[int, int]:

@@ -82,9 +82,28 @@ __device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, ui
   }
 }
 
-// One output row over 4 columns.
+// Coefficient row of a compile-time-K kernel: ceil(K/16) s_load_dwordx16 of
+// a row padded to a multiple of 16 words (the plan table's row stride,
+// coeff_stride(k)); K <= 16 is one load at stride kCoeffStride.
 template <int K>
-__device__ __forceinline__ uint4 dot4(const uint4 (&x)[K], const u32x16& c) {
+struct CoeffRow {
+  static constexpr int kVecs = (K + 15) / 16;
+  static constexpr int kStride = kVecs * 16;
+  u32x16 v[kVecs];
+  __device__ __forceinline__ uint32_t operator[](int j) const { return v[j >> 4][j & 15]; }
+};
+template <int K>
+__device__ __forceinline__ CoeffRow<K> load_coeff_row(const uint32_t* __restrict__ coeff, uint32_t i) {
+  CoeffRow<K> r;
+#pragma unroll
+  for (int q = 0; q < CoeffRow<K>::kVecs; ++q)
+    r.v[q] = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * CoeffRow<K>::kStride + 16 * q);
+  return r;
+}
+
+// One output row over 4 columns (C: a u32x16 for K <= 16, or a CoeffRow<K>).
+template <int K, class C>
+__device__ __forceinline__ uint4 dot4(const uint4 (&x)[K], const C& c) {
   uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
   uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
 #pragma unroll
@@ -219,8 +238,8 @@ __device__ __forceinline__ void load_tile(uint4 (&x)[U][K], const uint32_t* cons
 // XOR stand-in for dot4 (one full-rate op per term instead of mad + addc):
 // WRONG results, used only by the tuning harness (MODE != 0) to measure
 // how much of the pipelined kernel's time the field math costs.
-template <int K>
-__device__ __forceinline__ uint4 xor4(const uint4 (&x)[K], const u32x16& c) {
+template <int K, class C>
+__device__ __forceinline__ uint4 xor4(const uint4 (&x)[K], const C& c) {
   uint4 r = make_uint4(c[0], c[1], c[2], c[3]);
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -236,7 +255,7 @@ template <int K, int U, bool NTS, int MODE = 0>
 __device__ __forceinline__ void tile_row(const uint4 (&x)[U][K], uint32_t* __restrict__ ob,
                                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                          uint64_t out_shard, uint32_t i, uint32_t g0, uint32_t v1) {
-  const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+  const CoeffRow<K> c = load_coeff_row<K>(coeff, i);
   char* const orow = reinterpret_cast<char*>(ob + (uint64_t)out_idx[i] * out_shard);
 #pragma unroll
   for (int u = 0; u < U; ++u) {

@@ -514,6 +514,13 @@ int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std
   return 0;
 }
 
+// Process-wide split of host-pipeline time (slime_rs_host_stats): where the
+// host entry points spend their wall time, in microseconds.
+struct HostStats {
+  std::atomic<uint64_t> calls{0}, windows{0}, copy_in_us{0}, enqueue_us{0}, wait_us{0}, copy_out_us{0}, total_us{0};
+};
+HostStats g_host_stats;
+
 // io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its kernels.
 // SLIME_RS_PIPE_TRACE=1 prints each call's split of host time to stderr.
 template <class Io, class Launch>
@@ -584,9 +591,18 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   };
   const int rc = body();
   if (rc) drain_stages(ws);
+  const double t_total = ms_since(t_start);
+  auto us = [](double ms) { return (uint64_t)(ms * 1e3 + 0.5); };
+  g_host_stats.calls.fetch_add(1, std::memory_order_relaxed);
+  g_host_stats.windows.fetch_add(n, std::memory_order_relaxed);
+  g_host_stats.copy_in_us.fetch_add(us(t_in), std::memory_order_relaxed);
+  g_host_stats.enqueue_us.fetch_add(us(t_enq), std::memory_order_relaxed);
+  g_host_stats.wait_us.fetch_add(us(t_wait), std::memory_order_relaxed);
+  g_host_stats.copy_out_us.fetch_add(us(t_out), std::memory_order_relaxed);
+  g_host_stats.total_us.fetch_add(us(t_total), std::memory_order_relaxed);
   if (trace)
     fprintf(stderr, "slime_rs %s windows=%llu copy_in=%.3f enqueue=%.3f wait=%.3f copy_out=%.3f total=%.3f ms\n", what,
-            (unsigned long long)n, t_in, t_enq, t_wait, t_out, ms_since(t_start));
+            (unsigned long long)n, t_in, t_enq, t_wait, t_out, t_total);
   return rc;
 }
 
@@ -1716,6 +1732,19 @@ int slime_rs_plan_cache_stats(slime_rs_cache_stats_t* st) {
 int slime_rs_plan_cache_capacity(uint64_t capacity) {
   if (capacity == 0) return fail(Status::InvalidArg, "plan_cache_capacity: must be >= 1");
   plans().set_capacity((size_t)capacity);
+  return 0;
+}
+
+int slime_rs_host_stats(slime_rs_host_stats_t* st, int reset) {
+  if (!st) return fail(Status::InvalidArg, "host_stats: null");
+  auto take = [&](std::atomic<uint64_t>& a) { return reset ? a.exchange(0) : a.load(); };
+  st->calls = take(g_host_stats.calls);
+  st->windows = take(g_host_stats.windows);
+  st->copy_in_us = take(g_host_stats.copy_in_us);
+  st->enqueue_us = take(g_host_stats.enqueue_us);
+  st->wait_us = take(g_host_stats.wait_us);
+  st->copy_out_us = take(g_host_stats.copy_out_us);
+  st->total_us = take(g_host_stats.total_us);
   return 0;
 }
 

@@ -271,6 +271,23 @@ extern "C" int av_launch_wide(int math, const uint32_t* in, uint32_t* out, uint6
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// The k <= 16 pipelined kernel instantiated for wider k (coefficient rows of
+// ceil(K/16) x 16 words): a candidate for 17 <= k <= 32 instead of the wide kernel.
+extern "C" int av_launch_pipek(int K, int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is,
+                               uint64_t oo, uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                               uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream,
+                               uint32_t nseg) {
+  hipStream_t s = (hipStream_t)stream;
+#define PK(KK, UU)                                                                                               \
+  if (K == KK && U == UU) {                                                                                      \
+    gp<KK, UU, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);          \
+    return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
+  }
+  PK(20, 1) PK(20, 2) PK(24, 1) PK(24, 2) PK(28, 1) PK(32, 1)
+#undef PK
+  return -2;
+}
+
 // Phased walk launch (k = 8, 4 rows): U in {3, 6}.
 extern "C" int av_launch_phased(int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                 uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,

@@ -54,6 +54,7 @@ def main():
                     help="re-allocate until the product encode runs in the given placement mode")
     ap.add_argument("--phased", type=str, default="",
                     help="time-phased walks U:period:rwin (100 MHz ticks), comma list, e.g. 3:700:460,6:1400:930")
+    ap.add_argument("--pipek", type=str, default="", help="k > 16 through the pipelined k-template kernel: U list")
     ap.add_argument("--wide", type=int, default=0, help="k > 16: time the wide kernel with field math (500) and XOR (501)")
     ap.add_argument("--batched", type=str, default="", help="register-batched stores: U list (2,3)")
     ap.add_argument("--burst", type=str, default="", help="LDS-staged write bursts: tiles per burst, comma list (1..3)")
@@ -74,10 +75,16 @@ def main():
         VARIANTS.clear()
         VARIANTS[500] = "wide pipe, field math (product)"
         VARIANTS[501] = "wide pipe, XOR stand-in (wrong by design)"
+    for u in (int(x) for x in args.pipek.split(",") if x):
+        VARIANTS[700 + u] = f"pipe K={args.need} U{u} (k-template kernel)"
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libapplyvar.so"))
+    lib.av_launch_pipek.restype = ctypes.c_int
+    lib.av_launch_pipek.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_void_p, ctypes.c_uint32]
     lib.av_launch_wide.restype = ctypes.c_int
     lib.av_launch_wide.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -172,6 +179,12 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
 
     def launch(v, gx, gy, nseg=1):
+        if 700 <= v < 800:
+            rc = lib.av_launch_pipek(need, v - 700, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
+                                     ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx, gy, ctypes.c_void_p(s.cuda_stream),
+                                     nseg)
+            assert rc == 0, rc
+            return
         if v in (500, 501):
             rc = lib.av_launch_wide(int(v == 500), buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                                     ii.data_ptr(), oi.data_ptr(), L, nobj, r, need, gx, gy,

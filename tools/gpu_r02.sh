@@ -76,6 +76,10 @@ for step in "$@"; do
     widemath) run wide_20_24 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --blocks 256,1024 &&
               run wide_32_40 300 python tools/apply_variants.py --need 32 --total 40 --nobj 32 --wide 1 --blocks 256,1024 &&
               run wide_64_80 300 python tools/apply_variants.py --need 64 --total 80 --nobj 16 --wide 1 --blocks 256,1024 ;;
+    pipek) run pipek_20_24 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 &&
+           run pipek_24_28 300 python tools/apply_variants.py --need 24 --total 28 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 &&
+           run pipek_32_40 300 python tools/apply_variants.py --need 32 --total 40 --nobj 32 --wide 1 --pipek 1 --blocks 256,512,1024 &&
+           run pipek_20_24_dec 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 --decode 1 ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
