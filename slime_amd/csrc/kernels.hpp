@@ -34,6 +34,18 @@ inline uint32_t coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 
+// Launch geometry of the apply kernels (rs_apply.hip): resident 256-lane
+// blocks per launch (0 = per-k default) and object segments in flight; env
+// overrides for the tuning harness only.
+struct ApplyGeometry {
+  uint64_t target, inflight;
+};
+const ApplyGeometry& apply_geometry();
+
+// 17 <= k <= 32, 16-byte-aligned-capable layouts, shards under 4 GiB: the
+// pipelined k-template kernel instantiated for wide k (rs_apply_k32.hip).
+hipError_t launch_pipe_k32(const ApplyLaunch& a, hipStream_t stream);
+
 // Kernel form for shards/chunks under 4 GiB: software-pipelined (default) or
 // not (the form larger ones always take).  Process-wide; see rs_apply.hip.
 bool pipelined_kernels();

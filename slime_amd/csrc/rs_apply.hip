@@ -57,11 +57,20 @@ constexpr int unroll_for() {
 constexpr bool kNtLoads = true;
 constexpr bool kNtStores = true;
 
-uint64_t env_u64(const char* name, uint64_t dflt) {
+}  // namespace
+
+static uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
   const long long v = e ? atoll(e) : 0;
   return v > 0 ? (uint64_t)v : dflt;
 }
+
+const ApplyGeometry& apply_geometry() {
+  static const ApplyGeometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
+  return g;
+}
+
+namespace {
 
 // Launch geometry: `target` resident 256-lane blocks (8 per CU at 2048 on 256
 // CUs), spread over at most `inflight` objects at a time.  The default block
@@ -69,13 +78,8 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 // of symbols per wave; fewer, fatter waves measured +5..18% at 10/14 and
 // +2% at 12/16 on 1 GiB objects, profiles/r01/gridk/).  Environment
 // overrides exist for the tuning harness only.
-struct Geometry {
-  uint64_t target, inflight;  // target 0: per-k default
-};
-const Geometry& geometry() {
-  static const Geometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
-  return g;
-}
+using Geometry = ApplyGeometry;
+const Geometry& geometry() { return apply_geometry(); }
 template <int K>
 constexpr uint64_t default_blocks() {
   return K >= 9 && K <= 12 ? 256 : 512;
@@ -211,6 +215,7 @@ hipError_t launch_wide_pipe(const ApplyLaunch& a, hipStream_t stream) {
 }
 
 hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
+  if (pipe_ok(a) && a.k <= 32) return launch_pipe_k32(a, stream);
   if (pipe_ok(a)) return a.rows <= 8 ? launch_wide_pipe<8>(a, stream) : launch_wide_pipe<16>(a, stream);
   return a.k <= 32 ? launch_wide_k<32, 8>(a, stream) : launch_wide_k<16, 16>(a, stream);
 }

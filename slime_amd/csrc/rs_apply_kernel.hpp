@@ -52,36 +52,6 @@ __device__ __forceinline__ void st16(uint32_t* p, uint4 r) {
     *reinterpret_cast<u32x4*>(p) = v;
 }
 
-// One column per lane (tails, unaligned layouts, generic k).
-template <int K>
-__device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, uint32_t* __restrict__ ob,
-                                             const uint32_t* __restrict__ coeff,
-                                             const uint32_t* __restrict__ in_idx, uint64_t in_shard,
-                                             const uint32_t* __restrict__ out_idx, uint64_t out_shard,
-                                             uint32_t rows, uint32_t k, uint64_t b) {
-  if constexpr (K > 0) {
-    uint32_t x[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = ib[(uint64_t)in_idx[j] * in_shard + b];
-    for (uint32_t i = 0; i < rows; ++i) {
-      const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
-      uint64_t lo = 0;
-      uint32_t hi = 0;
-#pragma unroll
-      for (int j = 0; j < K; ++j) mac(lo, hi, x[j], c[j]);
-      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
-    }
-  } else {
-    for (uint32_t i = 0; i < rows; ++i) {
-      const uint32_t* c = coeff + (uint64_t)i * wide_coeff_stride(k);
-      uint64_t lo = 0;
-      uint32_t hi = 0;
-      for (uint32_t j = 0; j < k; ++j) mac(lo, hi, ib[(uint64_t)in_idx[j] * in_shard + b], c[j]);
-      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
-    }
-  }
-}
-
 // Coefficient row of a compile-time-K kernel: ceil(K/16) s_load_dwordx16 of
 // a row padded to a multiple of 16 words (the plan table's row stride,
 // coeff_stride(k)); K <= 16 is one load at stride kCoeffStride.
@@ -99,6 +69,36 @@ __device__ __forceinline__ CoeffRow<K> load_coeff_row(const uint32_t* __restrict
   for (int q = 0; q < CoeffRow<K>::kVecs; ++q)
     r.v[q] = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * CoeffRow<K>::kStride + 16 * q);
   return r;
+}
+
+// One column per lane (tails, unaligned layouts, generic k).
+template <int K>
+__device__ __forceinline__ void apply_column(const uint32_t* __restrict__ ib, uint32_t* __restrict__ ob,
+                                             const uint32_t* __restrict__ coeff,
+                                             const uint32_t* __restrict__ in_idx, uint64_t in_shard,
+                                             const uint32_t* __restrict__ out_idx, uint64_t out_shard,
+                                             uint32_t rows, uint32_t k, uint64_t b) {
+  if constexpr (K > 0) {
+    uint32_t x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ib[(uint64_t)in_idx[j] * in_shard + b];
+    for (uint32_t i = 0; i < rows; ++i) {
+      const CoeffRow<K> c = load_coeff_row<K>(coeff, i);
+      uint64_t lo = 0;
+      uint32_t hi = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) mac(lo, hi, x[j], c[j]);
+      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
+    }
+  } else {
+    for (uint32_t i = 0; i < rows; ++i) {
+      const uint32_t* c = coeff + (uint64_t)i * wide_coeff_stride(k);
+      uint64_t lo = 0;
+      uint32_t hi = 0;
+      for (uint32_t j = 0; j < k; ++j) mac(lo, hi, ib[(uint64_t)in_idx[j] * in_shard + b], c[j]);
+      ob[(uint64_t)out_idx[i] * out_shard + b] = fold96(lo, hi);
+    }
+  }
 }
 
 // One output row over 4 columns (C: a u32x16 for K <= 16, or a CoeffRow<K>).

@@ -944,3 +944,36 @@ def test_concurrent_host_callers_match_oracle():
     assert not errors, errors[:5]
     st = N.plan_cache_stats()
     assert st["live"] <= 256
+
+
+@pytest.mark.parametrize("need", list(range(17, 33)))
+def test_k17_to_32_pipelined_kernel_vs_oracle(torch_dev, need):
+    """17 <= k <= 32 runs the k-template pipelined kernel (rs_apply_k32.hip):
+    every k, non-canonical inputs (x >= p, 0xFFFFFFFF), a column tail past the
+    last 16-byte vector, 1..r output rows, encode in place and a reconstruct of
+    data and parity rows into a separate buffer."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(need)
+    r = 1 + need % 5
+    total, nobj = need + r, 2
+    L = 4 * 1024 + 1 + need % 3  # tail columns
+    h = np.stack([np.stack(rand_vecs(rng, total, L)) for _ in range(nobj)])  # [obj][shard][L]
+    buf = torch.from_numpy(h.reshape(-1).view(np.int32).copy()).cuda()
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+    for o in range(nobj):
+        ref = np.ascontiguousarray(h[o].copy())
+        OC.encode_object(ref, need, total)
+        assert np.array_equal(got[o], ref), o
+    erase = sorted(rng.choice(total, size=r, replace=False).tolist())
+    have = [i for i in range(total) if i not in erase][:need]
+    out = torch.zeros(nobj * r * L, dtype=torch.int32, device="cuda")
+    D.Plan.reconstruct(need, total, have, erase)(buf, lay, out, D.layout_of(r, L), L, nobj)
+    torch.cuda.synchronize()
+    rec = out.cpu().numpy().view(np.uint32).reshape(nobj, r, L)
+    for o in range(nobj):
+        for i, t in enumerate(erase):
+            assert np.array_equal(rec[o, i], got[o, t]), (o, t)

@@ -80,6 +80,7 @@ for step in "$@"; do
            run pipek_24_28 300 python tools/apply_variants.py --need 24 --total 28 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 &&
            run pipek_32_40 300 python tools/apply_variants.py --need 32 --total 40 --nobj 32 --wide 1 --pipek 1 --blocks 256,512,1024 &&
            run pipek_20_24_dec 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 --decode 1 ;;
+    pipekcheck) run pipek_check 300 python tools/pipek_check.py ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
