@@ -45,6 +45,9 @@ const ApplyGeometry& apply_geometry();
 // 17 <= k <= 32, 16-byte-aligned-capable layouts, shards under 4 GiB: the
 // pipelined k-template kernel instantiated for wide k (rs_apply_k32.hip).
 hipError_t launch_pipe_k32(const ApplyLaunch& a, hipStream_t stream);
+// Whether 17 <= k <= 32 take the k-template kernels (default) or the wide
+// 16-shard chunk kernels (env SLIME_RS_K32=0, read once: tuning A/B).
+bool k32_kernels();
 
 // Kernel form for shards/chunks under 4 GiB: software-pipelined (default) or
 // not (the form larger ones always take).  Process-wide; see rs_apply.hip.
@@ -78,6 +81,21 @@ struct BytesLaunch {
   uint64_t ncols = 0;  // 0: the whole chunk (L columns)
 };
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
+// 17 <= need <= 32 through the pipelined k-template byte kernels (rs_bytes_k32.hip).
+hipError_t launch_encode_bytes_k32(const BytesLaunch& a, hipStream_t stream);
+hipError_t launch_decode_bytes_k32(const BytesLaunch& a, hipStream_t stream);
+
+// Byte-kernel grid: about `target` resident 256-lane blocks over `work` object
+// segments of ncols/nseg columns, U 16-byte units per lane per step.
+inline dim3 bytes_grid(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t target = 512, int U = 1) {
+  uint64_t gy = work < 65535u ? work : 65535u;
+  if (gy < 1) gy = 1;
+  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t need = (ncols / nseg + 4ull * 256 * U - 1) / (4ull * 256 * U);
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  return dim3((uint32_t)gx, (uint32_t)gy);
+}
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t stream);
 

@@ -65,6 +65,14 @@ static uint64_t env_u64(const char* name, uint64_t dflt) {
   return v > 0 ? (uint64_t)v : dflt;
 }
 
+bool k32_kernels() {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_K32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 const ApplyGeometry& apply_geometry() {
   static const ApplyGeometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
   return g;
@@ -215,7 +223,7 @@ hipError_t launch_wide_pipe(const ApplyLaunch& a, hipStream_t stream) {
 }
 
 hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
-  if (pipe_ok(a) && a.k <= 32) return launch_pipe_k32(a, stream);
+  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_pipe_k32(a, stream);
   if (pipe_ok(a)) return a.rows <= 8 ? launch_wide_pipe<8>(a, stream) : launch_wide_pipe<16>(a, stream);
   return a.k <= 32 ? launch_wide_k<32, 8>(a, stream) : launch_wide_k<16, 16>(a, stream);
 }

@@ -6,6 +6,20 @@
 #include "rs_bytes_kernel.hpp"
 
 namespace slime {
+namespace bytes {
+// flags -> MapToGF's choice (map.go:35-62): 0 if no word >= p, else 1<<31 if
+// that fits, else the random fallback: status 1, resolved on the host.
+// `status` holds the flags on entry (in place: each lane owns one object).
+__global__ void select_mapping_kernel(uint32_t* __restrict__ mapping, uint32_t* __restrict__ status, uint32_t nobj) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= nobj) return;
+  const uint32_t f = status[o];
+  const bool zero_ok = !(f & 1u), high_ok = !(f & 2u);
+  mapping[o] = zero_ok ? 0u : (high_ok ? 0x80000000u : 0u);
+  status[o] = (!zero_ok && !high_ok) ? 1u : 0u;
+}
+}  // namespace bytes
+
 namespace {
 
 using apply::kBlock;
@@ -21,13 +35,7 @@ constexpr int bytes_unroll() {
 // `target` resident blocks (default 512) over `work` object segments of about
 // ncols/nseg columns, U units of 4 columns per lane per step.
 dim3 grid_for(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t target = 512, int U = 1) {
-  uint64_t gy = work < 65535u ? work : 65535u;
-  if (gy < 1) gy = 1;
-  uint64_t gx = (target + gy - 1) / gy;
-  const uint64_t need = (ncols / nseg + 4ull * kBlock * U - 1) / (4ull * kBlock * U);
-  if (gx > need) gx = need;
-  if (gx < 1) gx = 1;
-  return dim3((uint32_t)gx, (uint32_t)gy);
+  return bytes_grid(ncols, work, nseg, target, U);
 }
 
 // Software-pipelined forms (rs_bytes_kernel.hpp), the product for need <= 16
@@ -177,10 +185,12 @@ hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
 }
 
 hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_encode_bytes_k32(a, s);
   if (pipe_ok(a)) return a.rows <= 8 ? enc_wide_pipe<8>(a, s) : enc_wide_pipe<16>(a, s);
   return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s);
 }
 hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
+  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_decode_bytes_k32(a, s);
   if (pipe_ok(a)) return a.rows <= 8 ? dec_wide_pipe<8>(a, s) : dec_wide_pipe<16>(a, s);
   return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s);
 }

@@ -60,7 +60,7 @@ __device__ __forceinline__ void rows_out(const uint32_t (&x)[K][4], uint32_t row
                                          const uint32_t* __restrict__ out_idx, uint8_t* out_slot, uint64_t chunk,
                                          uint64_t byte_off, uint32_t m, int ncol) {
   for (uint32_t i = 0; i < rows; ++i) {
-    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    const apply::CoeffRow<K> c = apply::load_coeff_row<K>(coeff, i);
     uint64_t lo0 = 0, lo1 = 0, lo2 = 0, lo3 = 0;
     uint32_t hi0 = 0, hi1 = 0, hi2 = 0, hi3 = 0;
 #pragma unroll
@@ -85,7 +85,7 @@ __device__ __forceinline__ void rows_out_units(const uint32_t (&x)[U][K][4], int
                                                const uint32_t* __restrict__ out_idx, uint8_t* out_slot,
                                                uint64_t chunk, uint64_t g0, uint32_t m) {
   for (uint32_t i = 0; i < rows; ++i) {
-    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    const apply::CoeffRow<K> c = apply::load_coeff_row<K>(coeff, i);
     uint8_t* const orow = out_slot + (uint64_t)out_idx[i] * chunk;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -299,17 +299,6 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
   }
 }
 
-// flags -> MapToGF's choice (map.go:35-62): 0 if no word >= p, else 1<<31 if
-// that fits, else the random fallback: status 1, resolved on the host.
-// `status` holds the flags on entry (in place: each lane owns one object).
-__global__ void select_mapping_kernel(uint32_t* __restrict__ mapping, uint32_t* __restrict__ status, uint32_t nobj) {
-  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= nobj) return;
-  const uint32_t f = status[o];
-  const bool zero_ok = !(f & 1u), high_ok = !(f & 2u);
-  mapping[o] = zero_ok ? 0u : (high_ok ? 0x80000000u : 0u);
-  status[o] = (!zero_ok && !high_ok) ? 1u : 0u;
-}
 
 // Decode: rebuild `rows` chunks (out_idx slots) from need survivors (in_idx).
 template <int K>
@@ -400,7 +389,7 @@ __device__ __forceinline__ void rows_tile(const uint4 (&x)[U][K], uint32_t rows,
                                           const uint32_t* __restrict__ out_idx, uint8_t* base, uint64_t chunk,
                                           uint32_t g0, uint32_t v1, uint32_t m) {
   for (uint32_t i = 0; i < rows; ++i) {
-    const u32x16 c = *reinterpret_cast<const u32x16*>(coeff + (uint64_t)i * kCoeffStride);
+    const apply::CoeffRow<K> c = apply::load_coeff_row<K>(coeff, i);
     uint8_t* const orow = base + (uint64_t)out_idx[i] * chunk;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
