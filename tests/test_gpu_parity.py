@@ -979,3 +979,40 @@ def test_k17_to_32_pipelined_kernel_vs_oracle(torch_dev, need):
             # RecoverData returns canonical residues: a non-canonical data symbol x comes back as x mod p
             want = (got[o, t].astype(np.uint64) % P).astype(np.uint32)
             assert np.array_equal(rec[o, i], want), (o, t)
+
+
+@pytest.mark.parametrize("need,total", [(17, 18), (19, 24), (24, 30), (27, 32), (31, 36), (32, 40)])
+@pytest.mark.parametrize("S", [33, 65537, (1 << 20) + 7])
+def test_k17_to_32_byte_kernels_vs_oracle(torch_dev, kernel_form, need, total, S):
+    """17 <= need <= 32 byte kernels (rs_bytes_k32.hip in the pipelined form):
+    encode_objects against the oracle's writeChunks framing (mappings 0 and
+    1<<31), then repair of erased data and parity chunks in place."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(S + need)
+    objs = [rng.integers(0, 256, size=S, dtype=np.uint8).tobytes() for _ in range(2)]
+    b = bytearray(objs[1]); b[0:4] = b"\xff\xff\xff\xfd"; objs[1] = bytes(b)  # mapping 1<<31
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total, extra=8)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(2, dtype=torch.int32, device="cuda")
+    status = torch.empty(2, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 2, mapping, status)
+    torch.cuda.synchronize()
+    assert status.cpu().numpy().tolist() == [0, 0]
+    h = slots.cpu().numpy()
+    ms = mapping.cpu().numpy().view(np.uint32)
+    for o, obj in enumerate(objs):
+        m, chunks = _oracle_chunks(obj, need, total)
+        assert ms[o] == m
+        for c in range(total):
+            assert h[o * stride + c * chunk: o * stride + (c + 1) * chunk].tobytes() == chunks[c], (o, c)
+    truth = slots.clone()
+    r = total - need
+    erase = sorted(set([0, need - 1] + list(range(need, total))[:max(0, r - 2)]))[:r]
+    have = [i for i in range(total) if i not in erase][:need]
+    rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+    v = slots.view(2, stride)[:, : total * chunk].view(2, total, chunk)
+    v[:, erase, :] = 0x5A
+    D.decode_objects(rec, slots, stride, L, 2, mapping)
+    torch.cuda.synchronize()
+    assert torch.equal(slots, truth), erase

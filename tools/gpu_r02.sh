@@ -81,6 +81,10 @@ for step in "$@"; do
            run pipek_32_40 300 python tools/apply_variants.py --need 32 --total 40 --nobj 32 --wide 1 --pipek 1 --blocks 256,512,1024 &&
            run pipek_20_24_dec 300 python tools/apply_variants.py --need 20 --total 24 --nobj 32 --wide 1 --pipek 1,2 --blocks 256,512,1024 --decode 1 ;;
     pipekcheck) run pipek_check 300 python tools/pipek_check.py ;;
+    k32ab) for kn in "20 24 32" "24 28 32" "32 40 32" "17 20 32"; do set -- $kn
+             run k32_${1}_${2} 200 python bench.py --need $1 --total $2 --objects $3 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 &&
+             run k32off_${1}_${2} 200 env SLIME_RS_K32=0 python bench.py --need $1 --total $2 --objects $3 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 || exit $?
+           done ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
