@@ -423,6 +423,9 @@ def main():
     need, total = args.need, args.total
     r = total - need
     erase = [int(x) for x in args.erase.split(",") if x != ""]
+    if not erase or len(erase) > r or len(set(erase)) != len(erase) or not all(0 <= e < total for e in erase):
+        print(f"bench.py: --erase needs 1..{r} distinct shard indices below total={total}", file=sys.stderr)
+        sys.exit(2)
     have = [i for i in range(total) if i not in erase][:need]
     S = args.object_mib << 20
     L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) symbols (multi_store.go:272)

@@ -55,6 +55,11 @@ class Plan:
 
     @classmethod
     def reconstruct(cls, need: int, total: int, have: Sequence[int], want: Sequence[int], device: int = 0) -> "Plan":
+        # The C entry point reads exactly `need` survivor indices.
+        if len(have) != need:
+            raise ValueError(f"reconstruct needs exactly need={need} surviving shard indices, got {len(have)}")
+        if not want:
+            raise ValueError("reconstruct needs at least one output row")
         h = ctypes.c_void_p()
         hv = (ctypes.c_int * len(have))(*have)
         wv = (ctypes.c_int * len(want))(*want)

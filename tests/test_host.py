@@ -319,3 +319,24 @@ def test_go_shim_keeps_the_reference_api_and_binds_the_header():
     shim = "".join(open(os.path.join(ROOT, p)).read() for p in GO_API)
     for name in EX_BOUND:
         assert f"C.{name}_ex(" in shim, name
+
+
+def test_reconstruct_plan_checks_survivor_count_before_the_c_call():
+    """The C entry point reads exactly `need` survivor indices; the Python
+    binding refuses a shorter or longer list instead of letting C read past it."""
+    from slime_amd import device as D
+    with pytest.raises(ValueError):
+        D.Plan.reconstruct(17, 20, list(range(4, 20)), [0, 1, 2, 3])  # 16 survivors for need 17
+    with pytest.raises(ValueError):
+        D.Plan.reconstruct(4, 6, [0, 1, 2, 3, 4], [5])
+    with pytest.raises(ValueError):
+        D.Plan.reconstruct(4, 6, [0, 1, 2, 3], [])
+
+
+def test_bench_rejects_impossible_erasures():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--need", "17", "--total", "20",
+                        "--erase", "0,1,2,3"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2
