@@ -283,7 +283,7 @@ extern "C" int av_launch_pipek(int K, int U, const uint32_t* in, uint32_t* out, 
     gp<KK, UU, true, true>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, gx, gy, s, nseg);          \
     return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
-  PK(20, 1) PK(20, 2) PK(24, 1) PK(24, 2) PK(28, 1) PK(32, 1)
+  PK(20, 1) PK(20, 2) PK(24, 1) PK(24, 2) PK(28, 1) PK(32, 1) PK(40, 1) PK(48, 1)
 #undef PK
   return -2;
 }

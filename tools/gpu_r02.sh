@@ -85,6 +85,12 @@ for step in "$@"; do
              run k32_${1}_${2} 200 python bench.py --need $1 --total $2 --objects $3 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 &&
              run k32off_${1}_${2} 200 env SLIME_RS_K32=0 python bench.py --need $1 --total $2 --objects $3 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 || exit $?
            done ;;
+    pipek48) run pipek_40_48 300 python tools/apply_variants.py --need 40 --total 48 --nobj 16 --wide 1 --pipek 1 --blocks 256,512,1024 &&
+             run pipek_48_56 300 python tools/apply_variants.py --need 48 --total 56 --nobj 16 --wide 1 --pipek 1 --blocks 256,512,1024 ;;
+    c5sweep) for g in 256 512; do for sg in 16 32 64; do
+               run c5_g${g}_s${sg} 200 env SLIME_RS_GRID_TARGET=$g SLIME_RS_SEGMENTS=$sg python bench.py --need 10 --total 14 \
+                 --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 10 || exit $?
+             done; done ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
