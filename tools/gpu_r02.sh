@@ -91,6 +91,12 @@ for step in "$@"; do
                run c5_g${g}_s${sg} 200 env SLIME_RS_GRID_TARGET=$g SLIME_RS_SEGMENTS=$sg python bench.py --need 10 --total 14 \
                  --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 10 || exit $?
              done; done ;;
+    slowcheck) (timeout 20 amd-smi metric --usage --mem-usage > "$OUT/smi_before.txt" 2>&1 || true)
+               run sc_bench1 300 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 &&
+               (timeout 20 amd-smi metric --usage --mem-usage > "$OUT/smi_mid.txt" 2>&1 || true) &&
+               for i in 1 2 3 4 5 6; do echo "sleep $i/6" | tee -a "$OUT/session.log"; sleep 20; done &&
+               run sc_bench2 300 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 &&
+               run sc_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 ;;
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
