@@ -309,6 +309,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     par2 = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
+    digests = digest_leg(data, need, total, chunks, have, out, med, g)
     return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "link": link_probe(obj_mib),
             "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
                                "what": "mean per call: host copies in/out, launches, waits on the device/link side "
@@ -320,9 +321,42 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
                 "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF "
                         f"(write); {need} x MapToGFWith + RecoverData + {need} x MapFromGF (read); each call "
                         "host->GPU->host"},
+            "digests": digests,
             "object_mib": obj_mib, "erased": erase, "verified": ok,
             "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
                     "PCIe-inclusive; not `value`"}
+
+
+def digest_leg(data, need, total, chunks, have, out, med, g) -> dict:
+    """Chunk digests on the write path (store.DataV per chunk, multi_store.go:554-556)
+    and the object verify on the read path (:244-249), host threads."""
+    import hashlib
+    from slime_amd import _native as N
+    from slime_amd import objects
+    sha_ext, threads = N.digest_info()
+    box = {}
+    t_fused = med(lambda: box.update(r=objects.write_chunks_digest(data, need, total, out=chunks)))
+    m, _, shas, _ = box["r"]
+    t_seq = med(lambda: (objects.write_chunks(data, need, total, out=chunks), objects.chunk_digests(chunks)))
+    t_dig = med(lambda: objects.chunk_digests(chunks))
+    t_hdr = med(lambda: objects.chunk_digests(chunks, headers=True))
+    one = chunks[0]
+    t_one = med(lambda: objects.sha256(one))
+    want = hashlib.sha256(data.tobytes()).digest()
+    surv = [chunks[i] for i in have]
+    t_rv = med(lambda: objects.reconstruct(surv, have, m, data.size, out=out, sha=want))
+    t_obj = med(lambda: objects.sha256(out))
+    ok = shas == [hashlib.sha256(c.tobytes()).digest() for c in chunks] and bytes(out) == data.tobytes()
+    chunk_bytes = sum(c.size for c in chunks)
+    return {"write_chunks_digest_gibs": g(t_fused), "write_chunks_then_digests_gibs": g(t_seq),
+            "chunk_sha256_gbs": round(chunk_bytes / t_dig / 1e9, 2),
+            "chunk_sha256_fnv_header_gbs": round(chunk_bytes / t_hdr / 1e9, 2),
+            "sha256_one_thread_gbs": round(one.size / t_one / 1e9, 2),
+            "reconstruct_verify_gibs": g(t_rv), "object_sha256_gbs": round(data.size / t_obj / 1e9, 2),
+            "sha_extensions": sha_ext, "digest_threads": threads + 1, "verified": bool(ok),
+            "what": f"write_chunks_digest hashes the {total} chunks while the device pipeline runs (object GiB/s); "
+                    "the sequential form is write_chunks then chunk_digests; verify = reconstruct + the object's "
+                    "SHA-256 (one message, one thread)"}
 
 
 def link_probe(mib: int) -> dict:

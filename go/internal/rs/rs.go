@@ -21,6 +21,7 @@ package rs
 import "C"
 
 import (
+	"errors"
 	"fmt"
 	"runtime"
 	"sync"
@@ -355,3 +356,90 @@ func ReconstructObject(chunks [][]byte, indices []int, mapping uint32, size int)
 	k.raise(C.slime_rs_reconstruct_ex(k.c, ptrs, idx, C.int(n), C.uint64_t(cb), C.uint32_t(mapping), C.uint64_t(size), op))
 	return out
 }
+
+// WriteChunksDigest is WriteChunks plus every chunk's SHA-256: the value each
+// of writeChunks' per-chunk goroutines computes with store.DataV
+// (internal/store/store.go:104-110, multi_store.go:554-556), hashed by
+// libslime_rs on its host threads while the GPU pipeline still runs.  A
+// caller builds store.CASV{Present: true, SHA256: sums[i], Data: chunks[i]}
+// instead of calling store.DataV.
+func WriteChunksDigest(data []byte, need, total int) (uint32, [][]byte, [][32]byte) {
+	cb := int(C.slime_rs_chunk_size(C.uint64_t(len(data)), C.int(need)))
+	chunks := make([][]byte, total)
+	sums := make([][32]byte, total+1)
+	ptrs := (**C.uint8_t)(C.calloc(C.size_t(total+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
+	defer C.free(unsafe.Pointer(ptrs))
+	ps := unsafe.Slice(ptrs, total+1)
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for i := range chunks {
+		chunks[i] = make([]byte, cb)
+		if cb > 0 {
+			pinner.Pin(&chunks[i][0])
+			ps[i] = (*C.uint8_t)(unsafe.Pointer(&chunks[i][0]))
+		}
+	}
+	var in *C.uint8_t
+	if len(data) > 0 {
+		pinner.Pin(&data[0])
+		in = (*C.uint8_t)(unsafe.Pointer(&data[0]))
+	}
+	pinner.Pin(&sums[0])
+	var mapping C.uint32_t
+	k := newCall()
+	defer k.free()
+	k.raise(C.slime_rs_write_chunks_digest_ex(k.c, in, C.uint64_t(len(data)), C.int(need), C.int(total), ptrs, &mapping,
+		(*C.uint8_t)(unsafe.Pointer(&sums[0][0])), nil))
+	return uint32(mapping), chunks, sums[:total]
+}
+
+// ErrBadHash mirrors multi's ErrBadHash (multi_store.go:26).
+var ErrBadHash = errors.New("bad checksum after reconstruction")
+
+// ReconstructObjectVerified is ReconstructObject followed by reconstruct's
+// verify step (multi_store.go:244-249): the rebuilt object's SHA-256 must
+// equal sum (meta.File.SHA256), else ErrBadHash.
+func ReconstructObjectVerified(chunks [][]byte, indices []int, mapping uint32, size int, sum [32]byte) ([]byte, error) {
+	n := len(chunks)
+	if n != len(indices) {
+		panic("RecoverData: len(chunks) != len(indices)")
+	}
+	cb := 0
+	if n > 0 {
+		cb = len(chunks[0])
+	}
+	ptrs := (**C.uint8_t)(C.calloc(C.size_t(n+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
+	defer C.free(unsafe.Pointer(ptrs))
+	idx := (*C.int)(C.calloc(C.size_t(n+1), C.size_t(unsafe.Sizeof(C.int(0)))))
+	defer C.free(unsafe.Pointer(idx))
+	ps, is := unsafe.Slice(ptrs, n+1), unsafe.Slice(idx, n+1)
+	var pinner runtime.Pinner
+	defer pinner.Unpin()
+	for i, c := range chunks {
+		if len(c) < cb {
+			panic(fmt.Sprintf("runtime error: index out of range [%d] with length %d", len(c), len(c)))
+		}
+		if cb > 0 {
+			pinner.Pin(&c[0])
+			ps[i] = (*C.uint8_t)(unsafe.Pointer(&c[0]))
+		}
+		is[i] = C.int(indices[i])
+	}
+	out := make([]byte, size, size+16)
+	var op *C.uint8_t
+	if size > 0 {
+		pinner.Pin(&out[0])
+		op = (*C.uint8_t)(unsafe.Pointer(&out[0]))
+	}
+	pinner.Pin(&sum)
+	k := newCall()
+	defer k.free()
+	rc := C.slime_rs_reconstruct_verify_ex(k.c, ptrs, idx, C.int(n), C.uint64_t(cb), C.uint32_t(mapping), C.uint64_t(size),
+		op, (*C.uint8_t)(unsafe.Pointer(&sum[0])))
+	if rc == C.SLIME_RS_ERR_BAD_HASH {
+		return nil, ErrBadHash
+	}
+	k.raise(rc)
+	return out, nil
+}
+

@@ -45,7 +45,8 @@ enum slime_rs_status {
   SLIME_RS_ERR_INVALID_ARG = 9,    /* C-ABI misuse (null pointer, bad shape)                  */
   SLIME_RS_ERR_NO_DEVICE = 10,     /* no usable HIP device: compute calls fail loudly         */
   SLIME_RS_ERR_HIP = 11,           /* HIP runtime error (detail in slime_rs_last_error())     */
-  SLIME_RS_ERR_MAPPING_FALLBACK = 12 /* no candidate mapping fits (only with a bounded search) */
+  SLIME_RS_ERR_MAPPING_FALLBACK = 12, /* no candidate mapping fits (only with a bounded search) */
+  SLIME_RS_ERR_BAD_HASH = 13       /* "bad checksum after reconstruction" (ErrBadHash) multi_store.go:26,244-249 */
 };
 
 /* Reference panic message (codes 1..8) or a short description. Static storage. */
@@ -317,6 +318,50 @@ typedef struct slime_rs_host_stats {
 int slime_rs_host_stats(slime_rs_host_stats_t *stats, int reset);
 /* Host calls the device pool has routed to `device` so far and calls in flight there. */
 int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
+
+/* ==== chunk and object digests ======================
+ * Host computations on the library's digest threads (DESIGN.md "Chunk
+ * digests"): SHA-256 and FNV-1a are sequential per message, so one x86 core
+ * with the SHA extensions outruns a GPU lane ~100x; what the library adds is
+ * hashing writeChunks' chunks while its device pipeline still runs. */
+
+/* SHA-256 of len bytes (sha256.Sum256 as store.DataV uses it,
+ * internal/store/store.go:104-110, and reconstruct's verify, multi_store.go:244). */
+int slime_rs_sha256(const uint8_t *data, uint64_t len, uint8_t *out /* 32 bytes */);
+
+/* For each of n chunks (lens[i] bytes): sha[32i..] = SHA-256 of the chunk
+ * (store.DataV per chunk, multi_store.go:554-556) and, if hdr != NULL,
+ * hdr[8i..] = the chunk file's header hash: FNV-1a-64 over SHA-256 ‖ chunk,
+ * big-endian as hash.Sum appends it (storedir/directory.go:25-28,548-553).
+ * Chunks are hashed in parallel, one per digest thread. */
+int slime_rs_chunk_digests(const uint8_t *const *chunks, const uint64_t *lens, uint32_t n, uint8_t *sha,
+                           uint8_t *hdr);
+
+/* slime_rs_write_chunks plus every chunk's digests as slime_rs_chunk_digests
+ * gives them (sha: total x 32 bytes; hdr optional, total x 8), computed while
+ * the device pipeline runs: data chunks are hashed from `data` at once and
+ * finished when the mapping is known, parity chunks as their windows land in
+ * the caller's buffers.  Replaces writeChunks' per-chunk goroutines'
+ * MapFromGF + store.DataV (multi_store.go:552-557). */
+int slime_rs_write_chunks_digest(const uint8_t *data, uint64_t size, int need, int total, uint8_t *const *chunks,
+                                 uint32_t *mapping, uint8_t *sha, uint8_t *hdr);
+
+/* slime_rs_reconstruct, then the object's SHA-256 against want_sha (the
+ * file's SHA256, multi_store.go:244-249): SLIME_RS_ERR_BAD_HASH on mismatch
+ * (out holds the rebuilt bytes either way). */
+int slime_rs_reconstruct_verify(const uint8_t *const *chunks, const int *indices, int need, uint64_t chunk_bytes,
+                                uint32_t mapping, uint64_t size, uint8_t *out, const uint8_t *want_sha);
+
+/* Whether SHA-256 runs on the CPU's SHA extensions, and the digest threads
+ * besides the caller (env SLIME_RS_DIGEST_THREADS). */
+int slime_rs_digest_info(int *sha_extensions, int *threads);
+
+int slime_rs_write_chunks_digest_ex(const slime_rs_call_t *call, const uint8_t *data, uint64_t size, int need,
+                                    int total, uint8_t *const *chunks, uint32_t *mapping, uint8_t *sha,
+                                    uint8_t *hdr);
+int slime_rs_reconstruct_verify_ex(const slime_rs_call_t *call, const uint8_t *const *chunks, const int *indices,
+                                   int need, uint64_t chunk_bytes, uint32_t mapping, uint64_t size, uint8_t *out,
+                                   const uint8_t *want_sha);
 
 #ifdef __cplusplus
 }

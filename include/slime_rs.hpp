@@ -12,6 +12,7 @@
 #ifndef SLIME_RS_HPP
 #define SLIME_RS_HPP
 
+#include <array>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -265,6 +266,46 @@ inline std::vector<uint8_t> ReconstructObject(const std::vector<std::vector<uint
                                             chunks.empty() ? 0 : chunks[0].size(), mapping, size,
                                             out.empty() ? nullptr : out.data()));
   return out;
+}
+
+// WriteChunks plus each chunk's SHA-256 (store.DataV per chunk,
+// multi_store.go:554-556), hashed while the device pipeline runs.  Additive.
+struct WrittenChunks {
+  uint32_t mapping = 0;
+  std::vector<std::vector<uint8_t>> chunks;
+  std::vector<std::array<uint8_t, 32>> sha256;
+};
+inline WrittenChunks WriteChunksDigest(const std::vector<uint8_t>& data, int need, int total) {
+  WrittenChunks w;
+  const uint64_t cb = slime_rs_chunk_size(data.size(), need);
+  w.chunks.assign(total > 0 ? (size_t)total : 0, std::vector<uint8_t>(cb));
+  w.sha256.resize(w.chunks.size());
+  std::vector<uint8_t*> ptrs;
+  for (auto& c : w.chunks) ptrs.push_back(c.data());
+  std::vector<uint8_t> sha(32 * (w.chunks.size() + 1));
+  slime::detail::Call k;
+  k.check(slime_rs_write_chunks_digest_ex(k.ptr(), data.empty() ? nullptr : data.data(), data.size(), need, total,
+                                          ptrs.empty() ? nullptr : ptrs.data(), &w.mapping, sha.data(), nullptr));
+  for (size_t i = 0; i < w.chunks.size(); ++i) std::copy(sha.begin() + 32 * i, sha.begin() + 32 * i + 32, w.sha256[i].begin());
+  return w;
+}
+
+// ReconstructObject followed by reconstruct's verify (multi_store.go:244-249):
+// false (ErrBadHash) when the rebuilt object's SHA-256 is not `sha256`.
+inline bool ReconstructObjectVerified(const std::vector<std::vector<uint8_t>>& chunks, const std::vector<int>& indices,
+                                      uint32_t mapping, uint64_t size, const std::array<uint8_t, 32>& sha256,
+                                      std::vector<uint8_t>* out) {
+  std::vector<const uint8_t*> ptrs;
+  for (const auto& c : chunks) ptrs.push_back(c.data());
+  out->assign(size, 0);
+  slime::detail::Call k;
+  const int rc = slime_rs_reconstruct_verify_ex(k.ptr(), ptrs.empty() ? nullptr : ptrs.data(),
+                                                indices.empty() ? nullptr : indices.data(), (int)chunks.size(),
+                                                chunks.empty() ? 0 : chunks[0].size(), mapping, size,
+                                                out->empty() ? nullptr : out->data(), sha256.data());
+  if (rc == SLIME_RS_ERR_BAD_HASH) return false;
+  k.check(rc);
+  return true;
 }
 
 }  // namespace rs

@@ -36,6 +36,7 @@ def _load():
         "oracle_map_from_gf": (None, [ctypes.c_uint32, V, ctypes.c_uint64, V]),
         "oracle_split_vector": (ctypes.c_uint64, [V, ctypes.c_uint64, ctypes.c_int, V]),
         "oracle_encode_object": (ctypes.c_int, [V, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]),
+        "oracle_fnv1a64": (ctypes.c_uint64, [ctypes.c_uint64, V, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -136,3 +137,24 @@ def encode_object(shards: np.ndarray, need: int, total: int) -> None:
     assert shards.flags.c_contiguous and shards.dtype == np.uint32
     rc = lib.oracle_encode_object(shards.ctypes.data, need, total, shards.shape[1])
     assert rc == 0, rc
+
+
+FNV64_OFFSET = 14695981039346656037
+
+
+def fnv1a64(data, h: int = FNV64_OFFSET) -> int:
+    """Go hash/fnv New64a over `data` continuing from h (oracle_fnv1a64)."""
+    b = np.frombuffer(memoryview(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else \
+        np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return int(lib.oracle_fnv1a64(h, b.ctypes.data if b.size else None, b.size))
+
+
+def chunk_digests(chunk) -> tuple[bytes, bytes]:
+    """(SHA-256, chunk-file header) of one chunk as writeChunks and storedir
+    produce them: store.DataV's sha256.Sum256 (internal/store/store.go:104-110;
+    Python's hashlib, an independent SHA-256) and FNV-1a-64 over SHA-256 ‖ data,
+    big-endian (storedir/directory.go:548-553)."""
+    import hashlib
+    raw = chunk.tobytes() if isinstance(chunk, np.ndarray) else bytes(chunk)
+    sha = hashlib.sha256(raw).digest()
+    return sha, fnv1a64(raw, fnv1a64(sha)).to_bytes(8, "big")

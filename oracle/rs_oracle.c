@@ -260,3 +260,17 @@ int oracle_encode_object(uint32_t *shards, int need, int total, uint64_t L) {
     }
     return OR_OK;
 }
+
+/* Chunk-file header hash of storedir (internal/store/storedir/directory.go:25-28,548-553):
+ * fnv.New64a() over SHA-256 ‖ data.  Go's hash/fnv is the published FNV-1a:
+ * offset basis 14695981039346656037, prime 1099511628211, h ^= byte then
+ * h *= prime (Go standard library, not vendored in the reference; pinned by
+ * its published vectors in tests/test_digest.py).  Call with h = the basis
+ * to start, and again with the result to continue. */
+uint64_t oracle_fnv1a64(uint64_t h, const uint8_t *p, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) {
+        h ^= p[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}

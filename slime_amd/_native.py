@@ -149,6 +149,23 @@ SIGNATURES = [
     ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
     ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
     ("slime_rs_host_stats", ctypes.c_int, [ctypes.POINTER(HostStats), ctypes.c_int]),
+    # chunk and object digests (host)
+    ("slime_rs_sha256", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    ("slime_rs_chunk_digests", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_write_chunks_digest", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, c_u32p, ctypes.c_void_p,
+      ctypes.c_void_p]),
+    ("slime_rs_reconstruct_verify", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_digest_info", ctypes.c_int, [c_intp, c_intp]),
+    ("slime_rs_write_chunks_digest_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, c_u32p,
+      ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_reconstruct_verify_ex", ctypes.c_int,
+     [ctypes.POINTER(Call), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
 ]
 
 for _name, _res, _args in SIGNATURES:
@@ -170,6 +187,7 @@ ERR_INVALID_ARG = 9
 ERR_NO_DEVICE = 10
 ERR_HIP = 11
 ERR_MAPPING_FALLBACK = 12
+ERR_BAD_HASH = 13
 
 PANIC_CODES = range(1, 9)
 
@@ -191,6 +209,10 @@ class NativeError(RuntimeError):
         self.code = code
 
 
+class BadHash(NativeError):
+    """reconstruct's ErrBadHash: "bad checksum after reconstruction" (multi_store.go:26,244-249)."""
+
+
 def check(rc: int) -> None:
     """Turn a C-ABI status into the reference's behaviour (panic) or an error."""
     if rc == OK:
@@ -201,6 +223,8 @@ def check(rc: int) -> None:
         if rc == ERR_INDEX_RANGE and detail:
             msg = detail  # Go's runtime panic text carries the index
         raise Panic(rc, msg, detail)
+    if rc == ERR_BAD_HASH:
+        raise BadHash(rc, detail)
     raise NativeError(rc, detail)
 
 
@@ -223,6 +247,13 @@ def host_stats(reset: bool = False) -> dict:
     st = HostStats()
     check(lib.slime_rs_host_stats(ctypes.byref(st), int(reset)))
     return {f: int(getattr(st, f)) for f, _ in HostStats._fields_}
+
+
+def digest_info() -> tuple[bool, int]:
+    """(SHA-256 runs on the CPU's SHA extensions, digest threads besides the caller)."""
+    e, t = ctypes.c_int(), ctypes.c_int()
+    check(lib.slime_rs_digest_info(ctypes.byref(e), ctypes.byref(t)))
+    return bool(e.value), int(t.value)
 
 
 def pool_calls(device: int) -> tuple[int, int]:

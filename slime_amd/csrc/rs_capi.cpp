@@ -26,6 +26,7 @@
 #include <tuple>
 #include <vector>
 
+#include "digest.hpp"
 #include "gfp_host.hpp"
 #include "host_copy.hpp"
 #include "kernels.hpp"
@@ -492,6 +493,7 @@ void drain_stages(Workspace* ws) {
 // copies (write_chunks' data-chunk bodies), done with the window's inputs.
 
 struct Window {
+  uint64_t index = 0;  // window number c
   std::vector<Span> in, out;
   std::vector<CopyItem> host;
   std::vector<size_t> in_off, out_off;  // offsets in the stage's pinned buffer
@@ -521,11 +523,13 @@ struct HostStats {
 };
 HostStats g_host_stats;
 
-// io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its kernels.
-// SLIME_RS_PIPE_TRACE=1 prints each call's split of host time to stderr.
-template <class Io, class Launch>
+// io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its
+// kernels; landed(c) runs once window c's outputs are in the caller's buffers
+// (windows land in order).  SLIME_RS_PIPE_TRACE=1 prints each call's split of
+// host time to stderr.
+template <class Io, class Launch, class Landed>
 int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io,
-                Launch&& launch) {
+                Launch&& launch, Landed&& landed) {
   if (n == 0) return 0;
   static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
   using clk = std::chrono::steady_clock;
@@ -548,6 +552,7 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
     for (size_t i = 0; i < w.out.size(); ++i) items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
     parallel_copy(items.data(), items.size());
     t_out += ms_since(t0);
+    landed(w.index);
     return 0;
   };
   auto body = [&]() -> int {
@@ -556,6 +561,7 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       if (c >= (uint64_t)S)
         if (int rc = land(s)) return rc;
       Window& w = win[s];
+      w.index = c;
       w.in.clear(), w.out.clear(), w.host.clear();
       io(c, s, w);
       uint8_t* const pin = pin_of(s);
@@ -604,6 +610,12 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
     fprintf(stderr, "slime_rs %s windows=%llu copy_in=%.3f enqueue=%.3f wait=%.3f copy_out=%.3f total=%.3f ms\n", what,
             (unsigned long long)n, t_in, t_enq, t_wait, t_out, t_total);
   return rc;
+}
+
+template <class Io, class Launch>
+int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io,
+                Launch&& launch) {
+  return run_windows(what, ws, dev, n, stage_bytes, io, launch, [](uint64_t) {});
 }
 
 // Columns per window so that one window moves about `stage` bytes over
@@ -730,6 +742,7 @@ const char* status_text(int st) {
     case 10: return "no HIP device";
     case 11: return "HIP runtime error";
     case 12: return "no mapping value found";
+    case 13: return "bad checksum after reconstruction";
     default: return "unknown status";
   }
 }
@@ -1275,20 +1288,36 @@ static int write_data_chunks(int dev, const uint8_t* data, uint64_t size, int ne
   return 0;
 }
 
-int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
-                          uint32_t* mapping) {
+static int write_chunks_check(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
+                              uint32_t* mapping) {
   if (!mapping) return fail(Status::InvalidArg, "write_chunks: null mapping");
   *mapping = 0;
   if (need < 1 || total < need) return fail(Status::InvalidArg, "write_chunks: need must be >= 1 and total >= need");
-  const uint64_t L = slot_L(size, (uint32_t)need);
-  if (L == 0) return 0;  // MapToGF(empty) = (0, []): every chunk is empty
+  if (slot_L(size, (uint32_t)need) == 0) return 0;
   if (!data || !chunks) return fail(Status::InvalidArg, "write_chunks: null buffer");
   for (int i = 0; i < total; ++i)
     if (!chunks[i]) return fail(Status::InvalidArg, "write_chunks: null chunk buffer");
+  return 0;
+}
+
+// writeChunks' device pass; dg (optional) hashes the chunks as they become
+// final (WriteChunkDigests): it hears of every parity window that lands, of
+// a parity rewrite, and of the final mapping.  Arguments already checked.
+static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
+                             uint32_t* mapping, WriteChunkDigests* dg) {
+  const uint64_t L = slot_L(size, (uint32_t)need);
+  if (L == 0) {  // MapToGF(empty) = (0, []): every chunk is empty
+    if (dg) dg->finalize(0);
+    return 0;
+  }
   DeviceLease dl;
   if (int rc = dl.acquire()) return rc;
   const int dev = dl.device;
-  if (total == need) return write_data_chunks(dev, data, size, need, chunks, mapping);
+  if (total == need) {
+    const int rc = write_data_chunks(dev, data, size, need, chunks, mapping);
+    if (dg && !rc) dg->finalize(*mapping);
+    return rc;
+  }
   PlanRef plan_ref;
   if (int rc = cached_plan(PlanKey{dev, 'E', need, total, {}}, &plan_ref, make_encode_plan)) return rc;
   slime_rs_plan* const plan = plan_ref.get();
@@ -1331,6 +1360,9 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
               a.ncols = std::min(cl, L - a.col0);
               HIP_TRY(launch_encode_bytes(a, st));
               return 0;
+            },
+            [&](uint64_t c) {
+              if (dg) dg->parity_ready(4 * std::min(L, (c + 1) * cl));
             }))
       return rc;
     HIP_TRY(launch_select_mapping(d_map, d_status, 1, ws->stream));
@@ -1338,6 +1370,12 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
     HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
     const bool redo = ms[0] != 0 || ms[1] != 0;
+    if (dg) {
+      if (redo)
+        dg->parity_rewrite();  // parity chunks are written again below
+      else
+        dg->finalize(0);
+    }
     if (ms[1] != 0) {  // MapToGF's random fallback (map.go:64-66): resolved and re-encoded on device
       if (int rc = slime_rs_resolve_fallbacks(plan, slot, stride, size, 1, d_map, d_status, ws->stream, nullptr))
         return rc;
@@ -1357,10 +1395,32 @@ int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int tota
       for (int i = need; i < total; ++i) out.push_back({chunks[i], (uint64_t)i * chunk, chunk});
     if (int rc = staged_d2h(ws, slot, out.data(), out.size())) return rc;
     *mapping = ms[0];
+    if (dg && redo) {
+      dg->parity_ready(chunk);
+      dg->finalize(ms[0]);
+    }
     return 0;
   };
   const int rc = body();
   if (rc) drain_stages(ws);
+  return rc;
+}
+
+int slime_rs_write_chunks(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
+                          uint32_t* mapping) {
+  if (int rc = write_chunks_check(data, size, need, total, chunks, mapping)) return rc;
+  return write_chunks_impl(data, size, need, total, chunks, mapping, nullptr);
+}
+
+int slime_rs_write_chunks_digest(const uint8_t* data, uint64_t size, int need, int total, uint8_t* const* chunks,
+                                 uint32_t* mapping, uint8_t* sha, uint8_t* hdr) {
+  if (int rc = write_chunks_check(data, size, need, total, chunks, mapping)) return rc;
+  if (!sha) return fail(Status::InvalidArg, "write_chunks_digest: null sha output");
+  const uint64_t chunk = 4 * slot_L(size, (uint32_t)need);
+  WriteChunkDigests dg(data, size, need, total, chunk, chunks, sha, hdr);
+  const int rc = write_chunks_impl(data, size, need, total, chunks, mapping, &dg);
+  if (rc) dg.abort();
+  dg.finish();
   return rc;
 }
 
@@ -1713,7 +1773,6 @@ int slime_rs_solve_sub_identity_ex(const slime_rs_call_t* call, uint32_t* m, int
 int slime_rs_invert_matrix_ex(const slime_rs_call_t* call, const uint32_t* m, int d, uint32_t* inv) {
   SLIME_EX(call, slime_rs_invert_matrix(m, d, inv));
 }
-#undef SLIME_EX
 
 // ---- plan cache / device pool introspection ---------------------------------------
 
@@ -1754,5 +1813,65 @@ int slime_rs_pool_calls(int device, uint64_t* calls, int* inflight) {
   if (inflight) *inflight = g_pool.inflight[device].load();
   return 0;
 }
+
+// ---- chunk and object digests (host; digest.hpp) ------------------------------
+
+int slime_rs_sha256(const uint8_t* data, uint64_t len, uint8_t* out) {
+  if (!out || (len && !data)) return fail(Status::InvalidArg, "sha256: null buffer");
+  Sha256 h;
+  if (len) h.update(data, len);
+  h.final(out);
+  return 0;
+}
+
+int slime_rs_chunk_digests(const uint8_t* const* chunks, const uint64_t* lens, uint32_t n, uint8_t* sha,
+                           uint8_t* hdr) {
+  if (n == 0) return 0;
+  if (!chunks || !lens || !sha) return fail(Status::InvalidArg, "chunk_digests: null argument");
+  for (uint32_t i = 0; i < n; ++i)
+    if (lens[i] && !chunks[i]) return fail(Status::InvalidArg, "chunk_digests: null chunk");
+  digest_parallel(n, [&](size_t i) {
+    Sha256 h;
+    if (lens[i]) h.update(chunks[i], lens[i]);
+    h.final(sha + 32 * i);
+    if (hdr) {
+      const uint64_t f = fnv1a64(fnv1a64(kFnv64Offset, sha + 32 * i, 32), chunks[i], lens[i]);
+      for (int b = 0; b < 8; ++b) hdr[8 * i + b] = (uint8_t)(f >> (56 - 8 * b));
+    }
+  });
+  return 0;
+}
+
+int slime_rs_reconstruct_verify(const uint8_t* const* chunks, const int* indices, int need, uint64_t chunk_bytes,
+                                uint32_t mapping, uint64_t size, uint8_t* out, const uint8_t* want_sha) {
+  if (!want_sha) return fail(Status::InvalidArg, "reconstruct_verify: null sha");
+  if (int rc = slime_rs_reconstruct(chunks, indices, need, chunk_bytes, mapping, size, out)) return rc;
+  uint8_t have[32];
+  Sha256 h;
+  if (size) h.update(out, size);
+  h.final(have);
+  if (memcmp(have, want_sha, 32) != 0) return status_of(Status::BadHash, "reconstruct");
+  return 0;
+}
+
+int slime_rs_digest_info(int* sha_extensions_used, int* threads) {
+  if (sha_extensions_used) *sha_extensions_used = sha_extensions() ? 1 : 0;
+  if (threads) *threads = digest_threads();
+  return 0;
+}
+
+int slime_rs_write_chunks_digest_ex(const slime_rs_call_t* call, const uint8_t* data, uint64_t size, int need,
+                                    int total, uint8_t* const* chunks, uint32_t* mapping, uint8_t* sha,
+                                    uint8_t* hdr) {
+  SLIME_EX(call, slime_rs_write_chunks_digest(data, size, need, total, chunks, mapping, sha, hdr));
+}
+
+int slime_rs_reconstruct_verify_ex(const slime_rs_call_t* call, const uint8_t* const* chunks, const int* indices,
+                                   int need, uint64_t chunk_bytes, uint32_t mapping, uint64_t size, uint8_t* out,
+                                   const uint8_t* want_sha) {
+  SLIME_EX(call, slime_rs_reconstruct_verify(chunks, indices, need, chunk_bytes, mapping, size, out, want_sha));
+}
+
+#undef SLIME_EX
 
 }  // extern "C"

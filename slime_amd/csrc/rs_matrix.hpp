@@ -21,6 +21,7 @@ enum class Status : int {
   NoDevice = 10,
   Hip = 11,
   MappingFallback = 12,
+  BadHash = 13,
 };
 
 struct Matrix {

@@ -396,6 +396,47 @@ TEST_GPU(TestDevicePool) {  // calls without a pinned device go through the pool
   EXPECT(routed == 10);
 }
 
+// Chunk digests computed beside the device pipeline equal the digests of the
+// finished chunks, for the three mapping outcomes (0, 1<<31: parity chunks
+// rewritten after the speculative pass, random fallback); the verified
+// reconstruct accepts the object's own SHA-256 and rejects any other.
+TEST_GPU(TestWriteChunksDigest) {
+  std::mt19937_64 rng(29);
+  for (size_t size : {(size_t)5, (size_t)100003, (size_t)(3u << 20) + 11}) {
+    for (int kind : {0, 1, 2}) {
+      if (kind == 2 && size < 8) continue;
+      std::vector<uint8_t> obj(size);
+      for (uint8_t& b : obj) b = (uint8_t)rng();
+      if (kind == 1) obj[0] = obj[1] = obj[2] = obj[3] = 0xFF;
+      if (kind == 2) {
+        const uint8_t tricky[8] = {0xFF, 0xFF, 0xFF, 0xFF, 0x7F, 0xFF, 0xFF, 0xFF};
+        std::copy(tricky, tricky + 8, obj.begin());
+      }
+      const rs::WrittenChunks w = rs::WriteChunksDigest(obj, 4, 7);
+      EXPECT(kind != 1 || w.mapping == 1u << 31);
+      EXPECT(kind != 2 || (w.mapping != 0 && w.mapping != 1u << 31));
+      const auto [m, chunks] = rs::WriteChunks(obj, 4, 7);
+      EXPECT(kind == 2 || m == w.mapping);  // the fallback draw is random per call
+      std::vector<const uint8_t*> ptrs;
+      std::vector<uint64_t> lens;
+      for (const auto& c : w.chunks) ptrs.push_back(c.data()), lens.push_back(c.size());
+      std::vector<uint8_t> sha(32 * w.chunks.size());
+      EXPECT(slime_rs_chunk_digests(ptrs.data(), lens.data(), (uint32_t)ptrs.size(), sha.data(), nullptr) == 0);
+      for (size_t i = 0; i < w.chunks.size(); ++i)
+        EXPECT(std::equal(w.sha256[i].begin(), w.sha256[i].end(), sha.begin() + 32 * i));
+      std::array<uint8_t, 32> want;
+      EXPECT(slime_rs_sha256(obj.data(), obj.size(), want.data()) == 0);
+      const std::vector<int> have = {1, 3, 4, 6};
+      std::vector<std::vector<uint8_t>> surv;
+      for (int i : have) surv.push_back(w.chunks[i]);
+      std::vector<uint8_t> out;
+      EXPECT(rs::ReconstructObjectVerified(surv, have, w.mapping, size, want, &out) && out == obj);
+      want[7] ^= 1;
+      EXPECT(!rs::ReconstructObjectVerified(surv, have, w.mapping, size, want, &out));
+    }
+  }
+}
+
 TEST_GPU(TestCreateParity) {  // vector_test.go:24-63
   for (const Json& c : kats()["create_parity"].arr)
     EXPECT(rs::CreateParity(c["data"].mat(), (int)c["index"].u()) == c["out"].vec());

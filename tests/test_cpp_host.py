@@ -32,7 +32,7 @@ def test_cpp_host_mirror_host_only():
 def test_cpp_host_mirror_data_path():
     out = _run("gpu")
     for name in ("TestCreateParity", "TestRecovery", "TestMapTrivial", "TestMapTricky", "TestWriteChunksRoundTrip",
-                 "TestWriteChunksNoParity", "TestDevicePool"):
+                 "TestWriteChunksNoParity", "TestDevicePool", "TestWriteChunksDigest"):
         assert f"ok   {name}" in out
 
 

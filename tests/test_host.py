@@ -291,7 +291,7 @@ def _call_args(src, start):
 EX_BOUND = ["slime_rs_create_parity", "slime_rs_create_parities", "slime_rs_recover_data", "slime_rs_write_chunks",
             "slime_rs_reconstruct", "slime_gf_map_to_gf", "slime_gf_map_to_gf_with", "slime_gf_map_from_gf",
             "slime_rs_parity_matrix", "slime_rs_vandermonde_matrix", "slime_rs_solve_sub_identity",
-            "slime_rs_invert_matrix"]
+            "slime_rs_invert_matrix", "slime_rs_write_chunks_digest", "slime_rs_reconstruct_verify"]
 
 
 def test_go_shim_keeps_the_reference_api_and_binds_the_header():
