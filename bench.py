@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall time budget of the CPU sample")
     ap.add_argument("--bytes-path", type=int, default=1,
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
+    ap.add_argument("--ceilings", type=int, default=1,
+                    help="measure torch copy/fill HBM rates after the timed region (roofline.measured_streams)")
     ap.add_argument("--host-path", type=int, default=1,
                     help="rank 0 at N=1: PCIe-inclusive writeChunks/reconstruct from host memory (never `value`)")
     ap.add_argument("--host-order", choices=["before-free", "after-free"], default="before-free",
@@ -425,6 +427,38 @@ def shape_label(need: int, total: int, mib: int) -> str:
             (8, 12, 512): "north-star 64 MiB shards: "}.get((need, total, mib), "")
 
 
+def stream_ceilings(dev: int, stream, gib: int = 4, reps: int = 5) -> dict:
+    """the achieved rate beside measured stream rates on this
+    GPU in this process, after the timed region: torch's device copy (1:1
+    read:write) and fill (write-only) over `gib` GiB, median of `reps`, in
+    GB/s of HBM traffic.  Reference points from library kernels, not ceilings
+    of the apply kernel (its 2:1 mix runs above the copy)."""
+    import torch
+    n = (gib << 30) // 4
+    a = torch.empty(n, dtype=torch.int32, device=f"cuda:{dev}")
+    b = torch.empty_like(a)
+    a.fill_(1)
+
+    def timed(fn, nbytes):
+        fn()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return round(nbytes / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9, 1)
+
+    with torch.cuda.stream(stream):
+        copy = timed(lambda: b.copy_(a), 2 * a.numel() * 4)
+        fill = timed(lambda: b.fill_(7), a.numel() * 4)
+    del a, b
+    torch.cuda.empty_cache()
+    return {"torch_copy_gbs": copy, "torch_fill_gbs": fill, "bytes": f"{gib} GiB per pass, median of {reps}"}
+
+
 def kernel_source_id() -> str:
     """Hash of the apply kernel's sources: PMC traffic measured on one build
     is only replayed into a bench line of the same kernel source."""
@@ -563,6 +597,7 @@ def main():
             traffic = None
     # Distinct devices across ranks (n_gpus), by PCI address.
     bdfs = batch.gather_strings(board_info(dev)["bdf"])
+    ceilings = stream_ceilings(dev, stream) if args.ceilings else None
 
     host = None
     want_host = rank == 0 and world == 1 and args.host_path
@@ -620,6 +655,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_source,
                 "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg},
+                "measured_streams": ceilings,
             },
             "cpu_baseline": None,
             "object_bytes_path": bytes_path,
