@@ -248,6 +248,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     write; MapToGFWith per survivor (:224), RecoverData (:237) and MapFromGF
     per data row (:239) on read."""
     import numpy as np
+    from slime_amd import _native as N
     from slime_amd import gf, objects, rs
     rng = np.random.default_rng(0x5113E)
     data = rng.integers(0, 256, size=obj_mib << 20, dtype=np.uint8)
@@ -259,6 +260,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
 
     def med(fn):
         fn()
+        N.host_stats(reset=True)  # the pipeline split covers the timed calls only
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -266,17 +268,15 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
             ts.append(time.perf_counter() - t0)
         return sorted(ts)[len(ts) // 2]
 
-    from slime_amd import _native as N
-
     def split(st):  # ms per call of the windowed pipeline, from slime_rs_host_stats
         c = max(1, st["calls"])
         return {k[:-3] + "_ms": round(st[k] / 1e3 / c, 3) for k in ("copy_in_us", "enqueue_us", "wait_us",
                                                                       "copy_out_us", "total_us")}
 
     box = {}
-    N.host_stats(reset=True)
     t_w = med(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
     split_w = split(N.host_stats(reset=True))
+    t_wz = med(lambda: objects.write_chunks(data, need, total, out=chunks, alias=True))
     surv = [chunks[i] for i in have]
     t_r = med(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
     split_r = split(N.host_stats(reset=True))
@@ -312,7 +312,8 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
     digests = digest_leg(data, need, total, chunks, have, out, med, g)
-    return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "link": link_probe(obj_mib),
+    return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "write_chunks_zero_copy_gibs": g(t_wz),
+            "link": link_probe(obj_mib),
             "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
                                "what": "mean per call: host copies in/out, launches, waits on the device/link side "
                                        "(a large wait with normal copies = DMA contention, DESIGN.md End-to-end)"},
@@ -339,6 +340,7 @@ def digest_leg(data, need, total, chunks, have, out, med, g) -> dict:
     box = {}
     t_fused = med(lambda: box.update(r=objects.write_chunks_digest(data, need, total, out=chunks)))
     m, _, shas, _ = box["r"]
+    t_fz = med(lambda: objects.write_chunks_digest(data, need, total, out=chunks, alias=True))
     t_seq = med(lambda: (objects.write_chunks(data, need, total, out=chunks), objects.chunk_digests(chunks)))
     t_dig = med(lambda: objects.chunk_digests(chunks))
     t_hdr = med(lambda: objects.chunk_digests(chunks, headers=True))
@@ -350,7 +352,8 @@ def digest_leg(data, need, total, chunks, have, out, med, g) -> dict:
     t_obj = med(lambda: objects.sha256(out))
     ok = shas == [hashlib.sha256(c.tobytes()).digest() for c in chunks] and bytes(out) == data.tobytes()
     chunk_bytes = sum(c.size for c in chunks)
-    return {"write_chunks_digest_gibs": g(t_fused), "write_chunks_then_digests_gibs": g(t_seq),
+    return {"write_chunks_digest_gibs": g(t_fused), "write_chunks_digest_zero_copy_gibs": g(t_fz),
+            "write_chunks_then_digests_gibs": g(t_seq),
             "chunk_sha256_gbs": round(chunk_bytes / t_dig / 1e9, 2),
             "chunk_sha256_fnv_header_gbs": round(chunk_bytes / t_hdr / 1e9, 2),
             "sha256_one_thread_gbs": round(one.size / t_one / 1e9, 2),
@@ -597,7 +600,6 @@ def main():
             traffic = None
     # Distinct devices across ranks (n_gpus), by PCI address.
     bdfs = batch.gather_strings(board_info(dev)["bdf"])
-    ceilings = stream_ceilings(dev, stream) if args.ceilings else None
 
     host = None
     want_host = rank == 0 and world == 1 and args.host_path
@@ -609,6 +611,9 @@ def main():
 
     if want_host and args.host_order == "before-free":
         host = run_host_leg()
+    # After the host leg: the probe's buffers go back to the driver, whose
+    # wipe of freed VRAM would slow the host leg's DMA (DESIGN.md End-to-end).
+    ceilings = stream_ceilings(dev, stream) if args.ceilings else None
     bytes_path = None
     if args.bytes_path:
         del buf, rec  # rec aliases buf for in-place repair

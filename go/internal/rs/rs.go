@@ -282,22 +282,40 @@ func invertMatrix(m [][]uint32) [][]uint32 {
 	return matrixFromC(&inv[0], d, d)
 }
 
+// chunkBuffers allocates the total chunk slices of a writeChunks call.  A data
+// chunk that lies wholly inside the object is the object's own bytes
+// (MapFromGF(m, MapToGF(x)) = x, map.go:15-33,103-113), so it is returned as a
+// capacity-limited subslice of data and the library skips its copy; the rest
+// are fresh.  The caller must not modify data while it uses the chunks, which
+// writeChunks never does (the request body is read-only from there on).
+func chunkBuffers(data []byte, need, total, cb int) [][]byte {
+	chunks := make([][]byte, total)
+	for i := range chunks {
+		if i < need && cb > 0 && (i+1)*cb <= len(data) {
+			chunks[i] = data[i*cb : (i+1)*cb : (i+1)*cb]
+		} else {
+			chunks[i] = make([]byte, cb)
+		}
+	}
+	return chunks
+}
+
 // WriteChunks is the data path of Multi.writeChunks
 // (internal/store/multi/multi_store.go:526-531 and :554) in one GPU pass:
 // gf.MapToGF, splitVector, CreateParity for every parity row, gf.MapFromGF per
-// part.  It returns MappingValue and the total chunks as written to stores.
+// part.  It returns MappingValue and the total chunks as written to stores
+// (whole data chunks alias data, see chunkBuffers).
 // Not part of the reference's rs API: it lets writeChunks replace its
 // per-row CreateParity loop and per-part MapFromGF calls (see INTEGRATION.md).
 func WriteChunks(data []byte, need, total int) (uint32, [][]byte) {
 	cb := int(C.slime_rs_chunk_size(C.uint64_t(len(data)), C.int(need)))
-	chunks := make([][]byte, total)
+	chunks := chunkBuffers(data, need, total, cb)
 	ptrs := (**C.uint8_t)(C.calloc(C.size_t(total+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
 	defer C.free(unsafe.Pointer(ptrs))
 	ps := unsafe.Slice(ptrs, total+1)
 	var pinner runtime.Pinner
 	defer pinner.Unpin()
 	for i := range chunks {
-		chunks[i] = make([]byte, cb)
 		if cb > 0 {
 			pinner.Pin(&chunks[i][0])
 			ps[i] = (*C.uint8_t)(unsafe.Pointer(&chunks[i][0]))
@@ -365,7 +383,7 @@ func ReconstructObject(chunks [][]byte, indices []int, mapping uint32, size int)
 // instead of calling store.DataV.
 func WriteChunksDigest(data []byte, need, total int) (uint32, [][]byte, [][32]byte) {
 	cb := int(C.slime_rs_chunk_size(C.uint64_t(len(data)), C.int(need)))
-	chunks := make([][]byte, total)
+	chunks := chunkBuffers(data, need, total, cb)
 	sums := make([][32]byte, total+1)
 	ptrs := (**C.uint8_t)(C.calloc(C.size_t(total+1), C.size_t(unsafe.Sizeof(uintptr(0)))))
 	defer C.free(unsafe.Pointer(ptrs))
@@ -373,7 +391,6 @@ func WriteChunksDigest(data []byte, need, total int) (uint32, [][]byte, [][32]by
 	var pinner runtime.Pinner
 	defer pinner.Unpin()
 	for i := range chunks {
-		chunks[i] = make([]byte, cb)
 		if cb > 0 {
 			pinner.Pin(&chunks[i][0])
 			ps[i] = (*C.uint8_t)(unsafe.Pointer(&chunks[i][0]))

@@ -238,7 +238,11 @@ uint64_t slime_rs_chunk_size(uint64_t size, int need);
  * *mapping receives MappingValue.  The random-mapping fallback draws from the
  * library's stream (slime_gf_seed).  need >= 1 and total >= need (total ==
  * need: a store without parity, multi_config.go:36); size 0 gives mapping 0
- * and empty chunks.  Synchronous; thread-safe. */
+ * and empty chunks.  Zero-copy data chunks: chunks[j] (j < need) may be
+ * data + j*chunk_size when that chunk lies wholly inside the object; its bytes
+ * are then already final and are not copied.  Any other overlap between a
+ * chunk buffer and data is refused (SLIME_RS_ERR_INVALID_ARG).  Synchronous;
+ * thread-safe. */
 int slime_rs_write_chunks(const uint8_t *data, uint64_t size, int need, int total, uint8_t *const *chunks,
                           uint32_t *mapping);
 

@@ -1279,7 +1279,7 @@ static int write_data_chunks(int dev, const uint8_t* data, uint64_t size, int ne
     const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk;
     uint8_t* c = chunks[j];
     const uint64_t body = size > lo ? std::min(size, hi) - lo : 0;
-    if (body) memcpy(c, data + lo, body);
+    if (body && c != data + lo) memcpy(c, data + lo, body);  // an aliased chunk is already the object's bytes
     const uint64_t zero_end = word_end > lo ? std::min(word_end, hi) - lo : 0;
     if (zero_end > body) memset(c + body, 0, zero_end - body);
     for (uint64_t o = std::max(body, zero_end); o < chunk; o += 4) memcpy(c + o, pad, 4);
@@ -1297,6 +1297,19 @@ static int write_chunks_check(const uint8_t* data, uint64_t size, int need, int 
   if (!data || !chunks) return fail(Status::InvalidArg, "write_chunks: null buffer");
   for (int i = 0; i < total; ++i)
     if (!chunks[i]) return fail(Status::InvalidArg, "write_chunks: null chunk buffer");
+  // Zero-copy data chunks: chunk j < need may BE the object's bytes
+  // data + j*chunk when it lies wholly inside the object (its bytes are
+  // final as they are: MapFromGF(m, MapToGF(x)) = x, map.go:15-33,103-113).
+  // Any other overlap between a chunk buffer and the object is refused.
+  const uint64_t chunk = 4 * slot_L(size, (uint32_t)need);
+  const uintptr_t d0 = (uintptr_t)data, d1 = d0 + size;
+  for (int i = 0; i < total; ++i) {
+    const uintptr_t c0 = (uintptr_t)chunks[i], c1 = c0 + chunk;
+    if (c1 <= d0 || c0 >= d1) continue;
+    if (i < need && c0 == d0 + (uint64_t)i * chunk && (uint64_t)(i + 1) * chunk <= size) continue;
+    return fail(Status::InvalidArg, "write_chunks: chunk buffer overlaps the object (only data chunk j may alias "
+                                    "data + j*chunk_size, when it lies wholly inside the object)");
+  }
   return 0;
 }
 
@@ -1349,7 +1362,7 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
                 const uint64_t lo = (uint64_t)j * chunk + 4 * c0, hi = std::min(size, lo + 4 * nc);
                 if (lo >= hi) continue;
                 w.in.push_back({const_cast<uint8_t*>(data) + lo, lo, hi - lo});
-                w.host.push_back({chunks[j] + 4 * c0, data + lo, hi - lo});
+                if (chunks[j] + 4 * c0 != data + lo) w.host.push_back({chunks[j] + 4 * c0, data + lo, hi - lo});
               }
               for (int i = 0; i < r; ++i)
                 w.out.push_back({chunks[need + i] + 4 * c0, (uint64_t)(need + i) * chunk + 4 * c0, 4 * nc});

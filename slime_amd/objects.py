@@ -51,13 +51,14 @@ def _bytes_view(data) -> np.ndarray:
     return np.frombuffer(memoryview(data), dtype=np.uint8)
 
 
-def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None = None
+def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None = None, alias: bool = False
                  ) -> tuple[int, list[np.ndarray]]:
     """(MappingValue, [total chunk byte arrays]) for an object, as writeChunks
     stores them.  `out`: caller-owned uint8 chunk buffers (>= chunk_size bytes
-    each) written in place and returned as views."""
+    each) written in place and returned as views.  alias=True returns the data
+    chunks that lie wholly inside the object as views of `data` (no copy)."""
     buf = _bytes_view(data)
-    chunks = _chunk_out(buf, need, total, out)
+    chunks = _chunk_out(buf, need, total, out, alias)
     ptrs = (ctypes.c_void_p * max(len(chunks), 1))(*[c.ctypes.data for c in chunks])
     m = ctypes.c_uint32(0)
     N.check(lib.slime_rs_write_chunks(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
@@ -65,24 +66,33 @@ def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None =
     return int(m.value), chunks
 
 
-def _chunk_out(buf: np.ndarray, need: int, total: int, out) -> list[np.ndarray]:
+def _chunk_out(buf: np.ndarray, need: int, total: int, out, alias: bool = False) -> list[np.ndarray]:
     cb = chunk_size(buf.size, need) if need > 0 else 0
     if out is None:
-        return [np.empty(cb, dtype=np.uint8) for _ in range(max(total, 0))]
-    if len(out) != total or any(o.dtype != np.uint8 or not o.flags.c_contiguous or not o.flags.writeable
-                                or o.size < cb for o in out):
-        raise ValueError("write_chunks: out must be `total` writeable contiguous uint8 arrays of chunk_size bytes")
-    return [o[:cb] for o in out]
+        chunks = [np.empty(cb, dtype=np.uint8) for _ in range(max(total, 0))]
+    else:
+        if len(out) != total or any(o.dtype != np.uint8 or not o.flags.c_contiguous or not o.flags.writeable
+                                    or o.size < cb for o in out):
+            raise ValueError("write_chunks: out must be `total` writeable contiguous uint8 arrays of chunk_size bytes")
+        chunks = [o[:cb] for o in out]
+    if alias and cb:
+        # Zero-copy data chunks: chunk j is the object's own bytes where it lies
+        # wholly inside the object (views of `data`; slime_rs_write_chunks).
+        for j in range(min(need, total)):
+            if (j + 1) * cb <= buf.size:
+                chunks[j] = buf[j * cb:(j + 1) * cb]
+    return chunks
 
 
 def write_chunks_digest(data, need: int, total: int, out: Sequence[np.ndarray] | None = None,
-                        headers: bool = False) -> tuple[int, list[np.ndarray], list[bytes], list[bytes] | None]:
+                        headers: bool = False, alias: bool = False
+                        ) -> tuple[int, list[np.ndarray], list[bytes], list[bytes] | None]:
     """write_chunks plus each chunk's SHA-256 (what writeChunks' store.DataV
     stores, multi_store.go:554-556) and, with headers=True, each chunk file's
     8-byte FNV-1a-64 header over SHA-256 ‖ chunk (directory.go:548-553).
     Returns (mapping, chunks, shas, headers or None)."""
     buf = _bytes_view(data)
-    chunks = _chunk_out(buf, need, total, out)
+    chunks = _chunk_out(buf, need, total, out, alias)
     ptrs = (ctypes.c_void_p * max(len(chunks), 1))(*[c.ctypes.data for c in chunks])
     sha = np.zeros(max(total, 1) * 32, dtype=np.uint8)
     hdr = np.zeros(max(total, 1) * 8, dtype=np.uint8) if headers else None

@@ -111,3 +111,31 @@ def test_digest_argument_checks():
 def test_bad_hash_status_maps_to_reference_error():
     assert N.lib.slime_rs_status_string(N.ERR_BAD_HASH).decode() == "bad checksum after reconstruction"
     assert issubclass(N.BadHash, N.NativeError)
+
+
+def test_write_chunks_refuses_overlap_other_than_whole_data_chunks():
+    """Zero-copy data chunks (chunk j = data + j*chunk_size, wholly inside the
+    object) are admitted; any other overlap with the object is refused before
+    any device work (so this runs without a GPU)."""
+    import ctypes
+    size, need, total = 1000, 4, 6
+    cb = O.chunk_size(size, need)
+    data = np.zeros(size, dtype=np.uint8)
+    own = [np.zeros(cb, dtype=np.uint8) for _ in range(total)]
+    m = ctypes.c_uint32()
+
+    def call(ptrs):
+        arr = (ctypes.c_void_p * total)(*ptrs)
+        return N.lib.slime_rs_write_chunks(data.ctypes.data, size, need, total, arr, ctypes.byref(m))
+
+    base = data.ctypes.data
+    good = [o.ctypes.data for o in own]
+    assert (size + 3) // 4 > 3 * (cb // 4)  # the last data chunk is partly padding
+    for bad in ([base + 1] + good[1:],                                 # misaligned alias
+                good[:3] + [base + 3 * cb] + good[4:],                 # chunk 3 runs past the object
+                good[:4] + [base] + good[5:],                          # a parity chunk inside the object
+                [base + cb] + good[1:]):                               # chunk 0 at chunk 1's bytes
+        assert call(bad) == N.ERR_INVALID_ARG
+    assert "overlaps the object" in N.lib.slime_rs_last_error().decode()
+    rc = call([base, base + cb, base + 2 * cb] + good[3:])
+    assert rc in (N.OK, N.ERR_NO_DEVICE)

@@ -115,3 +115,24 @@ def test_reconstruct_verify(kind):
     corrupt[9][100] ^= 0x40  # a survivor flipped in storage: the rebuilt object no longer matches
     with pytest.raises(N.BadHash):
         objects.reconstruct([corrupt[i] for i in have], have, m, len(obj), sha=sha)
+
+
+@pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (8, 8), (17, 20)])
+@pytest.mark.parametrize("S", [5, 4096, 100003, (8 << 20) + 4])
+@pytest.mark.parametrize("kind", ["plain", "high"])
+def test_write_chunks_zero_copy_data_chunks(need, total, S, kind):
+    """alias=True: whole data chunks are views of the object and are not
+    copied; every chunk still equals the reference's framing."""
+    from slime_amd import objects
+    rng = np.random.default_rng(S + need)
+    obj = np.frombuffer(_obj_bytes(rng, S, kind), dtype=np.uint8).copy()
+    m, chunks = objects.write_chunks(obj, need, total, alias=True)
+    cb = objects.chunk_size(S, need)
+    for j in range(need):
+        if (j + 1) * cb <= S:
+            assert np.shares_memory(chunks[j], obj)
+    m_ref, want = _oracle_chunks(obj.tobytes(), need, total)
+    assert m == m_ref and [c.tobytes() for c in chunks] == want
+    m2, chunks2, shas, _ = objects.write_chunks_digest(obj, need, total, alias=True)
+    assert m2 == m and [c.tobytes() for c in chunks2] == want
+    assert shas == [hashlib.sha256(c).digest() for c in want]
