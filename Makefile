@@ -13,8 +13,13 @@ HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 CXXTEST  := tests/cpp/rs_host_test
 CACHETEST := tests/cpp/plan_cache_test
+COPYTEST := tests/cpp/copy_pool_test
 
-all: $(LIB) oracle $(CXXTEST) $(CACHETEST)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST)
+
+# The host copy pool under concurrent callers, CPU only.
+$(COPYTEST): tests/cpp/copy_pool_test.cpp $(SRC)/host_copy.cpp $(SRC)/host_copy.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -I$(SRC) -o $@ tests/cpp/copy_pool_test.cpp $(SRC)/host_copy.cpp
 
 # The plan cache (plan_cache.hpp) over the product's host matrix code, CPU only.
 $(CACHETEST): tests/cpp/plan_cache_test.cpp $(SRC)/plan_cache.hpp $(SRC)/rs_matrix.cpp $(SRC)/rs_matrix.hpp
@@ -42,7 +47,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST)
+	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -85,6 +86,9 @@ size_t drain(Job* j) {
   return did;
 }
 
+// Jobs of several callers at once (concurrent host calls of a proxy, main.go:107-109):
+// each caller posts its job and drains it itself; workers help the oldest
+// job that still has unclaimed pieces.
 class Pool {
  public:
   explicit Pool(int nthreads) {
@@ -101,8 +105,7 @@ class Pool {
   int threads() const { return (int)th_.size(); }
 
   void run(const CopyItem* pieces, size_t n) {
-    std::unique_lock<std::mutex> owner(run_mu_, std::try_to_lock);
-    if (!owner.owns_lock() || th_.empty()) {  // busy or no workers: copy here
+    if (th_.empty()) {
       for (size_t i = 0; i < n; ++i) copy_piece(pieces[i]);
       return;
     }
@@ -111,18 +114,29 @@ class Pool {
     j.n = n;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      cur_ = &j;
+      jobs_.push_back(&j);
       posted_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     const size_t did = drain(&j);
     std::unique_lock<std::mutex> lk(mu_);
+    auto it = std::find(jobs_.begin(), jobs_.end(), &j);
+    if (it != jobs_.end()) jobs_.erase(it);
     j.done += did;
     done_cv_.wait(lk, [&] { return j.done == j.n && j.active == 0; });
-    cur_ = nullptr;
   }
 
  private:
+  // First queued job with pieces left; drops exhausted ones.  Needs mu_.
+  Job* pick() {
+    while (!jobs_.empty()) {
+      Job* j = jobs_.front();
+      if (j->next.load(std::memory_order_relaxed) < j->n) return j;
+      jobs_.pop_front();
+    }
+    return nullptr;
+  }
+
   void worker() {
     uint64_t seen = 0;
     for (;;) {
@@ -138,15 +152,14 @@ class Pool {
         }
       }
       std::unique_lock<std::mutex> lk(mu_);
-      auto ready = [&] { return stop_.load() || (cur_ && cur_->next.load(std::memory_order_relaxed) < cur_->n); };
-      if (!timed_out && !ready()) {  // a job came and went while this worker spun up: keep spinning
+      Job* j = pick();
+      if (!timed_out && !j && !stop_.load()) {  // a job came and went while this worker spun up: keep spinning
         seen = posted_.load(std::memory_order_relaxed);
         continue;
       }
-      cv_.wait(lk, ready);
+      cv_.wait(lk, [&] { return stop_.load() || (j = pick()) != nullptr; });
       if (stop_.load()) return;
       seen = posted_.load(std::memory_order_relaxed);
-      Job* j = cur_;
       ++j->active;
       lk.unlock();
       const size_t did = drain(j);
@@ -157,10 +170,9 @@ class Pool {
     }
   }
 
-  std::mutex run_mu_;  // one job at a time
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  Job* cur_ = nullptr;
+  std::deque<Job*> jobs_;            // posted jobs, oldest first (guarded by mu_)
   std::atomic<uint64_t> posted_{0};  // jobs posted so far (the spinners' signal)
   std::atomic<bool> stop_{false};
   std::vector<std::thread> th_;

@@ -16,7 +16,7 @@ struct CopyItem {
 
 // Copy every item (non-overlapping ranges).  Large items are split into
 // pieces spread over the pool; the caller works too.  Concurrent callers are
-// safe: a caller that finds the pool busy copies on its own thread.
+// safe and share the pool: each drains its own job, workers help the oldest.
 void parallel_copy(const CopyItem* items, size_t n);
 
 // Threads the pool runs besides the caller (env SLIME_RS_COPY_THREADS, default 4).

@@ -315,7 +315,11 @@ struct Workspace {
     if (dbuf) (void)hipFree(dbuf);
     dbuf = nullptr;
     dcap = 0;
-    size_t want = std::max<size_t>(bytes, 1u << 20);
+    // Headroom: a host call's workspace serves calls of other shapes next
+    // (write_chunks needs total x chunk, reconstruct 2 x need x chunk), and
+    // every regrowth is a device-synchronising hipFree plus a fresh hipMalloc
+    // whose freed predecessor the driver wipes while other DMA runs.
+    size_t want = std::max<size_t>(bytes + bytes / 2, 1u << 20);
     HIP_TRY(hipMalloc((void**)&dbuf, want));
     dcap = want;
     return 0;
@@ -328,8 +332,9 @@ struct Workspace {
     if (pin) (void)hipHostFree(pin);
     pin = nullptr;
     pcap = 0;
-    HIP_TRY(hipHostMalloc((void**)&pin, bytes, hipHostMallocDefault));
-    pcap = bytes;
+    const size_t want = bytes + bytes / 4;  // headroom, as reserve()
+    HIP_TRY(hipHostMalloc((void**)&pin, want, hipHostMallocDefault));
+    pcap = want;
     if (getenv("SLIME_RS_PIPE_TRACE")) {
       const NumaInfo ni = numa_info(device, pin);
       fprintf(stderr, "slime_rs pinned %zu MiB: page node %d, gpu node %d, cpu %d (node %d)\n", bytes >> 20,
@@ -352,10 +357,13 @@ struct Workspace {
 std::mutex g_ws_mu;
 std::vector<Workspace*> g_ws_free;
 
+// Most recently released first: a caller's next call gets the workspace its
+// last call grew (buffers sized, pages warm), instead of cycling through every
+// workspace that a burst of concurrent calls once created and regrowing each.
 int acquire_ws(int device, Workspace** out) {
   {
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (size_t i = 0; i < g_ws_free.size(); ++i) {
+    for (size_t i = g_ws_free.size(); i-- > 0;) {
       if (g_ws_free[i]->device == device) {
         *out = g_ws_free[i];
         g_ws_free.erase(g_ws_free.begin() + (long)i);

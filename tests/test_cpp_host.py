@@ -48,3 +48,20 @@ def test_plan_cache_is_bounded_and_safe_under_eviction():
     assert r.returncode == 0, r.stdout + r.stderr
     for name in ("TestPlanCacheBounded", "TestPlanCacheFailedBuild", "TestPlanCacheConcurrent"):
         assert f"ok   {name}" in r.stdout
+
+
+COPY_BIN = os.path.join(ROOT, "tests", "cpp", "copy_pool_test")
+
+
+@pytest.mark.parametrize("threads", ["0", "4"])
+def test_copy_pool_under_concurrent_callers(threads):
+    """host_copy.cpp: 8 callers x 60 jobs of 1-5 items (tiny to 6 MiB, odd
+    offsets) land byte-exact with nothing written around them, with no pool
+    workers and with 4."""
+    if not os.path.exists(COPY_BIN):
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/copy_pool_test"], check=True, capture_output=True)
+    env = dict(os.environ, SLIME_RS_COPY_THREADS=threads)
+    r = subprocess.run([COPY_BIN], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
+
