@@ -88,6 +88,7 @@ for step in "$@"; do
     pipek48) run pipek_40_48 300 python tools/apply_variants.py --need 40 --total 48 --nobj 16 --wide 1 --pipek 1 --blocks 256,512,1024 &&
              run pipek_48_56 300 python tools/apply_variants.py --need 48 --total 56 --nobj 16 --wide 1 --pipek 1 --blocks 256,512,1024 ;;
     hostconc) run hostconc 400 python tools/host_concurrency.py ;;
+    hostconc_q16) run hostconc_q16 400 env GPU_MAX_HW_QUEUES=16 python tools/host_concurrency.py ;;
     ns64) run ns64_harness 300 python tools/apply_variants.py --mib 512 --nobj 64 --variants 13,14,15,20 \
             --blocks 256,512,1024 --nseg 1,2,4,8 &&
           run ns64_bench 300 python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
