@@ -11,7 +11,7 @@ GPU, no data-path collective: "weak" scaling, each rank owns its own batch).
 
 value = (sum of object bytes encoded + decoded over all ranks) / (max over
 ranks of the timed K steps), in GiB/s.  roofline: algorithmic HBM bytes per
-launch of the dominant kernel (rs_apply_pipe_kernel<8>) / its average duration,
+launch of the dominant kernel (rs_apply_queue_kernel<8>) / its average duration,
 from HIP events recorded on the launch stream.  cpu_baseline: the oracle's
 faithful scalar C restatement of the reference's Go path, on a bounded sample.
 
@@ -578,10 +578,15 @@ def main():
     dec_alg = nobj * 4 * L * (need + len(erase))
     launch_ms = (enc_ms + dec_ms) / 2
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
-    # The product dispatch (rs_apply.hip): the pipelined kernel for shards
-    # under 4 GiB, unless the kernel form was switched (slime_rs_kernel_pipeline).
-    kname = "rs_apply_pipe_kernel" if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1 \
-        else "rs_apply_kernel"
+    # The product dispatch (rs_apply.hip): the pipelined kernels for shards
+    # under 4 GiB unless the kernel form was switched (slime_rs_kernel_pipeline),
+    # with the dynamic (ticket) schedule for the k range slime_rs_kernel_schedule
+    # selects.
+    kname = "rs_apply_kernel"
+    if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
+        sched = D.lib.slime_rs_kernel_schedule(-1)
+        queue = need <= 16 and (sched == 2 or (sched == 1 and 5 <= need <= 12))
+        kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such
     # passes only when they were taken on this config AND this kernel source,

@@ -66,6 +66,7 @@ SIGNATURES = [
     ("slime_rs_select_device", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_host_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_pipeline", ctypes.c_int, [ctypes.c_int]),
+    ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
     ("slime_gf_max_val", ctypes.c_uint32, []),
     ("slime_gf_minverse", ctypes.c_uint32, [ctypes.c_uint32]),
     ("slime_gf_raise", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),

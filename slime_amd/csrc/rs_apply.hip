@@ -19,6 +19,9 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "kernels.hpp"
 #include "rs_apply_kernel.hpp"
@@ -151,6 +154,75 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Dynamic schedule (rs_apply_queue_kernel): tickets instead of a fixed share
+// per wave, so the XCDs that stream faster take more of the batch.  In-process
+// A/B against rs_apply_pipe_kernel<8,3> at C3 (profiles/r02/s39_queue3/):
+// encode 8.568 -> 8.295 ms, decode 8.441 -> 8.239 on a fast-placement
+// allocation; 9.915 -> 9.376 / 9.857 -> 9.341 on a slow one
+// (profiles/r02/s37_queue/).  A unit is C tiles of U KiB per stream (C x U
+// about 6), dealt over kQueueCounters ticket counters.
+constexpr int kQueueCounters = 8;
+template <int K>
+constexpr int queue_unit_tiles() {
+  return pipe_unroll<K>() >= 6 ? 1 : 6 / pipe_unroll<K>();
+}
+
+template <int K>
+bool queue_on() {
+  const int m = queue_mode();
+  return m == 2 || (m == 1 && K >= 5 && K <= 12);
+}
+
+// Two ticket-counter sets per (device, stream): a launch draws from set
+// `parity` and zeroes set `parity ^ 1` for the next launch on its stream,
+// which runs after it (stream order); other streams have sets of their own.
+// The lock is held across the launch so that launches reach each stream in
+// parity order.  Sets live for the process (a few KiB per stream used).
+struct TicketSets {
+  uint32_t* base = nullptr;  // 2 x kQueueCounters x kTicketStride words
+  uint32_t parity = 0;
+};
+std::mutex g_ticket_mu;
+std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
+  static auto* m = new std::map<std::pair<int, hipStream_t>, TicketSets>();
+  return *m;
+}
+
+template <int K>
+hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched) {
+  constexpr int U = pipe_unroll<K>();
+  constexpr int C = queue_unit_tiles<K>();
+  *launched = false;
+  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
+  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  std::lock_guard<std::mutex> lock(g_ticket_mu);
+  TicketSets& ts = ticket_sets()[{dev, stream}];
+  const size_t set_words = (size_t)kQueueCounters * apply::kTicketStride;
+  if (!ts.base) {
+    void* p = nullptr;
+    if (hipError_t e = hipMalloc(&p, 2 * set_words * sizeof(uint32_t))) return e;
+    // On the launch stream: a plain hipMemset (null stream) is not ordered
+    // before launches on non-blocking streams.
+    if (hipError_t e = hipMemsetAsync(p, 0, 2 * set_words * sizeof(uint32_t), stream)) {
+      (void)hipFree(p);
+      return e;
+    }
+    ts.base = (uint32_t*)p;
+  }
+  const Geometry& geo = geometry();
+  const uint64_t blocks = geo.target ? geo.target : pipe_blocks<K>();
+  hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
+                     dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
+                     a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k,
+                     ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words);
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) ts.parity ^= 1;  // a launch that never started zeroed nothing
+  *launched = true;
+  return e;
+}
+
 }  // namespace
 
 // Kernel form (process-wide): the software-pipelined kernels (default) or
@@ -163,6 +235,16 @@ static std::atomic<int> g_pipelined{[] {
   return e && e[0] == '0' ? 0 : 1;
 }()};
 bool pipelined_kernels() { return g_pipelined.load(std::memory_order_relaxed) != 0; }
+// Which k take the dynamic schedule (process-wide): 1 = 5..12 (default, the
+// measured ones), 0 = none, 2 = every k <= 16.  Env SLIME_RS_QUEUE sets the
+// initial value; slime_rs_kernel_schedule() switches it.
+static std::atomic<int> g_queue_mode{[] {
+  const char* e = getenv("SLIME_RS_QUEUE");
+  const int v = e ? atoi(e) : 1;
+  return v >= 0 && v <= 2 ? v : 1;
+}()};
+int queue_mode() { return g_queue_mode.load(std::memory_order_relaxed); }
+void set_queue_mode(int m) { g_queue_mode.store(m, std::memory_order_relaxed); }
 void set_pipelined_kernels(bool on) { g_pipelined.store(on ? 1 : 0, std::memory_order_relaxed); }
 
 namespace {
@@ -174,7 +256,13 @@ bool pipe_ok(const ApplyLaunch& a) { return pipelined_kernels() && a.ncols < (1u
 template <int K>
 hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   if (!a.vec_ok) return launch_k<K, false>(a, s);
-  return pipe_ok(a) ? launch_pipe<K>(a, s) : launch_k<K, true>(a, s);
+  if (!pipe_ok(a)) return launch_k<K, true>(a, s);
+  if (queue_on<K>()) {
+    bool launched = false;
+    const hipError_t e = launch_queue<K>(a, s, &launched);
+    if (launched || e != hipSuccess) return e;
+  }
+  return launch_pipe<K>(a, s);
 }
 
 // k > 16: rs_apply_wide_kernel -- all inputs in registers with 8-row blocks

@@ -341,6 +341,135 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
   }
 }
 
+// ---- dynamic schedule -------------------------------------------------------
+// rs_apply_pipe_kernel hands every wave a fixed share of the batch.  The eight
+// XCDs do not stream at the same rate (C3 on one box: waves on the odd XCDs
+// finished 4% after those on the even ones, so 3.3% of the launch's wave-time
+// was idle tail; tools/apply_variants.py --timed, profiles/r02/s36_tail/).
+// Here waves take work from ticket counters instead, so fast XCDs take more.
+//
+// Units: an object's tiles are cut into groups of 4*C consecutive tiles; unit
+// = (group, sub) walks tiles grp*4C + sub + 4i, i < C.  The waves that take
+// four consecutive tickets sweep one 4C-tile window of one object together --
+// as a block's four waves do in the static walk.  Group g belongs to object
+// g % nobj (group g / nobj within it), so the groups running at any moment
+// spread over all objects.
+//
+// Tickets: one device-scope counter serialises at ~12 ns per atomic (C = 1:
+// 1.4M tickets took 16.6 ms at C3), so the groups are dealt over NC counters
+// (partition p owns groups g = p (mod NC)), each on its own 256-byte line.  A
+// wave draws from its XCD's partition and, once that is exhausted, from the
+// next ones in turn; a wave is done when all NC have run dry.  Counters are
+// zero at launch: the host alternates two counter sets per stream, and each
+// launch zeroes the set the next launch on its stream will use
+// (`zero_next`; the previous launch that used it has finished by stream
+// order).  The ticket for a wave's next unit is requested when it
+// enters a unit and read one unit later, so its latency is hidden (the
+// compiler still waits vmcnt(0) before reading it: atomics and loads share the
+// counter).
+constexpr uint32_t kTicketStride = 64;  // words between counters
+
+__device__ __forceinline__ uint32_t hw_xcc_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xF;
+}
+
+template <int K, int U, int C, int NC, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next) {
+  static_assert(K > 0 && NC > 0 && NC <= 64, "compile-time k only");
+  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * kTicketStride] = 0;
+  // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  const uint32_t ngrp_all = nobj * ((ntiles + 4 * C - 1) / (4 * C));
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t ioff[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
+
+  // Walk state (wave-uniform): partition p, partitions found dry, current unit.
+  uint32_t p = hw_xcc_id() % NC, dry = 0;
+  uint32_t obj = 0, tb = 0, cnt = 0, i = 0;
+  bool live = true;
+  uint32_t pend = 0;
+  auto request = [&] {
+    pend = 0;
+    if (lane == 0) pend = atomicAdd(ticket + p * kTicketStride, 1u);
+  };
+  // Enter the unit of the pending ticket (or of later ones: exhausted
+  // partitions and empty sub-units are skipped) and request the next ticket.
+  auto next_unit = [&] {
+    for (;;) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane(pend);
+      const uint32_t units = 4 * ((ngrp_all + NC - 1 - p) / NC);
+      if (l >= units) {
+        if (++dry == NC) {
+          live = false;
+          return;
+        }
+        p = p + 1 == NC ? 0 : p + 1;
+        request();
+        continue;
+      }
+      request();
+      const uint32_t g = (l >> 2) * NC + p;
+      obj = g % nobj;
+      tb = (g / nobj) * (4 * C) + (l & 3);
+      i = 0;
+      cnt = tb < ntiles ? (ntiles - tb + 3) / 4 : 0;
+      if (cnt > C) cnt = C;
+      if (cnt) return;
+    }
+  };
+  request();
+  next_unit();
+  auto load = [&](uint4(&x)[U][K], uint32_t o, uint32_t t) {
+    const uint32_t* base = in + (uint64_t)o * in_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = base + ioff[j];
+    load_tile<K, U, NTL>(x, sb, t * (64 * U) + lane, nvec);
+  };
+  auto store = [&](const uint4(&x)[U][K], uint32_t o, uint32_t t) {
+    store_tile<K, U, NTS>(x, out + (uint64_t)o * out_obj_stride, coeff, out_idx, out_shard, rows, t * (64 * U) + lane,
+                          nvec);
+  };
+  if (live) {
+    uint4 xa[U][K], xb[U][K];
+    load(xa, obj, tb);
+    for (;;) {
+      uint32_t co = obj, ct = tb + 4 * i;
+      if (++i >= cnt) next_unit();
+      // Past the last unit the prefetch re-reads the current tile (unconditional loads, see load_tile).
+      load(xb, live ? obj : co, live ? tb + 4 * i : ct);
+      store(xa, co, ct);
+      if (!live) break;
+      co = obj;
+      ct = tb + 4 * i;
+      if (++i >= cnt) next_unit();
+      load(xa, live ? obj : co, live ? tb + 4 * i : ct);
+      store(xb, co, ct);
+      if (!live) break;
+    }
+  }
+  // Columns past the last whole vector of each object, one per lane.
+  const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
+  if (tailc) {
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t t = tid; t < (uint64_t)nobj * tailc; t += nthr) {
+      const uint64_t o = t / tailc;
+      apply_column<K>(in + o * in_obj_stride, out + o * out_obj_stride, coeff, in_idx, in_shard, out_idx, out_shard,
+                      rows, k, ((uint64_t)nvec << 2) + t % tailc);
+    }
+  }
+}
+
 // ---- wide k, software-pipelined ------------------------------------------
 // A wave's work is a stream of items (tile, row block rb, input chunk jc):
 // one 64-vector tile per step, row blocks of RB rows, chunks of 16 input

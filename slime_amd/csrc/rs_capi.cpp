@@ -786,6 +786,13 @@ int slime_rs_kernel_pipeline(int mode) {
   return 0;
 }
 
+int slime_rs_kernel_schedule(int mode) {
+  if (mode < 0) return queue_mode();
+  if (mode > 2) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0, 1 or 2");
+  set_queue_mode(mode);
+  return 0;
+}
+
 int slime_rs_select_device(int device) {
   if (device != SLIME_RS_ANY_DEVICE)
     if (int rc = check_device(device)) return rc;

@@ -45,6 +45,6 @@ def test_committed_traffic_matches_shipped_kernel_source():
     tj = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")))
     assert tj["kernel_source"] == bench.kernel_source_id(), \
         "apply kernel changed since its PMC passes: re-run tools/gpu_r02.sh pmc_fetch pmc_write"
-    assert tj["config"] == "8/12 L=8388608 nobj=128" and tj["kernel"] == "rs_apply_pipe_kernel"
+    assert tj["config"] == "8/12 L=8388608 nobj=128" and tj["kernel"] == "rs_apply_queue_kernel"
     alg = 128 * 4 * 8388608 * 12
     assert abs(tj["hbm_bytes_per_launch"] / alg - 1) < 0.01  # no wasted re-reads

@@ -1,0 +1,154 @@
+"""GPU parity of the apply kernels' work schedules (slime_rs_kernel_schedule):
+static shares per wave (rs_apply_pipe_kernel) and the dynamic ticket schedule
+(rs_apply_queue_kernel), both against the C oracle (applyMatrix,
+internal/rs/vector.go:90-102) and against each other, bit-exact.
+
+The dynamic schedule deals units of tiles over eight ticket counters; the cases
+here cover units that straddle object ends, empty sub-units, objects shorter
+than one tile (only column tails), many objects per counter, and consecutive
+launches on one stream and on two streams (each launch zeroes the counter set
+the next launch on its stream uses).
+"""
+import numpy as np
+import pytest
+
+from slime_amd import _native as N
+from slime_amd import gf
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+P = gf.MaxVal
+EDGES = np.array([0, 1, P - 1, P, P + 4, 0xFFFFFFFF, 0x80000000], dtype=np.uint32)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch
+
+
+@pytest.fixture
+def schedule():
+    before = N.lib.slime_rs_kernel_schedule(-1)
+    yield lambda m: N.lib.slime_rs_kernel_schedule(m)
+    N.lib.slime_rs_kernel_schedule(before)
+
+
+def _objects(rng, nobj, total, L):
+    h = rng.integers(0, 2**32, size=(nobj, total, L), dtype=np.uint64).astype(np.uint32)
+    flat = h.reshape(-1)
+    n = min(flat.size, 64)
+    flat[rng.choice(flat.size, size=n, replace=False)] = np.resize(EDGES, n)
+    return h
+
+
+def _encode_ref(h, need, total):
+    ref = h.copy()
+    for o in range(ref.shape[0]):
+        obj = np.ascontiguousarray(ref[o])
+        OC.encode_object(obj, need, total)
+        ref[o] = obj
+    return ref
+
+
+def test_schedule_switch_rejects_unknown_modes(schedule):
+    assert schedule(-1) in (0, 1, 2)
+    for m in (0, 1, 2):
+        assert schedule(3) != 0 and schedule(-1) in (0, 1, 2)
+        assert schedule(m) == 0 and schedule(-1) == m
+
+
+@pytest.mark.parametrize("need,total", [(1, 2), (3, 5), (4, 6), (5, 8), (8, 12), (10, 14), (12, 16), (13, 17),
+                                        (16, 20)])
+@pytest.mark.parametrize("L,nobj", [(1, 3), (3, 2), (4, 5), (191, 3), (768 + 4, 9), (6 * 768 * 4 + 17, 7),
+                                    (65536 + 3, 2)])
+def test_encode_every_schedule_vs_oracle(torch_dev, schedule, need, total, L, nobj):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(need * 1000 + L + nobj)
+    h = _objects(rng, nobj, total, L)
+    ref = _encode_ref(h, need, total)
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    outs = []
+    for m in (0, 2, 1):
+        assert schedule(m) == 0
+        buf = torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda()
+        plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+        assert np.array_equal(got, ref), m
+        outs.append(got)
+
+
+@pytest.mark.parametrize("need,total,erase", [(8, 12, [0, 1, 2, 3]), (8, 12, [0, 3, 8, 11]), (10, 14, [1, 12]),
+                                              (4, 6, [0, 5])])
+def test_reconstruct_every_schedule_vs_oracle(torch_dev, schedule, need, total, erase):
+    torch = torch_dev
+    from slime_amd import device as D
+    nobj, L = 11, 4 * 768 * 3 + 9
+    rng = np.random.default_rng(sum(erase) + need)
+    h = _encode_ref(_objects(rng, nobj, total, L), need, total)
+    have = [i for i in range(total) if i not in erase][:need]
+    rec = D.Plan.reconstruct(need, total, have, erase)
+    for m in (0, 2, 1):
+        assert schedule(m) == 0
+        src = torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda()
+        out = torch.zeros(nobj * len(erase) * L, dtype=torch.int32, device="cuda")
+        rec(src, D.layout_of(total, L), out, D.layout_of(len(erase), L), L, nobj)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32).reshape(nobj, len(erase), L)
+        for i, t in enumerate(erase):
+            # RecoverData yields canonical residues; the inputs hold symbols >= p.
+            assert np.array_equal(got[:, i], (h[:, t].astype(np.uint64) % P).astype(np.uint32)), (m, t)
+
+
+def test_consecutive_launches_one_stream_and_two_streams(torch_dev, schedule):
+    """Each launch zeroes the counter set of the next launch on its stream:
+    back-to-back launches of different sizes on one stream, and two streams
+    interleaved, all exact."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total = 8, 12
+    plan = D.Plan.encode(need, total)
+    assert schedule(1) == 0
+    rng = np.random.default_rng(7)
+    cases = [(5, 3 * 768 * 4 + 1), (1, 1000), (17, 2 * 768 * 4), (2, 7), (9, 768 * 4 * 5 + 33)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(2):
+        bufs = []
+        for ci, (nobj, L) in enumerate(cases):
+            h = _objects(rng, nobj, total, L)
+            buf = torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda()
+            torch.cuda.synchronize()
+            s = streams[ci % 2] if rep else torch.cuda.current_stream()
+            plan(buf, D.layout_of(total, L), buf, D.layout_of(total, L), L, nobj, stream=s, dst_offset=need * L)
+            bufs.append((h, buf, nobj, L))
+        torch.cuda.synchronize()
+        for h, buf, nobj, L in bufs:
+            got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+            assert np.array_equal(got, _encode_ref(h, need, total)), (rep, nobj, L)
+
+
+def test_dynamic_schedule_full_batch_matches_static(torch_dev, schedule):
+    """A C3-sized launch (8/12, 128 x 256 MiB) under both schedules: identical
+    parity shards (compared on the device)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, nobj = 8, 12, 128
+    L = (256 << 20) // 4 // need
+    lay = D.layout_of(total, L)
+    buf = torch.empty(nobj * total * L, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, seed=11)
+    plan = D.Plan.encode(need, total)
+    first = None
+    for m in (0, 1):
+        assert schedule(m) == 0
+        buf.view(nobj, total, L)[:, need:].zero_()
+        plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+        if first is None:
+            first = buf.view(nobj, total, L)[:, need:].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(first, buf.view(nobj, total, L)[:, need:])

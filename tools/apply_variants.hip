@@ -215,7 +215,105 @@ __global__ __launch_bounds__(kBlock) void batched_kernel(const uint32_t* __restr
     }
   }
 }
+// The product's pipelined walk (rs_apply_pipe_kernel<K,U,true,true>) with a
+// per-wave record of when it started, when it issued its last store, which
+// XCD it ran on and how many tiles it walked: is the launch's tail (waves
+// idle while others finish) worth a dynamic schedule?
+struct WaveStamp {
+  uint64_t t0, t1;
+  uint32_t xcc, tiles;
+};
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xF;
+}
+template <int K, int U>
+__global__ __launch_bounds__(kBlock) void timed_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       uint64_t in_obj_stride, uint64_t in_shard,
+                                                       uint64_t out_obj_stride, uint64_t out_shard,
+                                                       const uint32_t* __restrict__ coeff,
+                                                       const uint32_t* __restrict__ in_idx,
+                                                       const uint32_t* __restrict__ out_idx, uint64_t ncols,
+                                                       uint32_t nobj, uint32_t rows, uint32_t nseg,
+                                                       WaveStamp* __restrict__ stamps) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t seg_vec = segment_vectors(nvec, nseg);
+  const uint64_t nwork = (uint64_t)nobj * nseg;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  uint32_t walked = 0;
+  for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
+    const uint64_t obj = wi / nseg;
+    const uint32_t seg = (uint32_t)(wi % nseg);
+    const uint32_t* __restrict__ ib = in + obj * in_obj_stride;
+    uint32_t* __restrict__ ob = out + obj * out_obj_stride;
+    const uint32_t* sb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sb[j] = ib + (uint64_t)in_idx[j] * in_shard;
+    const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
+    const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
+    const uint32_t ntiles = (v1 - v0 + 64 * U - 1) / (64 * U);
+    uint4 xa[U][K], xb[U][K];
+    uint32_t step = wave;
+    if (step < ntiles) load_tile<K, U, true>(xa, sb, v0 + step * (64 * U) + lane, v1);
+    while (step < ntiles) {
+      uint32_t next = step + nwaves;
+      load_tile<K, U, true>(xb, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, true>(xa, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      ++walked;
+      step = next;
+      if (step >= ntiles) break;
+      next = step + nwaves;
+      load_tile<K, U, true>(xa, sb, v0 + (next < ntiles ? next : step) * (64 * U) + lane, v1);
+      store_tile<K, U, true>(xb, ob, coeff, out_idx, out_shard, rows, v0 + step * (64 * U) + lane, v1);
+      ++walked;
+      step = next;
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    const uint32_t w = (blockIdx.y * gridDim.x + blockIdx.x) * kWaves + (threadIdx.x >> 6);
+    WaveStamp st;
+    st.t0 = t0;
+    st.t1 = t1;
+    st.xcc = xcc_id();
+    st.tiles = walked;
+    stamps[w] = st;
+  }
+}
 }  // namespace
+
+// Product walk with per-wave stamps (k = 8, U = 3); stamps: gx*gy*4 records.
+extern "C" int av_launch_timed(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os,
+                               const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi, uint64_t ncols,
+                               uint32_t nobj, uint32_t rows, uint32_t gx, uint32_t gy, void* stream, uint32_t nseg,
+                               void* stamps) {
+  hipLaunchKernelGGL((timed_kernel<8, 3>), dim3(gx, gy), dim3(kBlock), 0, (hipStream_t)stream, in, out, io, is, oo, os,
+                     coeff, ii, oi, ncols, nobj, rows, nseg, (WaveStamp*)stamps);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Dynamic-schedule walk (rs_apply_queue_kernel<K, 3, C, NC>), k = 8 or 10; C argument = C + 100 * NC;
+// tickets (NC x 64 words) zeroed by the caller.
+extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
+                               uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
+                               uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t blocks, void* stream,
+                               void* ticket) {
+  hipStream_t s = (hipStream_t)stream;
+#define Q(KK, CC, NN)                                                                                              \
+  if (k == KK && C == CC + 100 * NN) {                                                                             \
+    hipLaunchKernelGGL((rs_apply_queue_kernel<KK, 3, CC, NN, true, true>), dim3(blocks), dim3(kBlock), 0, s, in, out, \
+                       io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, (uint32_t*)ticket,   \
+                       (uint32_t*)ticket + 16 * kTicketStride);         \
+    return hipGetLastError() == hipSuccess ? 0 : -3;                                                              \
+  }
+  Q(8, 4, 1) Q(8, 1, 8) Q(8, 2, 8) Q(8, 4, 8) Q(8, 8, 8) Q(8, 2, 16) Q(8, 4, 16) Q(10, 2, 8) Q(10, 4, 8)
+#undef Q
+  return -2;
+}
 
 extern "C" int av_launch_batched(int U, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                  uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,

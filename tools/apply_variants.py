@@ -27,6 +27,7 @@ import torch  # noqa: E402
 from slime_amd import device as D  # noqa: E402
 
 BATCHED: dict = {}  # variant id -> U
+QUEUE: dict = {}  # variant id -> tiles per wave unit (C)
 BURST: dict = {}  # variant id -> tiles per store burst
 PHASED: dict = {}  # variant id -> (U, period ticks, read-window ticks)
 ALL_VARIANTS = {0: "U1 ntL", 1: "U1 plain", 2: "U1 ntL ntS", 3: "U1 ntS", 4: "U2 ntL", 5: "U2 plain",
@@ -57,7 +58,12 @@ def main():
     ap.add_argument("--pipek", type=str, default="", help="k > 16 through the pipelined k-template kernel: U list")
     ap.add_argument("--wide", type=int, default=0, help="k > 16: time the wide kernel with field math (500) and XOR (501)")
     ap.add_argument("--batched", type=str, default="", help="register-batched stores: U list (2,3)")
+    ap.add_argument("--queue", type=str, default="",
+                    help="dynamic-schedule walk (rs_apply_queue_kernel, U3): C + 100 * NC (tiles per wave unit, "
+                         "ticket counters), comma list, e.g. 104,802,804")
     ap.add_argument("--burst", type=str, default="", help="LDS-staged write bursts: tiles per burst, comma list (1..3)")
+    ap.add_argument("--timed", type=int, default=0,
+                    help="also run the product walk with per-wave stamps N times per geometry (k = 8, U = 3): tail report")
     ap.add_argument("--separate", type=int, default=-1,
                     help="1: write to a separate buffer, 0: in place (default: encode in place, decode separate)")
     args = ap.parse_args()
@@ -77,6 +83,9 @@ def main():
         VARIANTS[501] = "wide pipe, XOR stand-in (wrong by design)"
     for u in (int(x) for x in args.pipek.split(",") if x):
         VARIANTS[700 + u] = f"pipe K={args.need} U{u} (k-template kernel)"
+    for c in (int(x) for x in args.queue.split(",") if x):
+        QUEUE[400 + c] = c
+        VARIANTS[400 + c] = f"queue U3 C{c % 100} NC{c // 100} (dynamic schedule)"
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
@@ -101,6 +110,14 @@ def main():
     lib.av_launch_phased.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                  ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    lib.av_launch_queue.restype = ctypes.c_int
+    lib.av_launch_queue.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                 ctypes.c_void_p]
+    lib.av_launch_timed.restype = ctypes.c_int
+    lib.av_launch_timed.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+         ctypes.c_uint32, ctypes.c_void_p]
     lib.av_launch.restype = ctypes.c_int
     lib.av_launch.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -177,6 +194,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
         d_ptr, oo = buf.data_ptr(), total * SS
         view = lambda: shards()[:, slot0:slot0 + r, :]  # noqa: E731
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
+    ticket = torch.zeros(32 * 64, dtype=torch.int32, device="cuda")  # counters + the zero_next set
 
     def launch(v, gx, gy, nseg=1):
         if 700 <= v < 800:
@@ -189,6 +207,13 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
             rc = lib.av_launch_wide(int(v == 500), buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                                     ii.data_ptr(), oi.data_ptr(), L, nobj, r, need, gx, gy,
                                     ctypes.c_void_p(s.cuda_stream), nseg)
+            assert rc == 0, rc
+            return
+        if v in QUEUE:
+            ticket.zero_()
+            rc = lib.av_launch_queue(QUEUE[v], need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
+                                     ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx * gy,
+                                     ctypes.c_void_p(s.cuda_stream), ticket.data_ptr())
             assert rc == 0, rc
             return
         if v in BATCHED:
@@ -245,6 +270,51 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
             if not torch.equal(view(), ref):
                 bad.append((v, ns))
     alg = nobj * 4 * L * total
+    tails = []
+    if args.timed:
+        assert need == 8, "timed walk is built for k = 8"
+        for t, y, ns in geos:
+            gx = max(1, t // y)
+            nw = gx * y * 4
+            st = torch.zeros(nw * 3, dtype=torch.int64, device="cuda")  # {t0, t1, xcc | tiles << 32}
+            for it in range(args.timed):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                rc = lib.av_launch_timed(buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(), ii.data_ptr(),
+                                         oi.data_ptr(), L, nobj, r, gx, y, ctypes.c_void_p(s.cuda_stream), ns,
+                                         st.data_ptr())
+                assert rc == 0, rc
+                b.record(s)
+                torch.cuda.synchronize()
+                if it < args.timed - 1:
+                    continue
+                ms = a.elapsed_time(b)
+                rec = st.view(nw, 3).cpu().numpy()
+                t0, t1 = rec[:, 0].astype(np.float64), rec[:, 1].astype(np.float64)
+                xcc = (rec[:, 2] & 0xFFFFFFFF).astype(np.int64)
+                tiles = (rec[:, 2] >> 32).astype(np.int64)
+                base = t0.min()
+                end = (t1 - base) / 100.0  # 100 MHz ticks -> us
+                span = end.max()
+                per_xcc = {int(x): {"waves": int((xcc == x).sum()), "end_med_us": round(float(np.median(end[xcc == x])), 1),
+                                    "end_max_us": round(float(end[xcc == x].max()), 1)} for x in sorted(set(xcc.tolist()))}
+                tails.append({"blocks": t, "objects_in_flight": y, "nseg": ns, "event_ms": round(ms, 3),
+                              "start_spread_us": round(float((t0.max() - base) / 100.0), 1),
+                              "end_us": {q: round(float(np.percentile(end, p)), 1)
+                                         for q, p in (("min", 0), ("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
+                              "idle_frac": round(float((span - end).sum() / (len(end) * span)), 4),
+                              "tiles": [int(tiles.min()), int(tiles.max())], "per_xcc": per_xcc})
+            view().zero_()
+            launch(15, 4, 8, ns)
+            torch.cuda.synchronize()
+            good = view().clone()
+            view().zero_()
+            rc = lib.av_launch_timed(buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(), ii.data_ptr(),
+                                     oi.data_ptr(), L, nobj, r, 1, 8, ctypes.c_void_p(s.cuda_stream), ns,
+                                     torch.zeros(8 * 4 * 3, dtype=torch.int64, device="cuda").data_ptr())
+            torch.cuda.synchronize()
+            if not torch.equal(view(), good):
+                bad.append(("timed", ns))
     rows = []
     for (v, (t, y, ns)), ts in times.items():
         med = statistics.median(ts)
@@ -252,7 +322,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
                      "GBps": round(alg / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: -x["GBps"])
     return {"separate": int(args.separate if args.separate >= 0 else separate), "bad_variants": bad,
-            "top": rows[:12], "all": rows}
+            "top": rows[:12], "all": rows, "tails": tails}
 
 
 if __name__ == "__main__":

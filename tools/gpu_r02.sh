@@ -105,6 +105,25 @@ for step in "$@"; do
     hostdiag2) run hostdiag2 600 python tools/host_diag.py --threads 4 --pre bench &&
                run hostdiag3 600 python tools/host_diag.py --threads 4 --pre none &&
                run bench_hostonly 300 python bench.py --cpu-baseline 0 --bytes-path 0 ;;
+    tail) run tail_enc 300 python tools/apply_variants.py --variants 15 --blocks 256,512 --nseg 1,2,4 --rounds 3 --timed 3 &&
+          run tail_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 3 --timed 3 ;;
+    queue) run queue_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 4,8,16 &&
+           run queue_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 4,8,16 &&
+           run queue_blocks 300 python tools/apply_variants.py --variants 15 --blocks 256,512,1024 --nseg 2 --rounds 3 --queue 8,16 ;;
+    queue2) run queue2_enc 300 python tools/apply_variants.py --variants 15 --blocks 256,512 --nseg 2 --rounds 5 --queue 1,2,4,104,108 &&
+            run queue2_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 1,2,4,104 ;;
+    queue3) run queue3_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 104,801,802,804,808,1602,1604 &&
+            run queue3_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 104,801,802,804,1602 ;;
+    qab) for q in 0 1; do
+           run qab_c3_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+           run qab_ns64_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+           run qab_c5_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
+         done
+         for q in 0 2; do
+           run qab_c2_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+           run qab_k16_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 16 --total 20 --objects 64 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+           run qab_k3_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 3 --total 5 --objects 64 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
+         done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -28,7 +28,7 @@ def kernel_source_id() -> str:
     return h.hexdigest()[:16]
 
 
-KERNELS = ("rs_apply_pipe_kernel", "rs_apply_kernel")  # product apply kernels (rs_apply.hip)
+KERNELS = ("rs_apply_queue_kernel", "rs_apply_pipe_kernel", "rs_apply_kernel")  # product apply kernels (rs_apply.hip)
 
 
 def per_dispatch(d, counter):
