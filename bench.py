@@ -580,12 +580,11 @@ def main():
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
     # The product dispatch (rs_apply.hip): the pipelined kernels for shards
     # under 4 GiB unless the kernel form was switched (slime_rs_kernel_pipeline),
-    # with the dynamic (ticket) schedule for the k range slime_rs_kernel_schedule
-    # selects.
+    # with the dynamic (ticket) schedule for k <= 16 unless slime_rs_kernel_schedule
+    # switched it off.
     kname = "rs_apply_kernel"
     if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
-        sched = D.lib.slime_rs_kernel_schedule(-1)
-        queue = need <= 16 and (sched == 2 or (sched == 1 and 5 <= need <= 12))
+        queue = need <= 16 and D.lib.slime_rs_kernel_schedule(-1) == 1
         kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such

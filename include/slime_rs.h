@@ -100,10 +100,9 @@ int slime_rs_host_pipeline(int mode);
  * Results are identical; the parity tests run both. */
 int slime_rs_kernel_pipeline(int mode);
 /* Work schedule of the pipelined apply kernels for k <= 16 (process-wide; env
- * SLIME_RS_QUEUE sets the initial value): 1 = dynamic (ticket counters) for
- * 5 <= k <= 12, the measured range (default); 0 = static shares for every k;
- * 2 = dynamic for every k <= 16.  mode < 0 queries.  Results are identical;
- * the parity tests run each schedule. */
+ * SLIME_RS_QUEUE=0 sets the initial value): 1 = dynamic, waves take units of
+ * work from ticket counters (default); 0 = static shares per wave.  mode < 0
+ * queries.  Results are identical; the parity tests run both. */
 int slime_rs_kernel_schedule(int mode);
 
 /* ==== internal/rs/gf ===================================================== */

@@ -53,8 +53,8 @@ bool k32_kernels();
 // not (the form larger ones always take).  Process-wide; see rs_apply.hip.
 bool pipelined_kernels();
 void set_pipelined_kernels(bool on);
-// Dynamic schedule of the k <= 16 pipelined apply kernels: 0 none, 1 the
-// default k range (5..12), 2 every k <= 16.  Process-wide; see rs_apply.hip.
+// Work schedule of the k <= 16 pipelined apply kernels: 1 dynamic (ticket
+// counters, default), 0 static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
 

@@ -155,22 +155,24 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
 }
 
 // Dynamic schedule (rs_apply_queue_kernel): tickets instead of a fixed share
-// per wave, so the XCDs that stream faster take more of the batch.  In-process
-// A/B against rs_apply_pipe_kernel<8,3> at C3 (profiles/r02/s39_queue3/):
-// encode 8.568 -> 8.295 ms, decode 8.441 -> 8.239 on a fast-placement
-// allocation; 9.915 -> 9.376 / 9.857 -> 9.341 on a slow one
-// (profiles/r02/s37_queue/).  A unit is C tiles of U KiB per stream (C x U
-// about 6), dealt over kQueueCounters ticket counters.
+// per wave, so the XCDs that stream faster take more of the batch (the static
+// walk left 3.4% of C3's wave-time idle behind the four slower XCDs; the
+// dynamic one 0.1%, profiles/r02/s41_queue4/).  In-process A/B against the
+// static kernel's best geometry: C3 encode 8.568 -> 8.295 ms, decode 8.441 ->
+// 8.239 on a fast-placement allocation and 9.79 -> 9.33 on a slow one
+// (s39_queue3/, s41_queue4/); 16/20 3.737 -> 3.600, C2 (4/6) 0.586 -> 0.575
+// (s42_queuek/).  Geometry: 256 blocks (one per CU) for every k; U = 4 up to
+// k = 4, 3 up to 12, 1 above; a unit is C tiles with C x U about 6 (C = 2 at
+// U >= 3), dealt over kQueueCounters ticket counters.
 constexpr int kQueueCounters = 8;
+constexpr uint64_t kQueueBlocks = 256;
+template <int K>
+constexpr int queue_unroll() {
+  return K <= 4 ? 4 : K <= 12 ? 3 : 1;
+}
 template <int K>
 constexpr int queue_unit_tiles() {
-  return pipe_unroll<K>() >= 6 ? 1 : 6 / pipe_unroll<K>();
-}
-
-template <int K>
-bool queue_on() {
-  const int m = queue_mode();
-  return m == 2 || (m == 1 && K >= 5 && K <= 12);
+  return queue_unroll<K>() >= 3 ? 2 : 6 / queue_unroll<K>();
 }
 
 // Two ticket-counter sets per (device, stream): a launch draws from set
@@ -190,7 +192,7 @@ std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
 
 template <int K>
 hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched) {
-  constexpr int U = pipe_unroll<K>();
+  constexpr int U = queue_unroll<K>();
   constexpr int C = queue_unit_tiles<K>();
   *launched = false;
   const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
@@ -212,11 +214,11 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
     ts.base = (uint32_t*)p;
   }
   const Geometry& geo = geometry();
-  const uint64_t blocks = geo.target ? geo.target : pipe_blocks<K>();
+  const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
   hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
                      dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
                      a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k,
-                     ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words);
+                     ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words, nullptr);
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess) ts.parity ^= 1;  // a launch that never started zeroed nothing
   *launched = true;
@@ -235,13 +237,12 @@ static std::atomic<int> g_pipelined{[] {
   return e && e[0] == '0' ? 0 : 1;
 }()};
 bool pipelined_kernels() { return g_pipelined.load(std::memory_order_relaxed) != 0; }
-// Which k take the dynamic schedule (process-wide): 1 = 5..12 (default, the
-// measured ones), 0 = none, 2 = every k <= 16.  Env SLIME_RS_QUEUE sets the
-// initial value; slime_rs_kernel_schedule() switches it.
+// Work schedule of the k <= 16 pipelined kernels (process-wide): 1 = dynamic
+// (default), 0 = static shares.  Env SLIME_RS_QUEUE=0 sets the initial value;
+// slime_rs_kernel_schedule() switches it.
 static std::atomic<int> g_queue_mode{[] {
   const char* e = getenv("SLIME_RS_QUEUE");
-  const int v = e ? atoi(e) : 1;
-  return v >= 0 && v <= 2 ? v : 1;
+  return e && e[0] == '0' ? 0 : 1;
 }()};
 int queue_mode() { return g_queue_mode.load(std::memory_order_relaxed); }
 void set_queue_mode(int m) { g_queue_mode.store(m, std::memory_order_relaxed); }
@@ -257,7 +258,7 @@ template <int K>
 hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   if (!a.vec_ok) return launch_k<K, false>(a, s);
   if (!pipe_ok(a)) return launch_k<K, true>(a, s);
-  if (queue_on<K>()) {
+  if (queue_mode() == 1) {
     bool launched = false;
     const hipError_t e = launch_queue<K>(a, s, &launched);
     if (launched || e != hipSuccess) return e;

@@ -375,13 +375,20 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
   return v & 0xF;
 }
 
-template <int K, int U, int C, int NC, bool NTL, bool NTS>
+// Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
+// per atomic (a wave takes TB consecutive units at a time); STAMP records per
+// wave {start, end, XCD | tiles << 32} (s_memrealtime ticks) into `stamps`.
+template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false>
 __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
-    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next) {
-  static_assert(K > 0 && NC > 0 && NC <= 64, "compile-time k only");
+    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
+    uint64_t* __restrict__ stamps) {
+  static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
+  uint64_t t_start = 0;
+  uint32_t walked = 0;
+  if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * kTicketStride] = 0;
   // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
   const uint32_t nvec = (uint32_t)(ncols >> 2);
@@ -396,16 +403,26 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
   uint32_t p = hw_xcc_id() % NC, dry = 0;
   uint32_t obj = 0, tb = 0, cnt = 0, i = 0;
   bool live = true;
-  uint32_t pend = 0;
+  uint32_t pend = 0, bl = 0, bn = 0;  // pending atomic; rest of the current ticket batch (TB > 1)
   auto request = [&] {
     pend = 0;
-    if (lane == 0) pend = atomicAdd(ticket + p * kTicketStride, 1u);
+    if (lane == 0) pend = atomicAdd(ticket + p * kTicketStride, (uint32_t)TB);
   };
   // Enter the unit of the pending ticket (or of later ones: exhausted
   // partitions and empty sub-units are skipped) and request the next ticket.
   auto next_unit = [&] {
     for (;;) {
-      const uint32_t l = __builtin_amdgcn_readfirstlane(pend);
+      uint32_t l;
+      bool fresh = true;
+      if (TB > 1 && bn) {
+        l = bl++;
+        --bn;
+        fresh = false;
+      } else {
+        l = __builtin_amdgcn_readfirstlane(pend);
+        bl = l + 1;
+        bn = TB - 1;
+      }
       const uint32_t units = 4 * ((ngrp_all + NC - 1 - p) / NC);
       if (l >= units) {
         if (++dry == NC) {
@@ -413,10 +430,11 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
           return;
         }
         p = p + 1 == NC ? 0 : p + 1;
-        request();
+        bn = 0;
+        if (fresh) request();  // else the batch's successor is already pending
         continue;
       }
-      request();
+      if (fresh) request();
       const uint32_t g = (l >> 2) * NC + p;
       obj = g % nobj;
       tb = (g / nobj) * (4 * C) + (l & 3);
@@ -444,6 +462,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     load(xa, obj, tb);
     for (;;) {
       uint32_t co = obj, ct = tb + 4 * i;
+      if constexpr (STAMP) ++walked;
       if (++i >= cnt) next_unit();
       // Past the last unit the prefetch re-reads the current tile (unconditional loads, see load_tile).
       load(xb, live ? obj : co, live ? tb + 4 * i : ct);
@@ -451,10 +470,20 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
       if (!live) break;
       co = obj;
       ct = tb + 4 * i;
+      if constexpr (STAMP) ++walked;
       if (++i >= cnt) next_unit();
       load(xa, live ? obj : co, live ? tb + 4 * i : ct);
       store(xb, co, ct);
       if (!live) break;
+    }
+  }
+  if constexpr (STAMP) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      uint64_t* r = stamps + 3 * ((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6));
+      r[0] = t_start;
+      r[1] = t_end;
+      r[2] = hw_xcc_id() | ((uint64_t)walked << 32);
     }
   }
   // Columns past the last whole vector of each object, one per lane.

@@ -788,7 +788,7 @@ int slime_rs_kernel_pipeline(int mode) {
 
 int slime_rs_kernel_schedule(int mode) {
   if (mode < 0) return queue_mode();
-  if (mode > 2) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0, 1 or 2");
+  if (mode > 1) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0 (static) or 1 (dynamic)");
   set_queue_mode(mode);
   return 0;
 }

@@ -296,22 +296,39 @@ extern "C" int av_launch_timed(const uint32_t* in, uint32_t* out, uint64_t io, u
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// Dynamic-schedule walk (rs_apply_queue_kernel<K, 3, C, NC>), k = 8 or 10; C argument = C + 100 * NC;
-// tickets (NC x 64 words) zeroed by the caller.
+// Dynamic-schedule walk (rs_apply_queue_kernel<K, 3, C, NC, .., TB, STAMP>), k = 8 or 10.
+// C argument = C + 100 * NC + 10000 * TB + 100000 * U (TB = tickets per atomic, 1 when 0; U = 3 when 0);
+// tickets (16 x 64 words, then the zero_next set) zeroed by the caller;
+// stamps (3 words per wave) recorded when non-null.
 extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
                                uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t blocks, void* stream,
-                               void* ticket) {
+                               void* ticket, void* stamps) {
   hipStream_t s = (hipStream_t)stream;
-#define Q(KK, CC, NN)                                                                                              \
-  if (k == KK && C == CC + 100 * NN) {                                                                             \
-    hipLaunchKernelGGL((rs_apply_queue_kernel<KK, 3, CC, NN, true, true>), dim3(blocks), dim3(kBlock), 0, s, in, out, \
-                       io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, (uint32_t*)ticket,   \
-                       (uint32_t*)ticket + 16 * kTicketStride);         \
-    return hipGetLastError() == hipSuccess ? 0 : -3;                                                              \
+  uint32_t* t = (uint32_t*)ticket;
+  uint32_t* z = t + 16 * kTicketStride;
+  if ((C / 10000) % 10 == 0) C += 10000;  // TB defaults to 1
+#define QU(KK, UU, CC, NN, TT)                                                                                   \
+  if (k == KK && C == CC + 100 * NN + 10000 * TT + 100000 * (UU == 3 ? 0 : UU)) {                              \
+    if (stamps)                                                                                                 \
+      hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, true>), dim3(blocks), dim3(kBlock), \
+                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
+                         (uint64_t*)stamps);                                                                    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, false>), dim3(blocks), dim3(kBlock), \
+                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
+                         nullptr);                                                                              \
+    return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
-  Q(8, 4, 1) Q(8, 1, 8) Q(8, 2, 8) Q(8, 4, 8) Q(8, 8, 8) Q(8, 2, 16) Q(8, 4, 16) Q(10, 2, 8) Q(10, 4, 8)
+#define Q(KK, CC, NN, TT) QU(KK, 3, CC, NN, TT)
+  Q(8, 4, 1, 1) Q(8, 1, 8, 1) Q(8, 2, 8, 1) Q(8, 4, 8, 1) Q(8, 8, 8, 1) Q(10, 2, 8, 1) Q(10, 4, 8, 1)
+  Q(8, 2, 8, 2) Q(8, 2, 8, 4) Q(8, 1, 8, 4) Q(8, 1, 8, 8)
+  // k = 4 (C2): U = 3, 2, 1
+  Q(4, 2, 8, 1) Q(4, 4, 8, 1) QU(4, 2, 3, 8, 1) QU(4, 1, 6, 8, 1) QU(4, 1, 12, 8, 1) QU(4, 4, 2, 8, 1)
+  // k = 16: U = 1, 2
+  QU(16, 1, 6, 8, 1) QU(16, 1, 12, 8, 1) QU(16, 2, 3, 8, 1)
 #undef Q
+#undef QU
   return -2;
 }
 

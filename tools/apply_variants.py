@@ -59,8 +59,8 @@ def main():
     ap.add_argument("--wide", type=int, default=0, help="k > 16: time the wide kernel with field math (500) and XOR (501)")
     ap.add_argument("--batched", type=str, default="", help="register-batched stores: U list (2,3)")
     ap.add_argument("--queue", type=str, default="",
-                    help="dynamic-schedule walk (rs_apply_queue_kernel, U3): C + 100 * NC (tiles per wave unit, "
-                         "ticket counters), comma list, e.g. 104,802,804")
+                    help="dynamic-schedule walk (rs_apply_queue_kernel, U3): C + 100 * NC + 10000 * TB (tiles per wave "
+                         "unit, ticket counters, tickets per atomic), comma list, e.g. 104,802,20802")
     ap.add_argument("--burst", type=str, default="", help="LDS-staged write bursts: tiles per burst, comma list (1..3)")
     ap.add_argument("--timed", type=int, default=0,
                     help="also run the product walk with per-wave stamps N times per geometry (k = 8, U = 3): tail report")
@@ -85,7 +85,8 @@ def main():
         VARIANTS[700 + u] = f"pipe K={args.need} U{u} (k-template kernel)"
     for c in (int(x) for x in args.queue.split(",") if x):
         QUEUE[400 + c] = c
-        VARIANTS[400 + c] = f"queue U3 C{c % 100} NC{c // 100} (dynamic schedule)"
+        VARIANTS[400 + c] = (f"queue U{c // 100000 or 3} C{c % 100} NC{c // 100 % 100} TB{max(1, c // 10000 % 10)} "
+                             "(dynamic schedule)")
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
@@ -113,7 +114,7 @@ def main():
     lib.av_launch_queue.restype = ctypes.c_int
     lib.av_launch_queue.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
-                                 ctypes.c_void_p]
+                                 ctypes.c_void_p, ctypes.c_void_p]
     lib.av_launch_timed.restype = ctypes.c_int
     lib.av_launch_timed.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p] * 3 + \
         [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
@@ -195,6 +196,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
         view = lambda: shards()[:, slot0:slot0 + r, :]  # noqa: E731
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
     ticket = torch.zeros(32 * 64, dtype=torch.int32, device="cuda")  # counters + the zero_next set
+    stamp_ptr = [None]  # queue variants record per-wave stamps here when set (--timed)
 
     def launch(v, gx, gy, nseg=1):
         if 700 <= v < 800:
@@ -213,7 +215,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
             ticket.zero_()
             rc = lib.av_launch_queue(QUEUE[v], need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                                      ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx * gy,
-                                     ctypes.c_void_p(s.cuda_stream), ticket.data_ptr())
+                                     ctypes.c_void_p(s.cuda_stream), ticket.data_ptr(), stamp_ptr[0])
             assert rc == 0, rc
             return
         if v in BATCHED:
@@ -271,6 +273,25 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
                 bad.append((v, ns))
     alg = nobj * 4 * L * total
     tails = []
+
+    def tail_report(label, geo, ms, rec):
+        t0, t1 = rec[:, 0].astype(np.float64), rec[:, 1].astype(np.float64)
+        xcc = (rec[:, 2] & 0xFFFFFFFF).astype(np.int64)
+        tiles = (rec[:, 2] >> 32).astype(np.int64)
+        base = t0.min()
+        end = (t1 - base) / 100.0  # 100 MHz ticks -> us
+        span = end.max()
+        per_xcc = {int(x): {"waves": int((xcc == x).sum()), "end_med_us": round(float(np.median(end[xcc == x])), 1),
+                            "end_max_us": round(float(end[xcc == x].max()), 1), "tiles": int(tiles[xcc == x].sum())}
+                   for x in sorted(set(xcc.tolist()))}
+        t, y, ns = geo
+        return {"variant": label, "blocks": t, "objects_in_flight": y, "nseg": ns, "event_ms": round(ms, 3),
+                "start_spread_us": round(float((t0.max() - base) / 100.0), 1),
+                "end_us": {q: round(float(np.percentile(end, p)), 1)
+                           for q, p in (("min", 0), ("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
+                "idle_frac": round(float((span - end).sum() / (len(end) * span)), 4),
+                "tiles": [int(tiles.min()), int(tiles.max())], "per_xcc": per_xcc}
+
     if args.timed:
         assert need == 8, "timed walk is built for k = 8"
         for t, y, ns in geos:
@@ -286,24 +307,22 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
                 assert rc == 0, rc
                 b.record(s)
                 torch.cuda.synchronize()
-                if it < args.timed - 1:
-                    continue
-                ms = a.elapsed_time(b)
-                rec = st.view(nw, 3).cpu().numpy()
-                t0, t1 = rec[:, 0].astype(np.float64), rec[:, 1].astype(np.float64)
-                xcc = (rec[:, 2] & 0xFFFFFFFF).astype(np.int64)
-                tiles = (rec[:, 2] >> 32).astype(np.int64)
-                base = t0.min()
-                end = (t1 - base) / 100.0  # 100 MHz ticks -> us
-                span = end.max()
-                per_xcc = {int(x): {"waves": int((xcc == x).sum()), "end_med_us": round(float(np.median(end[xcc == x])), 1),
-                                    "end_max_us": round(float(end[xcc == x].max()), 1)} for x in sorted(set(xcc.tolist()))}
-                tails.append({"blocks": t, "objects_in_flight": y, "nseg": ns, "event_ms": round(ms, 3),
-                              "start_spread_us": round(float((t0.max() - base) / 100.0), 1),
-                              "end_us": {q: round(float(np.percentile(end, p)), 1)
-                                         for q, p in (("min", 0), ("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
-                              "idle_frac": round(float((span - end).sum() / (len(end) * span)), 4),
-                              "tiles": [int(tiles.min()), int(tiles.max())], "per_xcc": per_xcc})
+                if it == args.timed - 1:
+                    tails.append(tail_report("pipe U3 (stamped)", (t, y, ns), a.elapsed_time(b),
+                                             st.view(nw, 3).cpu().numpy()))
+            for v in QUEUE:
+                st = torch.zeros(t * 4 * 3, dtype=torch.int64, device="cuda")
+                stamp_ptr[0] = st.data_ptr()
+                for it in range(args.timed):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(s)
+                    launch(v, gx, y, ns)
+                    b.record(s)
+                    torch.cuda.synchronize()
+                    if it == args.timed - 1:
+                        tails.append(tail_report(VARIANTS[v] + " (stamped)", (t, y, ns), a.elapsed_time(b),
+                                                 st.view(t * 4, 3).cpu().numpy()))
+                stamp_ptr[0] = None
             view().zero_()
             launch(15, 4, 8, ns)
             torch.cuda.synchronize()

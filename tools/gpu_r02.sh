@@ -124,6 +124,17 @@ for step in "$@"; do
            run qab_k16_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 16 --total 20 --objects 64 --erase 0,1,2,3 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
            run qab_k3_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 3 --total 5 --objects 64 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
          done ;;
+    queue4) run queue4_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 802,808,20802,40802,40801,80801 --timed 2 &&
+            run queue4_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 802,20802,40802,40801 ;;
+    queuek) run queuek_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13,14,15 --blocks 256,512 --nseg 8 --rounds 5 --queue 802,804,200803,100806,100812,400802 &&
+            run queuek_16 300 python tools/apply_variants.py --need 16 --total 20 --nobj 64 --variants 13,14 --blocks 256,1024 --nseg 4 --rounds 5 --queue 100806,100812,200803 ;;
+    qab2) for kn in "1 2 0" "2 3 0" "3 5 0,1" "4 6 0,1" "6 9 0,1,2" "8 12 0,1,2,3" "12 16 0,1,2,3" "13 17 0,1,2,3" "16 20 0,1,2,3"; do
+            set -- $kn
+            for q in 0 1; do
+              run qab2_${1}_${2}_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need $1 --total $2 --objects 64 --erase $3 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
+            done
+          done
+          for q in 0 1; do run qab2_c2_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
