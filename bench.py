@@ -580,11 +580,12 @@ def main():
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
     # The product dispatch (rs_apply.hip): the pipelined kernels for shards
     # under 4 GiB unless the kernel form was switched (slime_rs_kernel_pipeline),
-    # with the dynamic (ticket) schedule for k <= 16 unless slime_rs_kernel_schedule
-    # switched it off.
+    # with the dynamic (ticket) schedule for k <= 32 unless slime_rs_kernel_schedule
+    # switched it off (17 <= k <= 32: unless SLIME_RS_K32=0 chose the wide kernels).
     kname = "rs_apply_kernel"
     if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
-        queue = need <= 16 and D.lib.slime_rs_kernel_schedule(-1) == 1
+        queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1 and \
+            (need <= 16 or os.environ.get("SLIME_RS_K32", "1")[:1] != "0")
         kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such

@@ -99,7 +99,7 @@ int slime_rs_host_pipeline(int mode);
  * non-pipelined forms that larger shards always take.  mode < 0 queries.
  * Results are identical; the parity tests run both. */
 int slime_rs_kernel_pipeline(int mode);
-/* Work schedule of the pipelined apply kernels for k <= 16 (process-wide; env
+/* Work schedule of the pipelined apply kernels for k <= 32 (process-wide; env
  * SLIME_RS_QUEUE=0 sets the initial value): 1 = dynamic, waves take units of
  * work from ticket counters (default); 0 = static shares per wave.  mode < 0
  * queries.  Results are identical; the parity tests run both. */

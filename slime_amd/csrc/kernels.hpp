@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
+
 namespace slime {
 
 // One matrix application over a batch of objects:
@@ -57,6 +59,12 @@ void set_pipelined_kernels(bool on);
 // counters, default), 0 static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
+// Ticket counters of the dynamic-schedule kernels (rs_apply_queue_kernel):
+// kQueueCounters counters per set, two sets per (device, stream).  Calls
+// launch(draw, zero_next) under a lock with the set to draw from and the set
+// to zero for the next launch on `stream`; returns launch's result.
+constexpr int kQueueCounters = 8;
+hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*, uint32_t*)>& launch);
 
 // Column segments per object for a launch over nobj objects of ncols
 // columns (the apply and byte kernels cut each object into this many

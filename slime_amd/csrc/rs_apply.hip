@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -164,7 +165,6 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
 // (s42_queuek/).  Geometry: 256 blocks (one per CU) for every k; U = 4 up to
 // k = 4, 3 up to 12, 1 above; a unit is C tiles with C x U about 6 (C = 2 at
 // U >= 3), dealt over kQueueCounters ticket counters.
-constexpr int kQueueCounters = 8;
 constexpr uint64_t kQueueBlocks = 256;
 template <int K>
 constexpr int queue_unroll() {
@@ -175,11 +175,33 @@ constexpr int queue_unit_tiles() {
   return queue_unroll<K>() >= 3 ? 2 : 6 / queue_unroll<K>();
 }
 
+template <int K>
+hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched) {
+  constexpr int U = queue_unroll<K>();
+  constexpr int C = queue_unit_tiles<K>();
+  *launched = false;
+  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
+  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+  *launched = true;
+  const Geometry& geo = geometry();
+  const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
+  return with_tickets(stream, [&](uint32_t* draw, uint32_t* zero_next) {
+    hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
+                       dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride,
+                       a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols,
+                       a.nobj, a.rows, a.k, draw, zero_next, nullptr);
+    return hipGetLastError();
+  });
+}
+
+}  // namespace
+
 // Two ticket-counter sets per (device, stream): a launch draws from set
 // `parity` and zeroes set `parity ^ 1` for the next launch on its stream,
 // which runs after it (stream order); other streams have sets of their own.
 // The lock is held across the launch so that launches reach each stream in
-// parity order.  Sets live for the process (a few KiB per stream used).
+// parity order.  Sets live for the process (4 KiB per stream used).
+namespace {
 struct TicketSets {
   uint32_t* base = nullptr;  // 2 x kQueueCounters x kTicketStride words
   uint32_t parity = 0;
@@ -189,14 +211,9 @@ std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
   static auto* m = new std::map<std::pair<int, hipStream_t>, TicketSets>();
   return *m;
 }
+}  // namespace
 
-template <int K>
-hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched) {
-  constexpr int U = queue_unroll<K>();
-  constexpr int C = queue_unit_tiles<K>();
-  *launched = false;
-  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
-  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*, uint32_t*)>& launch) {
   int dev = 0;
   if (hipError_t e = hipGetDevice(&dev)) return e;
   std::lock_guard<std::mutex> lock(g_ticket_mu);
@@ -213,19 +230,10 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
     }
     ts.base = (uint32_t*)p;
   }
-  const Geometry& geo = geometry();
-  const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
-  hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
-                     dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
-                     a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k,
-                     ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words, nullptr);
-  const hipError_t e = hipGetLastError();
+  const hipError_t e = launch(ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words);
   if (e == hipSuccess) ts.parity ^= 1;  // a launch that never started zeroed nothing
-  *launched = true;
   return e;
 }
-
-}  // namespace
 
 // Kernel form (process-wide): the software-pipelined kernels (default) or
 // the non-pipelined forms that shards/chunks of 4 GiB and more always take.

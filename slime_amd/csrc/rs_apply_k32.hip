@@ -19,8 +19,34 @@
 namespace slime {
 namespace {
 
+// Dynamic schedule (rs_apply_queue_kernel, as for k <= 16 in rs_apply.hip):
+// a unit is C = 6 / U tiles.
+template <int K>
+hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched) {
+  constexpr int U = K <= 24 ? 2 : 1;
+  constexpr int C = 6 / U;
+  *launched = false;
+  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
+  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+  *launched = true;
+  const ApplyGeometry& geo = apply_geometry();
+  const uint64_t blocks = geo.target ? geo.target : 256;
+  return with_tickets(stream, [&](uint32_t* draw, uint32_t* zero_next) {
+    hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true>), dim3((uint32_t)blocks),
+                       dim3(apply::kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
+                       a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows,
+                       a.k, draw, zero_next, nullptr);
+    return hipGetLastError();
+  });
+}
+
 template <int K>
 hipError_t launch_k32(const ApplyLaunch& a, hipStream_t stream) {
+  if (queue_mode() == 1) {
+    bool launched = false;
+    const hipError_t e = launch_k32_queue<K>(a, stream, &launched);
+    if (launched || e != hipSuccess) return e;
+  }
   constexpr int U = K <= 24 ? 2 : 1;
   constexpr uint64_t kBlocks = 256;
   const uint64_t per_block = 4ull * apply::kBlock * U;

@@ -61,7 +61,7 @@ def test_schedule_switch_rejects_unknown_modes(schedule):
 
 
 @pytest.mark.parametrize("need,total", [(1, 2), (3, 5), (4, 6), (5, 8), (8, 12), (10, 14), (12, 16), (13, 17),
-                                        (16, 20)])
+                                        (16, 20), (17, 20), (24, 28), (25, 30), (32, 40)])
 @pytest.mark.parametrize("L,nobj", [(1, 3), (3, 2), (4, 5), (191, 3), (768 + 4, 9), (6 * 768 * 4 + 17, 7),
                                     (65536 + 3, 2)])
 def test_encode_every_schedule_vs_oracle(torch_dev, schedule, need, total, L, nobj):
@@ -84,7 +84,7 @@ def test_encode_every_schedule_vs_oracle(torch_dev, schedule, need, total, L, no
 
 
 @pytest.mark.parametrize("need,total,erase", [(8, 12, [0, 1, 2, 3]), (8, 12, [0, 3, 8, 11]), (10, 14, [1, 12]),
-                                              (4, 6, [0, 5])])
+                                              (4, 6, [0, 5]), (20, 24, [0, 1, 2, 3]), (32, 40, [5, 33])])
 def test_reconstruct_every_schedule_vs_oracle(torch_dev, schedule, need, total, erase):
     torch = torch_dev
     from slime_amd import device as D

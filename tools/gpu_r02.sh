@@ -135,6 +135,12 @@ for step in "$@"; do
             done
           done
           for q in 0 1; do run qab2_c2_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?; done ;;
+    qab3) for kn in "20 24 0,1,2,3" "24 28 0,1,2,3" "28 32 0,1,2,3" "32 40 0,1,2,3"; do
+            set -- $kn
+            for q in 0 1; do
+              run qab3_${1}_${2}_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need $1 --total $2 --objects 32 --erase $3 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
+            done
+          done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
