@@ -375,42 +375,33 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
   return v & 0xF;
 }
 
-// Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
-// per atomic (a wave takes TB consecutive units at a time); STAMP records per
-// wave {start, end, XCD | tiles << 32} (s_memrealtime ticks) into `stamps`.
-template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false>
-__global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
-    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
-    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
-    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
-    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
-    uint64_t* __restrict__ stamps) {
-  static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
-  uint64_t t_start = 0;
-  uint32_t walked = 0;
-  if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
-  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * kTicketStride] = 0;
-  // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
-  const uint32_t nvec = (uint32_t)(ncols >> 2);
-  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
-  const uint32_t ngrp_all = nobj * ((ntiles + 4 * C - 1) / (4 * C));
-  const uint32_t lane = threadIdx.x & 63;
-  uint64_t ioff[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
-
-  // Walk state (wave-uniform): partition p, partitions found dry, current unit.
-  uint32_t p = hw_xcc_id() % NC, dry = 0;
-  uint32_t obj = 0, tb = 0, cnt = 0, i = 0;
+// A wave's walk over the units of a launch (device state, wave-uniform):
+// the current unit (object obj, tiles tb + 4i for i < cnt) and the ticket
+// bookkeeping.  Shared by the apply and byte queue kernels.  TB tickets per
+// atomic (tuning harness; the product uses 1).
+template <int C, int NC, int TB = 1>
+struct TicketWalk {
+  uint32_t* ticket;
+  uint32_t ngrp_all, nobj, ntiles, lane;
+  uint32_t p, dry = 0;                           // partition, partitions found dry
+  uint32_t obj = 0, tb = 0, cnt = 0, i = 0;      // current unit
+  uint32_t pend = 0, bl = 0, bn = 0;             // pending atomic; rest of the ticket batch
   bool live = true;
-  uint32_t pend = 0, bl = 0, bn = 0;  // pending atomic; rest of the current ticket batch (TB > 1)
-  auto request = [&] {
+
+  // ntiles: tiles per object; the launch's units cover nobj objects.
+  __device__ __forceinline__ TicketWalk(uint32_t* t, uint32_t nobj_, uint32_t ntiles_, uint32_t lane_)
+      : ticket(t), ngrp_all(nobj_ * ((ntiles_ + 4 * C - 1) / (4 * C))), nobj(nobj_), ntiles(ntiles_), lane(lane_) {
+    p = hw_xcc_id() % NC;
+    request();
+    next_unit();
+  }
+  __device__ __forceinline__ void request() {
     pend = 0;
     if (lane == 0) pend = atomicAdd(ticket + p * kTicketStride, (uint32_t)TB);
-  };
+  }
   // Enter the unit of the pending ticket (or of later ones: exhausted
   // partitions and empty sub-units are skipped) and request the next ticket.
-  auto next_unit = [&] {
+  __device__ __forceinline__ void next_unit() {
     for (;;) {
       uint32_t l;
       bool fresh = true;
@@ -443,9 +434,37 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
       if (cnt > C) cnt = C;
       if (cnt) return;
     }
-  };
-  request();
-  next_unit();
+  }
+  __device__ __forceinline__ uint32_t tile() const { return tb + 4 * i; }
+  // Step to the next tile (the next unit's first after the last of this one).
+  __device__ __forceinline__ void advance() {
+    if (++i >= cnt) next_unit();
+  }
+};
+
+// Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
+// per atomic (a wave takes TB consecutive units at a time); STAMP records per
+// wave {start, end, XCD | tiles << 32} (s_memrealtime ticks) into `stamps`.
+template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false>
+__global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
+    const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
+    uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
+    const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
+    uint64_t* __restrict__ stamps) {
+  static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
+  uint64_t t_start = 0;
+  uint32_t walked = 0;
+  if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * kTicketStride] = 0;
+  // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t ioff[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
+  TicketWalk<C, NC, TB> w(ticket, nobj, ntiles, lane);
   auto load = [&](uint4(&x)[U][K], uint32_t o, uint32_t t) {
     const uint32_t* base = in + (uint64_t)o * in_obj_stride;
     const uint32_t* sb[K];
@@ -457,24 +476,24 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     store_tile<K, U, NTS>(x, out + (uint64_t)o * out_obj_stride, coeff, out_idx, out_shard, rows, t * (64 * U) + lane,
                           nvec);
   };
-  if (live) {
+  if (w.live) {
     uint4 xa[U][K], xb[U][K];
-    load(xa, obj, tb);
+    load(xa, w.obj, w.tile());
     for (;;) {
-      uint32_t co = obj, ct = tb + 4 * i;
+      uint32_t co = w.obj, ct = w.tile();
       if constexpr (STAMP) ++walked;
-      if (++i >= cnt) next_unit();
+      w.advance();
       // Past the last unit the prefetch re-reads the current tile (unconditional loads, see load_tile).
-      load(xb, live ? obj : co, live ? tb + 4 * i : ct);
+      load(xb, w.live ? w.obj : co, w.live ? w.tile() : ct);
       store(xa, co, ct);
-      if (!live) break;
-      co = obj;
-      ct = tb + 4 * i;
+      if (!w.live) break;
+      co = w.obj;
+      ct = w.tile();
       if constexpr (STAMP) ++walked;
-      if (++i >= cnt) next_unit();
-      load(xa, live ? obj : co, live ? tb + 4 * i : ct);
+      w.advance();
+      load(xa, w.live ? w.obj : co, w.live ? w.tile() : ct);
       store(xb, co, ct);
-      if (!live) break;
+      if (!w.live) break;
     }
   }
   if constexpr (STAMP) {

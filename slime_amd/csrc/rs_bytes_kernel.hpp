@@ -566,6 +566,188 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_pipe_kernel(
   }
 }
 
+// ---- dynamic schedule (need <= 16, chunks < 4 GiB): the product forms -------
+// The pipelined byte kernels above with rs_apply_queue_kernel's ticket walk
+// (apply::TicketWalk: units of C tiles drawn from NC counters, zero at launch,
+// each launch zeroing `zero_next`), so the faster XCDs take more of the
+// batch.  Every object of a launch has the same window, so a unit is any
+// object's tiles and the schedule spans the whole batch.
+template <int K, int U, int C, int NC>
+__global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
+    const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ zero_next) {
+  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
+  const uint64_t chunk = 4 * L;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  uint64_t ioff[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * chunk;
+  auto window = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
+  auto load = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
+    const uint8_t* cb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) cb[j] = window(o) + ioff[j];
+    load_raw_tile<K, U>(r, cb, t * (64 * U) + lane, nvec);
+  };
+  // The tile's mapping is read when its loads are issued, so it is in SGPRs by the math.
+  auto compute = [&](const uint4(&r)[U][K], uint32_t o, uint32_t t, uint32_t m) {
+    uint4 x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        x[u][j] = make_uint4(be(r[u][j].x) ^ m, be(r[u][j].y) ^ m, be(r[u][j].z) ^ m, be(r[u][j].w) ^ m);
+    rows_tile<K, U>(x, rows, coeff, out_idx, window(o), chunk, t * (64 * U) + lane, nvec, m);
+  };
+  apply::TicketWalk<C, NC> w(ticket, nobj, ntiles, lane);
+  if (w.live) {
+    uint4 ra[U][K], rb[U][K];
+    uint32_t ma = mapping[w.obj], mb = 0;
+    load(ra, w.obj, w.tile());
+    for (;;) {
+      uint32_t co = w.obj, ct = w.tile();
+      w.advance();
+      mb = mapping[w.live ? w.obj : co];
+      load(rb, w.live ? w.obj : co, w.live ? w.tile() : ct);
+      compute(ra, co, ct, ma);
+      if (!w.live) break;
+      co = w.obj;
+      ct = w.tile();
+      w.advance();
+      ma = mapping[w.live ? w.obj : co];
+      load(ra, w.live ? w.obj : co, w.live ? w.tile() : ct);
+      compute(rb, co, ct, mb);
+      if (!w.live) break;
+    }
+  }
+  // Columns past the last whole vector of each object, one per lane.
+  const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x, nthr = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t t = tid; tailc && t < (uint64_t)nobj * tailc; t += nthr) {
+    const uint32_t o = (uint32_t)(t / tailc);
+    const uint64_t b = ((uint64_t)nvec << 2) + t % tailc;
+    const uint32_t m = mapping[o];
+    uint32_t x[K][4];
+    load_chunk_symbols<K>(window(o), ioff, b, 1, m, x);
+    rows_out<K>(x, rows, coeff, out_idx, window(o), chunk, 4 * b, m, 1);
+  }
+}
+
+// MODE 0 (speculative, mapping 0) encode on the ticket walk: the interior
+// tiles (encode_bytes_pipe_kernel's pipelined prefix, the same count for
+// every object) are dealt as units; MapToGF's flags are OR-ed into
+// flags[obj] whenever a wave's tiles move to another object.  The few edge
+// tiles and column tails of every object follow, spread over all waves.
+// (Phase 1 re-encodes a handful of objects and keeps the static kernel.)
+template <int K, int U, int C, int NC>
+__global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next) {
+  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  // Interior tiles t < nint: (t+1)*64U <= nvec and (K-1)L + col0 + 4*end < first_tail_word.
+  const uint64_t lim = (uint64_t)(K - 1) * L + col0;
+  uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+  if (end_max > nvec) end_max = nvec;
+  const uint32_t nint = (uint32_t)(end_max / (64 * U));
+  auto window = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
+  auto load = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
+    const uint8_t* cb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) cb[j] = window(o) + (uint64_t)j * chunk;
+    load_raw_tile<K, U>(r, cb, t * (64 * U) + lane, nvec);
+  };
+  Flags fl;
+  uint32_t fobj = 0xFFFFFFFFu;  // the object fl belongs to
+  auto flush = [&] {
+    const uint32_t f = fl.bits();
+    const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+    const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+    if (wf && lane == 0) atomicOr(&flags[fobj], wf);
+    fl = Flags();
+  };
+  auto compute = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
+    if (o != fobj) {
+      if (fobj != 0xFFFFFFFFu) flush();
+      fobj = o;
+    }
+    encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, 0u, rows, coeff, out_idx,
+                                     t * (64 * U) + lane, nvec, fl);
+  };
+  {
+    apply::TicketWalk<C, NC> w(ticket, nobj, nint, lane);
+    if (w.live) {
+      uint4 ra[U][K], rb[U][K];
+      load(ra, w.obj, w.tile());
+      for (;;) {
+        uint32_t co = w.obj, ct = w.tile();
+        w.advance();
+        load(rb, w.live ? w.obj : co, w.live ? w.tile() : ct);
+        compute(ra, co, ct);
+        if (!w.live) break;
+        co = w.obj;
+        ct = w.tile();
+        w.advance();
+        load(ra, w.live ? w.obj : co, w.live ? w.tile() : ct);
+        compute(rb, co, ct);
+        if (!w.live) break;
+      }
+    }
+  }
+  if (fobj != 0xFFFFFFFFu) flush();
+  // Edge tiles [nint, ntiles) of every object (encode_bytes_kernel's edge step).
+  const uint32_t nedge = ntiles - nint;
+  for (uint64_t e = wave; e < (uint64_t)nobj * nedge; e += nwaves) {
+    const uint32_t o = (uint32_t)(e / nedge);
+    uint8_t* const slot = window(o);
+    const uint64_t g0 = (uint64_t)(nint + (uint32_t)(e % nedge)) * (64 * U) + lane;
+    uint32_t x[U][K][4];
+    int n = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (g0 + 64 * u < nvec) {
+        load_data_symbols<K, false, true>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, 0u, x[u], &fl);
+        n = u + 1;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= n) break;
+      const uint64_t b = (g0 + 64 * u) << 2;
+      if ((uint64_t)(K - 1) * L + col0 + b + 4 > first_tail_word) fix_data_tail<K>(slot, chunk, L, col0, b, 4, ow, 0u, x[u]);
+    }
+    rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, g0, 0u);
+    fobj = o;
+    flush();
+  }
+  // Columns past the last whole vector of each object, one per lane.
+  const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x, nthr = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t t = tid; tailc && t < (uint64_t)nobj * tailc; t += nthr) {
+    const uint32_t o = (uint32_t)(t / tailc);
+    uint8_t* const slot = window(o);
+    const uint64_t b = ((uint64_t)nvec << 2) + t % tailc;
+    uint32_t x[K][4];
+    Flags f1;
+    load_data_symbols<K, false, true>(slot, chunk, L, col0, b, 1, ow, 0u, x, &f1);
+    fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, 0u, x);
+    rows_out<K>(x, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, 4 * b, 0u, 1);
+    const uint32_t f = f1.bits();
+    if (f) atomicOr(&flags[o], f);  // per lane: tails are a handful of columns per object
+  }
+}
+
 // ---- wide k (need > 16): the byte kernels in 16-chunk form ------------------
 // Same column walk as rs_apply_wide_kernel (4 columns per lane, one unit per
 // step), with the byte<->symbol transforms of the kernels above: inputs in

@@ -522,14 +522,19 @@ def _make_slots(torch, objs, need, total, extra=0):
     return torch.from_numpy(host).cuda(), L, chunk, stride
 
 
-@pytest.fixture(params=["1", "0"], ids=["pipelined", "fallback"])
+@pytest.fixture(params=[("1", 1), ("1", 0), ("0", 1)], ids=["queue", "pipelined", "fallback"])
 def kernel_form(request):
-    """Byte kernels: the pipelined product form and the non-pipelined form
-    (chunks >= 4 GiB), selected process-wide by slime_rs_kernel_pipeline."""
-    before = N.lib.slime_rs_kernel_pipeline(-1)
-    assert N.lib.slime_rs_kernel_pipeline(int(request.param)) == 0
-    yield request.param
-    N.lib.slime_rs_kernel_pipeline(before)
+    """Byte kernels: the product form (pipelined, dynamic schedule), the
+    pipelined form with static shares (slime_rs_kernel_schedule(0)) and the
+    non-pipelined form (chunks >= 4 GiB), selected process-wide by
+    slime_rs_kernel_pipeline / slime_rs_kernel_schedule."""
+    pipe, sched = request.param
+    before = N.lib.slime_rs_kernel_pipeline(-1), N.lib.slime_rs_kernel_schedule(-1)
+    assert N.lib.slime_rs_kernel_pipeline(int(pipe)) == 0
+    assert N.lib.slime_rs_kernel_schedule(sched) == 0
+    yield pipe
+    N.lib.slime_rs_kernel_pipeline(before[0])
+    N.lib.slime_rs_kernel_schedule(before[1])
 
 
 @pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20), (17, 20), (33, 50)])

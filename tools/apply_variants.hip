@@ -325,6 +325,8 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
   Q(8, 2, 8, 2) Q(8, 2, 8, 4) Q(8, 1, 8, 4) Q(8, 1, 8, 8)
   // k = 4 (C2): U = 3, 2, 1
   Q(4, 2, 8, 1) Q(4, 4, 8, 1) QU(4, 2, 3, 8, 1) QU(4, 1, 6, 8, 1) QU(4, 1, 12, 8, 1) QU(4, 4, 2, 8, 1)
+  // k = 8: U = 4, 2
+  QU(8, 4, 2, 8, 1) QU(8, 4, 1, 8, 1) QU(8, 2, 3, 8, 1) QU(8, 2, 2, 8, 1) Q(8, 3, 8, 1)
   // k = 16: U = 1, 2
   QU(16, 1, 6, 8, 1) QU(16, 1, 12, 8, 1) QU(16, 2, 3, 8, 1)
 #undef Q

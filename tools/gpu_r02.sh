@@ -141,6 +141,14 @@ for step in "$@"; do
               run qab3_${1}_${2}_q$q 200 env SLIME_RS_QUEUE=$q python bench.py --need $1 --total $2 --objects 32 --erase $3 --cpu-baseline 0 --host-path 0 --bytes-path 0 || exit $?
             done
           done ;;
+    queue5) run queue5_enc 300 python tools/apply_variants.py --variants 15 --blocks 256,512 --nseg 2 --rounds 5 --queue 802,803,801,400802,400801,200803,200802 &&
+            run queue5_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256,512 --nseg 2 --rounds 5 --queue 802,803,400802,200803 ;;
+    bytesab) for q in 1 0; do run bytesab_c3_q$q 300 env SLIME_RS_QUEUE=$q python bench.py --cpu-baseline 0 --host-path 0 || exit $?; done
+             for q in 1 0; do run bytesab_c5_q$q 300 env SLIME_RS_QUEUE=$q python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 || exit $?; done ;;
+    bytesab2) run bab_c3 300 python tools/bytes_ab.py &&
+              run bab_c5 300 python tools/bytes_ab.py --need 10 --total 14 --object-mib 1024 --objects 16 &&
+              run bab_c2 300 python tools/bytes_ab.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 &&
+              run bab_k16 300 python tools/bytes_ab.py --need 16 --total 20 --objects 32 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
