@@ -199,14 +199,16 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
 // Two ticket-counter sets per (device, stream): a launch draws from set
 // `parity` and zeroes set `parity ^ 1` for the next launch on its stream,
 // which runs after it (stream order); other streams have sets of their own.
-// The lock is held across the launch so that launches reach each stream in
-// parity order.  Sets live for the process (4 KiB per stream used).
+// The stream's lock is held across the launch so that launches reach each
+// stream in parity order; launches on different streams do not contend.
+// Sets live for the process (4 KiB per stream used).
 namespace {
 struct TicketSets {
+  std::mutex mu;
   uint32_t* base = nullptr;  // 2 x kQueueCounters x kTicketStride words
   uint32_t parity = 0;
 };
-std::mutex g_ticket_mu;
+std::mutex g_ticket_map_mu;
 std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
   static auto* m = new std::map<std::pair<int, hipStream_t>, TicketSets>();
   return *m;
@@ -216,10 +218,14 @@ std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
 hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*, uint32_t*)>& launch) {
   int dev = 0;
   if (hipError_t e = hipGetDevice(&dev)) return e;
-  std::lock_guard<std::mutex> lock(g_ticket_mu);
-  TicketSets& ts = ticket_sets()[{dev, stream}];
+  TicketSets* ts;
+  {
+    std::lock_guard<std::mutex> lock(g_ticket_map_mu);
+    ts = &ticket_sets()[{dev, stream}];  // std::map: the entry's address is stable
+  }
+  std::lock_guard<std::mutex> lock(ts->mu);
   const size_t set_words = (size_t)kQueueCounters * apply::kTicketStride;
-  if (!ts.base) {
+  if (!ts->base) {
     void* p = nullptr;
     if (hipError_t e = hipMalloc(&p, 2 * set_words * sizeof(uint32_t))) return e;
     // On the launch stream: a plain hipMemset (null stream) is not ordered
@@ -228,10 +234,10 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
       (void)hipFree(p);
       return e;
     }
-    ts.base = (uint32_t*)p;
+    ts->base = (uint32_t*)p;
   }
-  const hipError_t e = launch(ts.base + ts.parity * set_words, ts.base + (ts.parity ^ 1) * set_words);
-  if (e == hipSuccess) ts.parity ^= 1;  // a launch that never started zeroed nothing
+  const hipError_t e = launch(ts->base + ts->parity * set_words, ts->base + (ts->parity ^ 1) * set_words);
+  if (e == hipSuccess) ts->parity ^= 1;  // a launch that never started zeroed nothing
   return e;
 }
 

@@ -293,12 +293,11 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
                 "tiles": [int(tiles.min()), int(tiles.max())], "per_xcc": per_xcc}
 
     if args.timed:
-        assert need == 8, "timed walk is built for k = 8"
         for t, y, ns in geos:
             gx = max(1, t // y)
             nw = gx * y * 4
             st = torch.zeros(nw * 3, dtype=torch.int64, device="cuda")  # {t0, t1, xcc | tiles << 32}
-            for it in range(args.timed):
+            for it in range(args.timed if need == 8 else 0):  # the stamped static walk is built for k = 8
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(s)
                 rc = lib.av_launch_timed(buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(), ii.data_ptr(),
@@ -323,6 +322,8 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
                         tails.append(tail_report(VARIANTS[v] + " (stamped)", (t, y, ns), a.elapsed_time(b),
                                                  st.view(t * 4, 3).cpu().numpy()))
                 stamp_ptr[0] = None
+            if need != 8:
+                continue
             view().zero_()
             launch(15, 4, 8, ns)
             torch.cuda.synchronize()

@@ -149,6 +149,10 @@ for step in "$@"; do
               run bab_c5 300 python tools/bytes_ab.py --need 10 --total 14 --object-mib 1024 --objects 16 &&
               run bab_c2 300 python tools/bytes_ab.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 &&
               run bab_k16 300 python tools/bytes_ab.py --need 16 --total 20 --objects 32 ;;
+    c2tail) run c2tail 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 8 --rounds 5 --queue 400802 --timed 3 &&
+            run c2big 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 256 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+            run c2std 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    ns64b) run ns64_final 300 python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
