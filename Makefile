@@ -81,3 +81,8 @@ placeprobe: tools/libplaceprobe.so
 tools/libplaceprobe.so: tools/placement_probe.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: placeprobe
+
+# Physical-placement probe (tools only): make tools/vmm_probe
+tools/vmm_probe: tools/vmm_probe.hip include/slime_rs.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
+	  -Wl,-rpath,'$$ORIGIN/../slime_amd/lib'

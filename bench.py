@@ -70,6 +70,10 @@ def parse():
                          "freed them: the driver then wipes the freed VRAM with the same DMA engines the host "
                          "path uses, which slows its transfers for seconds (DESIGN.md, End-to-end)")
     ap.add_argument("--host-delay", type=float, default=0.0, help="seconds to wait before the host leg")
+    ap.add_argument("--allocator", choices=["vmm", "torch"], default="vmm",
+                    help="batch buffers from slime_rs_device_alloc (physical chunks mapped into one range: the "
+                         "placement the kernels stream well from, DESIGN.md 'Placement modes') or torch.empty "
+                         "(hipMalloc through the caching allocator)")
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
@@ -167,6 +171,17 @@ def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, secon
                       f"{allc['seconds']} s); oracle/rs_oracle.c, gcc -O2"}
 
 
+def batch_empty(args, numel: int, dtype: torch.dtype, dev: int) -> torch.Tensor:
+    """A device batch buffer: slime_rs_device_alloc (default) or torch.empty."""
+    if args.allocator == "vmm":
+        return D.device_empty(numel, dtype, dev)
+    return torch.empty(numel, dtype=dtype, device=f"cuda:{dev}")
+
+
+ALLOCATOR_NOTE = {"vmm": "slime_rs_device_alloc: HIP virtual memory, physical chunks mapped in order",
+                  "torch": "torch.empty (hipMalloc via the caching allocator)"}
+
+
 def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int) -> dict:
     """writeChunks / reconstruct on device from object bytes (rs_bytes.hip): one
     speculative encode pass that also picks gf.MapToGF's mapping, a re-encode
@@ -175,7 +190,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     fallback are re-drawn before timing and counted."""
     S = args.object_mib << 20
     L, chunk, slot = D.slot_geometry(S, need, total)
-    slots = torch.empty(nobj * slot, dtype=torch.uint8, device=f"cuda:{dev}")
+    slots = batch_empty(args, nobj * slot, torch.uint8, dev)
     words = slots.view(torch.int32)
     D.fill_symbols(words, 0xB17E5 + 7919 * rank)
     enc = D.Plan.encode(need, total, dev)
@@ -512,7 +527,7 @@ def main():
     SS = ceil_div(L, max(1, args.shard_align)) * max(1, args.shard_align)
     lay = D.layout_of(total, L, SS)
 
-    buf = torch.empty(nobj * total * SS, dtype=torch.int32, device=f"cuda:{dev}")
+    buf = batch_empty(args, nobj * total * SS, torch.int32, dev)
     # Data shards: deterministic symbols, distinct per rank (synthetic objects).
     D.fill_symbols(buf, 0x5113E + 7919 * rank)
     enc = D.Plan.encode(need, total, dev)
@@ -523,7 +538,7 @@ def main():
         dec.set_outputs(erase)
         rec, rec_lay = buf, lay
     else:
-        rec = torch.empty(nobj * len(erase) * SS, dtype=torch.int32, device=f"cuda:{dev}")
+        rec = batch_empty(args, nobj * len(erase) * SS, torch.int32, dev)
         rec_lay = D.layout_of(len(erase), L, SS)
     stream = torch.cuda.current_stream(dev)
 
@@ -647,6 +662,7 @@ def main():
                 "need": need, "total": total, "object_mib": args.object_mib, "objects_per_gpu": nobj,
                 "symbols_per_shard": L, "shard_stride_symbols": SS, "erased": erase, "decode_dst": args.decode_dst,
                 "parallelism": f"object-partition x{world} (no RCCL)",
+                "allocator": ALLOCATOR_NOTE[args.allocator],
             },
             "encode_gibs": round(obj_bytes / GIB / (enc_ms * 1e-3), 2),
             "decode_gibs": round(obj_bytes / GIB / (dec_ms * 1e-3), 2),

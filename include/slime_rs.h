@@ -272,6 +272,23 @@ int slime_gf_pack_device(int device, const uint8_t *bytes, uint64_t len, uint32_
 int slime_gf_unpack_device(int device, const uint32_t *words, uint64_t count, uint32_t mapping, uint8_t *bytes,
                            void *stream);
 
+/* Device batch buffers (MI355X; no reference counterpart: the Go path works in
+ * host memory).  A hipMalloc'd batch of tens of GiB lands, allocation by
+ * allocation, in one of two physical placements, and the apply kernels stream
+ * about 13% slower from the bad one (DESIGN.md "Placement modes").  This allocator
+ * builds the buffer from physical chunks (HIP virtual memory: hipMemCreate,
+ * mapped in order into one reserved virtual range): 2 MiB-chunk buffers were in
+ * the good placement in 34 of 34 trials, hipMalloc'd ones in 50 of 80
+ * (DESIGN.md "the allocator decides the placement").  `bytes` is
+ * rounded up to the chunk size (env SLIME_RS_VMM_CHUNK_MIB, default 2 MiB);
+ * *ptr receives a base usable by every device entry point.  Synchronous.
+ * Returns 0, SLIME_RS_ERR_INVALID_ARG, SLIME_RS_ERR_NO_DEVICE or
+ * SLIME_RS_ERR_HIP (out of memory). */
+int slime_rs_device_alloc(int device, uint64_t bytes, void **ptr);
+/* Frees a buffer from slime_rs_device_alloc (its base); the device must be
+ * done with it.  Returns SLIME_RS_ERR_INVALID_ARG for other pointers. */
+int slime_rs_device_free(void *ptr);
+
 /* Deterministic synthetic symbols (benchmarks/tests): word g of the buffer is
  * a pure function of (seed, g), uniform over [0, p). Asynchronous. */
 int slime_rs_fill_symbols(int device, uint32_t *dst, uint64_t count, uint64_t seed, void *stream);

@@ -67,6 +67,8 @@ SIGNATURES = [
     ("slime_rs_host_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
+    ("slime_rs_device_alloc", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    ("slime_rs_device_free", ctypes.c_int, [ctypes.c_void_p]),
     ("slime_gf_max_val", ctypes.c_uint32, []),
     ("slime_gf_minverse", ctypes.c_uint32, [ctypes.c_uint32]),
     ("slime_gf_raise", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),

@@ -1114,6 +1114,94 @@ int slime_rs_fill_symbols(int device, uint32_t* dst, uint64_t count, uint64_t se
   return 0;
 }
 
+// ---- device batch buffers (HIP virtual memory) ------------------------------------
+// A buffer is `n` physical chunks (hipMemCreate) mapped in order into one
+// reserved virtual range.  Registry: base -> chunks, for slime_rs_device_free.
+namespace {
+struct VmmBuffer {
+  int device;
+  uint64_t bytes, chunk;
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+};
+std::mutex g_vmm_mu;
+std::map<void*, VmmBuffer>& vmm_buffers() {
+  static auto* m = new std::map<void*, VmmBuffer>();
+  return *m;
+}
+uint64_t vmm_chunk_bytes() {
+  static const uint64_t c = [] {
+    const char* e = getenv("SLIME_RS_VMM_CHUNK_MIB");
+    const long long v = e ? atoll(e) : 0;
+    return (uint64_t)(v > 0 ? v : 2) << 20;
+  }();
+  return c;
+}
+// Unmaps and releases the first `mapped` / `created` chunks, frees the range.
+void vmm_unwind(void* va, uint64_t bytes, uint64_t chunk, const std::vector<hipMemGenericAllocationHandle_t>& h,
+                size_t created, size_t mapped) {
+  for (size_t i = 0; i < mapped; ++i) (void)hipMemUnmap((char*)va + i * chunk, chunk);
+  for (size_t i = 0; i < created; ++i) (void)hipMemRelease(h[i]);
+  (void)hipMemAddressFree(va, bytes);
+}
+}  // namespace
+
+int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
+  if (!ptr || bytes == 0) return fail(Status::InvalidArg, "device_alloc: null ptr or zero bytes");
+  *ptr = nullptr;
+  if (int rc = check_device(device)) return rc;
+  DeviceScope ds(device);
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+  uint64_t chunk = vmm_chunk_bytes();
+  if (gran && chunk % gran) chunk = (chunk + gran - 1) / gran * gran;
+  const uint64_t total = (bytes + chunk - 1) / chunk * chunk;
+  const size_t n = (size_t)(total / chunk);
+  void* va = nullptr;
+  HIP_TRY(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
+  std::vector<hipMemGenericAllocationHandle_t> h(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (hipError_t e = hipMemCreate(&h[i], chunk, &prop, 0)) {
+      vmm_unwind(va, total, chunk, h, i, i);
+      return fail(Status::Hip, std::string("device_alloc: hipMemCreate: ") + hipGetErrorString(e));
+    }
+    if (hipError_t e = hipMemMap((char*)va + i * chunk, chunk, 0, h[i], 0)) {
+      vmm_unwind(va, total, chunk, h, i + 1, i);
+      return fail(Status::Hip, std::string("device_alloc: hipMemMap: ") + hipGetErrorString(e));
+    }
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipError_t e = hipMemSetAccess(va, total, &acc, 1)) {
+    vmm_unwind(va, total, chunk, h, n, n);
+    return fail(Status::Hip, std::string("device_alloc: hipMemSetAccess: ") + hipGetErrorString(e));
+  }
+  {
+    std::lock_guard<std::mutex> lock(g_vmm_mu);
+    vmm_buffers()[va] = VmmBuffer{device, total, chunk, std::move(h)};
+  }
+  *ptr = va;
+  return 0;
+}
+
+int slime_rs_device_free(void* ptr) {
+  VmmBuffer b;
+  {
+    std::lock_guard<std::mutex> lock(g_vmm_mu);
+    auto it = vmm_buffers().find(ptr);
+    if (it == vmm_buffers().end()) return fail(Status::InvalidArg, "device_free: not a slime_rs_device_alloc base");
+    b = std::move(it->second);
+    vmm_buffers().erase(it);
+  }
+  DeviceScope ds(b.device);
+  vmm_unwind(ptr, b.bytes, b.chunk, b.handles, b.handles.size(), b.handles.size());
+  return 0;
+}
+
 // ---- Go-API data entry points (host memory) ------------------------------------------
 
 static int make_rows_plan(const PlanKey& key, slime_rs_plan** out) {

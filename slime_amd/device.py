@@ -30,6 +30,42 @@ def _dev_index(t: torch.Tensor) -> int:
     return t.device.index if t.device.index is not None else torch.cuda.current_device()
 
 
+_TYPESTR = {torch.int32: "<i4", torch.uint8: "|u1", torch.int64: "<i8", torch.uint32: "<u4"}
+
+
+class _DeviceBuffer:
+    """A slime_rs_device_alloc buffer exposed through __cuda_array_interface__;
+    freed when the last tensor viewing it is gone (torch.as_tensor keeps its
+    source object alive for the tensor's lifetime)."""
+
+    def __init__(self, device: int, numel: int, dtype: torch.dtype):
+        itemsize = torch.empty((), dtype=dtype).element_size()
+        p = ctypes.c_void_p()
+        N.check(lib.slime_rs_device_alloc(device, max(1, numel * itemsize), ctypes.byref(p)))
+        self.ptr = p.value
+        self.__cuda_array_interface__ = {"shape": (numel,), "typestr": _TYPESTR[dtype], "data": (self.ptr, False),
+                                         "strides": None, "version": 3, "stream": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def device_empty(numel: int, dtype: torch.dtype = torch.int32, device: int = 0) -> torch.Tensor:
+    """An uninitialised 1-D tensor on `device` backed by slime_rs_device_alloc:
+    physical chunks mapped into one virtual range, the batch-buffer placement
+    the apply kernels stream well from (include/slime_rs.h, DESIGN.md
+    "Placement modes").  Use it for large device-resident batches."""
+    if dtype not in _TYPESTR:
+        raise TypeError(f"device_empty: unsupported dtype {dtype}")
+    with torch.cuda.device(device):
+        t = torch.as_tensor(_DeviceBuffer(device, numel, dtype), device=f"cuda:{device}")
+    if t.data_ptr() == 0 or t.numel() != numel:
+        raise RuntimeError("device_empty: torch did not wrap the device buffer")
+    return t
+
+
 def layout_of(nshards: int, L: int, shard_stride: Optional[int] = None) -> N.Layout:
     ss = L if shard_stride is None else shard_stride
     return N.Layout(obj_stride=ss * nshards, shard_stride=ss)

@@ -153,6 +153,18 @@ for step in "$@"; do
             run c2big 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 256 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
             run c2std 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     ns64b) run ns64_final 300 python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    vmm) run vmm_256 300 tools/vmm_probe malloc,vmm-id:256,vmm-rnd:256,malloc 2 &&
+         run vmm_2 400 tools/vmm_probe malloc,vmm-id:2,vmm-rnd:2,malloc 2 &&
+         run vmm_1024 300 tools/vmm_probe malloc,vmm-id:1024,vmm-rnd:1024,malloc 2 ;;
+    vmm1g) run vmm1g 400 tools/vmm_probe malloc,vmm-id:1024,vmm-rnd:1024,malloc 5 ;;
+    vmmid) run vmmid 500 tools/vmm_probe malloc,vmm-id:2,vmm-id:64,vmm-id:256,malloc 4 ;;
+    vmmmix) run vmmmix 500 tools/vmm_probe malloc,vmm-rnd:2,vmm-id:2,vmm-rnd:64,malloc 4 ;;
+    allocab) run bench_torch 300 python bench.py --allocator torch --cpu-baseline 0 --host-path 0 &&
+             run bench_vmm 300 python bench.py --cpu-baseline 0 --host-path 0 &&
+             run bench_torch2 300 python bench.py --allocator torch --cpu-baseline 0 --host-path 0 &&
+             run bench_vmm2 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
+    vmm2) run vmm2 500 tools/vmm_probe malloc,vmm-id:2,vmm-id:2,malloc,vmm-id:2 3 &&
+          run bench_vmm_2m 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
