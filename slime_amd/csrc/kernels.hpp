@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <functional>
 
 namespace slime {
@@ -70,6 +72,28 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
 // columns (the apply and byte kernels cut each object into this many
 // contiguous segments scheduled like separate objects).
 uint32_t object_segments(uint32_t nobj, uint64_t ncols);
+
+// Segments per object of a dynamic-schedule launch (TicketWalk `spread`,
+// rs_apply_kernel.hpp): about 64 segments over the batch, ceil(64 / nobj),
+// capped at the object's groups of 4*C tiles of U 16-byte vectors per lane
+// (in-process sweeps, profiles/r02/s61_spread/, s62_spread2/: best S = 1 at
+// 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
+// Env SLIME_RS_SEGMENTS forces a count (tuning).  0 when the launch has too
+// many units for 32-bit tickets (the caller takes the static kernel).
+inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
+  const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
+  const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
+  static const uint64_t forced = [] {
+    const char* e = getenv("SLIME_RS_SEGMENTS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (uint64_t)v : 0ull;
+  }();
+  uint64_t S = forced ? forced : (64 + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
+  if (S > groups) S = groups ? groups : 1;
+  const uint64_t B = (groups + S - 1) / S;
+  if ((uint64_t)nobj * S * B * 4 >= (1ull << 32)) return 0;
+  return (uint32_t)S;
+}
 
 // --- fused byte-domain encode/decode over object slots (rs_bytes.hip) --------
 // Slot o at slots + o*slot_stride bytes; chunk c at slot + c*4L.  coeff /

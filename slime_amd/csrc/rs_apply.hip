@@ -180,8 +180,8 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
   constexpr int U = queue_unroll<K>();
   constexpr int C = queue_unit_tiles<K>();
   *launched = false;
-  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
-  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
+  if (!spread) return hipSuccess;
   *launched = true;
   const Geometry& geo = geometry();
   const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
@@ -189,7 +189,7 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
     hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
                        dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride,
                        a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols,
-                       a.nobj, a.rows, a.k, draw, zero_next, nullptr);
+                       a.nobj, a.rows, a.k, draw, zero_next, nullptr, spread);
     return hipGetLastError();
   });
 }

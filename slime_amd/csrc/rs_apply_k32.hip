@@ -26,8 +26,8 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
   constexpr int U = K <= 24 ? 2 : 1;
   constexpr int C = 6 / U;
   *launched = false;
-  const uint64_t ntiles = ((a.ncols >> 2) + 64 * U - 1) / (64 * U);
-  if ((uint64_t)a.nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 >= (1ull << 32)) return hipSuccess;
+  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
+  if (!spread) return hipSuccess;
   *launched = true;
   const ApplyGeometry& geo = apply_geometry();
   const uint64_t blocks = geo.target ? geo.target : 256;
@@ -35,7 +35,7 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
     hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true>), dim3((uint32_t)blocks),
                        dim3(apply::kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
                        a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows,
-                       a.k, draw, zero_next, nullptr);
+                       a.k, draw, zero_next, nullptr, spread);
     return hipGetLastError();
   });
 }

@@ -351,9 +351,12 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
 // Units: an object's tiles are cut into groups of 4*C consecutive tiles; unit
 // = (group, sub) walks tiles grp*4C + sub + 4i, i < C.  The waves that take
 // four consecutive tickets sweep one 4C-tile window of one object together --
-// as a block's four waves do in the static walk.  Group g belongs to object
-// g % nobj (group g / nobj within it), so the groups running at any moment
-// spread over all objects.
+// as a block's four waves do in the static walk.  Ticket-order group g
+// belongs to object g % nobj, so the groups running at any moment spread over
+// all objects; within an object, its q-th group in ticket order sits at
+// segment q % S, position q / S (S = `spread` segments of B groups), so a
+// batch of few objects also keeps its windows spread over each object, as
+// the static walk's column segments do.
 //
 // Tickets: one device-scope counter serialises at ~12 ns per atomic (C = 1:
 // 1.4M tickets took 16.6 ms at C3), so the groups are dealt over NC counters
@@ -379,20 +382,34 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
 // the current unit (object obj, tiles tb + 4i for i < cnt) and the ticket
 // bookkeeping.  Shared by the apply and byte queue kernels.  TB tickets per
 // atomic (tuning harness; the product uses 1).
-template <int C, int NC, int TB = 1>
+// SYNC: fetch a ticket only when it is needed (the wave waits for the atomic
+// there) instead of one unit ahead.  With a ticket pending across tiles, the
+// compiler waits vmcnt(0) before every tile's loads (an atomic and loads share
+// the counter), draining the wave's pipeline each tile; fetched on demand,
+// only the tiles that start a ticket batch pay the atomic's round trip.
+template <int C, int NC, int TB = 1, bool SYNC = false>
 struct TicketWalk {
   uint32_t* ticket;
+  uint32_t spread, seg_groups;  // S segments of B groups per object
   uint32_t ngrp_all, nobj, ntiles, lane;
   uint32_t p, dry = 0;                           // partition, partitions found dry
   uint32_t obj = 0, tb = 0, cnt = 0, i = 0;      // current unit
   uint32_t pend = 0, bl = 0, bn = 0;             // pending atomic; rest of the ticket batch
   bool live = true;
 
-  // ntiles: tiles per object; the launch's units cover nobj objects.
-  __device__ __forceinline__ TicketWalk(uint32_t* t, uint32_t nobj_, uint32_t ntiles_, uint32_t lane_)
-      : ticket(t), ngrp_all(nobj_ * ((ntiles_ + 4 * C - 1) / (4 * C))), nobj(nobj_), ntiles(ntiles_), lane(lane_) {
+  // ntiles: tiles per object; the launch's units cover nobj objects.  The
+  // host guarantees nobj * spread * B * 4 < 2^32 (B = ceil(groups / spread)).
+  __device__ __forceinline__ TicketWalk(uint32_t* t, uint32_t nobj_, uint32_t ntiles_, uint32_t lane_,
+                                        uint32_t spread_ = 1)
+      : ticket(t),
+        spread(spread_ ? spread_ : 1),
+        seg_groups(((ntiles_ + 4 * C - 1) / (4 * C) + spread - 1) / spread),
+        ngrp_all(nobj_ * spread * seg_groups),
+        nobj(nobj_),
+        ntiles(ntiles_),
+        lane(lane_) {
     p = hw_xcc_id() % NC;
-    request();
+    if (!SYNC) request();
     next_unit();
   }
   __device__ __forceinline__ void request() {
@@ -410,6 +427,7 @@ struct TicketWalk {
         --bn;
         fresh = false;
       } else {
+        if (SYNC) request();
         l = __builtin_amdgcn_readfirstlane(pend);
         bl = l + 1;
         bn = TB - 1;
@@ -422,13 +440,14 @@ struct TicketWalk {
         }
         p = p + 1 == NC ? 0 : p + 1;
         bn = 0;
-        if (fresh) request();  // else the batch's successor is already pending
+        if (fresh && !SYNC) request();  // else the batch's successor is already pending
         continue;
       }
-      if (fresh) request();
+      if (fresh && !SYNC) request();
       const uint32_t g = (l >> 2) * NC + p;
       obj = g % nobj;
-      tb = (g / nobj) * (4 * C) + (l & 3);
+      const uint32_t q = g / nobj;
+      tb = ((q % spread) * seg_groups + q / spread) * (4 * C) + (l & 3);
       i = 0;
       cnt = tb < ntiles ? (ntiles - tb + 3) / 4 : 0;
       if (cnt > C) cnt = C;
@@ -445,13 +464,13 @@ struct TicketWalk {
 // Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
 // per atomic (a wave takes TB consecutive units at a time); STAMP records per
 // wave {start, end, XCD | tiles << 32} (s_memrealtime ticks) into `stamps`.
-template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false>
+template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false, bool SYNC = false>
 __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, uint32_t spread) {
   static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
   uint64_t t_start = 0;
   uint32_t walked = 0;
@@ -464,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
   uint64_t ioff[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) ioff[j] = (uint64_t)in_idx[j] * in_shard;
-  TicketWalk<C, NC, TB> w(ticket, nobj, ntiles, lane);
+  TicketWalk<C, NC, TB, SYNC> w(ticket, nobj, ntiles, lane, spread);
   auto load = [&](uint4(&x)[U][K], uint32_t o, uint32_t t) {
     const uint32_t* base = in + (uint64_t)o * in_obj_stride;
     const uint32_t* sb[K];

@@ -61,27 +61,24 @@ constexpr int enc_pipe_unroll() {
 
 // Dynamic schedule (rs_bytes_kernel.hpp queue kernels, as the apply kernels in
 // rs_apply.hip): 256 blocks, units of C tiles with C x U about 6, unless the
-// schedule was switched to static (slime_rs_kernel_schedule).  *launched is
-// false when the batch has too many units for 32-bit tickets.
+// schedule was switched to static (slime_rs_kernel_schedule) or the batch has
+// too many units for 32-bit tickets (queue_spread, kernels.hpp).
 constexpr uint64_t kQueueBlocks = 256;
 template <int U>
 constexpr int queue_tiles() {
   return U >= 3 ? 2 : 6 / U;
-}
-bool queue_fits(uint64_t nobj, uint64_t ncols, int U, int C) {
-  const uint64_t ntiles = ((ncols >> 2) + 64 * U - 1) / (64 * U);
-  return nobj * ((ntiles + 4 * C - 1) / (4 * C)) * 4 < (1ull << 32);
 }
 
 template <int K>
 hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = enc_pipe_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  if (a.phase == 0 && queue_mode() == 1 && queue_fits(a.nobj, ncols, U, queue_tiles<U>())) {
+  const uint32_t spread = a.phase == 0 && queue_mode() == 1 ? queue_spread(a.nobj, ncols, U, queue_tiles<U>()) : 0;
+  if (spread) {
     return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
       hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, queue_tiles<U>(), kQueueCounters>),
                          dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols,
-                         a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, draw, zero_next);
+                         a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, draw, zero_next, spread);
       return hipGetLastError();
     });
   }
@@ -109,11 +106,12 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = pipe_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   constexpr int QU = dec_queue_unroll<K>();
-  if (queue_mode() == 1 && queue_fits(a.nobj, ncols, QU, queue_tiles<QU>())) {
+  const uint32_t spread = queue_mode() == 1 ? queue_spread(a.nobj, ncols, QU, queue_tiles<QU>()) : 0;
+  if (spread) {
     return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
       hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),
                          dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols,
-                         a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, draw, zero_next);
+                         a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, draw, zero_next, spread);
       return hipGetLastError();
     });
   }

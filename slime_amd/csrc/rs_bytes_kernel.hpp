@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t* __restrict__ ticket,
-    uint32_t* __restrict__ zero_next) {
+    uint32_t* __restrict__ zero_next, uint32_t spread) {
   if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
   const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
         x[u][j] = make_uint4(be(r[u][j].x) ^ m, be(r[u][j].y) ^ m, be(r[u][j].z) ^ m, be(r[u][j].w) ^ m);
     rows_tile<K, U>(x, rows, coeff, out_idx, window(o), chunk, t * (64 * U) + lane, nvec, m);
   };
-  apply::TicketWalk<C, NC> w(ticket, nobj, ntiles, lane);
+  apply::TicketWalk<C, NC> w(ticket, nobj, ntiles, lane, spread);
   if (w.live) {
     uint4 ra[U][K], rb[U][K];
     uint32_t ma = mapping[w.obj], mb = 0;
@@ -647,7 +647,8 @@ template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next) {
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
+    uint32_t spread) {
   if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
@@ -687,7 +688,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
                                      t * (64 * U) + lane, nvec, fl);
   };
   {
-    apply::TicketWalk<C, NC> w(ticket, nobj, nint, lane);
+    apply::TicketWalk<C, NC> w(ticket, nobj, nint, lane, spread);
     if (w.live) {
       uint4 ra[U][K], rb[U][K];
       load(ra, w.obj, w.tile());

@@ -303,7 +303,7 @@ extern "C" int av_launch_timed(const uint32_t* in, uint32_t* out, uint64_t io, u
 extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
                                uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t blocks, void* stream,
-                               void* ticket, void* stamps) {
+                               void* ticket, void* stamps, uint32_t spread) {
   hipStream_t s = (hipStream_t)stream;
   uint32_t* t = (uint32_t*)ticket;
   uint32_t* z = t + 16 * kTicketStride;
@@ -313,14 +313,24 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
     if (stamps)                                                                                                 \
       hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, true>), dim3(blocks), dim3(kBlock), \
                          0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
-                         (uint64_t*)stamps);                                                                    \
+                         (uint64_t*)stamps, spread);                                                            \
     else                                                                                                        \
       hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, false>), dim3(blocks), dim3(kBlock), \
                          0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
-                         nullptr);                                                                              \
+                         nullptr, spread);                                                                      \
     return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
 #define Q(KK, CC, NN, TT) QU(KK, 3, CC, NN, TT)
+  // C + 100 NC + 10000 TB + 1000000: on-demand (SYNC) ticket fetch
+#define QS(KK, UU, CC, NN, TT)                                                                                   \
+  if (k == KK && C == CC + 100 * NN + 10000 * TT + 100000 * (UU == 3 ? 0 : UU) + 1000000) {                    \
+    hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, false, true>), dim3(blocks),        \
+                       dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, \
+                       t, z, nullptr, spread);                                                                  \
+    return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
+  }
+  QS(8, 3, 2, 8, 1) QS(8, 3, 2, 8, 2) QS(8, 3, 2, 8, 4) QS(8, 3, 2, 8, 8) QS(8, 3, 4, 8, 2)
+  QS(4, 4, 2, 8, 2) QS(4, 4, 2, 8, 4) QS(4, 4, 2, 8, 8)
   Q(8, 4, 1, 1) Q(8, 1, 8, 1) Q(8, 2, 8, 1) Q(8, 4, 8, 1) Q(8, 8, 8, 1) Q(10, 2, 8, 1) Q(10, 4, 8, 1)
   Q(8, 2, 8, 2) Q(8, 2, 8, 4) Q(8, 1, 8, 4) Q(8, 1, 8, 8)
   // k = 4 (C2): U = 3, 2, 1
@@ -331,6 +341,7 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
   QU(16, 1, 6, 8, 1) QU(16, 1, 12, 8, 1) QU(16, 2, 3, 8, 1)
 #undef Q
 #undef QU
+#undef QS
   return -2;
 }
 

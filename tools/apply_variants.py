@@ -85,8 +85,8 @@ def main():
         VARIANTS[700 + u] = f"pipe K={args.need} U{u} (k-template kernel)"
     for c in (int(x) for x in args.queue.split(",") if x):
         QUEUE[400 + c] = c
-        VARIANTS[400 + c] = (f"queue U{c // 100000 or 3} C{c % 100} NC{c // 100 % 100} TB{max(1, c // 10000 % 10)} "
-                             "(dynamic schedule)")
+        VARIANTS[400 + c] = (f"queue U{c // 100000 % 10 or 3} C{c % 100} NC{c // 100 % 100} TB{max(1, c // 10000 % 10)}"
+                             f"{' on-demand' if c >= 1000000 else ''} (dynamic schedule)")
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"
@@ -114,7 +114,7 @@ def main():
     lib.av_launch_queue.restype = ctypes.c_int
     lib.av_launch_queue.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
-                                 ctypes.c_void_p, ctypes.c_void_p]
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
     lib.av_launch_timed.restype = ctypes.c_int
     lib.av_launch_timed.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p] * 3 + \
         [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
@@ -215,7 +215,7 @@ def run_pad(args, lib, whole, enc, need, total, r, nobj, L, SS, VARIANTS):
             ticket.zero_()
             rc = lib.av_launch_queue(QUEUE[v], need, buf.data_ptr(), d_ptr, total * SS, SS, oo, SS, c_t.data_ptr(),
                                      ii.data_ptr(), oi.data_ptr(), L, nobj, r, gx * gy,
-                                     ctypes.c_void_p(s.cuda_stream), ticket.data_ptr(), stamp_ptr[0])
+                                     ctypes.c_void_p(s.cuda_stream), ticket.data_ptr(), stamp_ptr[0], nseg)
             assert rc == 0, rc
             return
         if v in BATCHED:

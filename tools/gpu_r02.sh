@@ -165,6 +165,19 @@ for step in "$@"; do
              run bench_vmm2 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
     vmm2) run vmm2 500 tools/vmm_probe malloc,vmm-id:2,vmm-id:2,malloc,vmm-id:2 3 &&
           run bench_vmm_2m 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
+    ondemand) run od_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 802,1010802,1020802,1040802,1080802,1020804 &&
+              run od_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 2 --rounds 5 --queue 802,1020802,1040802,1080802 &&
+              run od_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 8 --rounds 7 --queue 400802,1420802,1440802,1480802 ;;
+    spread) run spread_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --variants 15 --blocks 256 --nseg 1,4,16,32 --rounds 5 --queue 802 &&
+            run spread_c3 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 1,2,4 --rounds 5 --queue 802 &&
+            run spread_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 1,8 --rounds 7 --queue 400802 ;;
+    spread2) run spread2_c5 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --variants 15 --blocks 256 --nseg 1,2,4,8 --rounds 5 --queue 802 &&
+             run spread2_c2 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 2,4,8,16 --rounds 7 --queue 400802 &&
+             run spread2_ns 300 python tools/apply_variants.py --mib 512 --nobj 64 --variants 15 --blocks 256 --nseg 1,2,4 --rounds 5 --queue 802 ;;
+    shapes2) run shape2_ns64 300 python bench.py --object-mib 512 --objects 64 --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+             run shape2_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 &&
+             run shape2_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 &&
+             run shape2_c5x8 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
