@@ -285,8 +285,9 @@ int slime_gf_unpack_device(int device, const uint32_t *words, uint64_t count, ui
  * Returns 0, SLIME_RS_ERR_INVALID_ARG, SLIME_RS_ERR_NO_DEVICE or
  * SLIME_RS_ERR_HIP (out of memory). */
 int slime_rs_device_alloc(int device, uint64_t bytes, void **ptr);
-/* Frees a buffer from slime_rs_device_alloc (its base); the device must be
- * done with it.  Returns SLIME_RS_ERR_INVALID_ARG for other pointers. */
+/* Frees a buffer from slime_rs_device_alloc (its base).  Waits for the device
+ * first (hipDeviceSynchronize), so work still queued on it cannot fault.
+ * Returns SLIME_RS_ERR_INVALID_ARG for other pointers. */
 int slime_rs_device_free(void *ptr);
 
 /* Deterministic synthetic symbols (benchmarks/tests): word g of the buffer is

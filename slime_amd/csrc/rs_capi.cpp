@@ -1198,7 +1198,11 @@ int slime_rs_device_free(void* ptr) {
     vmm_buffers().erase(it);
   }
   DeviceScope ds(b.device);
+  // Work still queued on any stream may touch the range (a tensor dropped right
+  // after an asynchronous launch): wait for the device before unmapping.
+  const hipError_t e = hipDeviceSynchronize();
   vmm_unwind(ptr, b.bytes, b.chunk, b.handles, b.handles.size(), b.handles.size());
+  if (e != hipSuccess) return fail(Status::Hip, std::string("device_free: hipDeviceSynchronize: ") + hipGetErrorString(e));
   return 0;
 }
 

@@ -48,7 +48,10 @@ class _DeviceBuffer:
 
     def __del__(self):
         if getattr(self, "ptr", None):
-            lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))
+            try:
+                lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))  # waits for the device, then unmaps
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
             self.ptr = None
 
 

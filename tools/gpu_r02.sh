@@ -178,6 +178,7 @@ for step in "$@"; do
              run shape2_c2 300 python bench.py --need 4 --total 6 --object-mib 64 --objects 32 --erase 0,1 --cpu-baseline 0 --host-path 0 &&
              run shape2_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 &&
              run shape2_c5x8 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+    torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
