@@ -278,7 +278,7 @@ int slime_gf_unpack_device(int device, const uint32_t *words, uint64_t count, ui
  * about 13% slower from the bad one (DESIGN.md "Placement modes").  This allocator
  * builds the buffer from physical chunks (HIP virtual memory: hipMemCreate,
  * mapped in order into one reserved virtual range): 2 MiB-chunk buffers landed
- * in the slow placement in 1 of 52 trials, hipMalloc'd ones in 36 of 92
+ * in the slow placement in 1 of 58 trials, hipMalloc'd ones in 36 of 98
  * (DESIGN.md "the allocator changes the odds").  `bytes` is
  * rounded up to the chunk size (env SLIME_RS_VMM_CHUNK_MIB, default 2 MiB);
  * *ptr receives a base usable by every device entry point.  Synchronous.
