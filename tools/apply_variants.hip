@@ -331,6 +331,15 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
   }
   QS(8, 3, 2, 8, 1) QS(8, 3, 2, 8, 2) QS(8, 3, 2, 8, 4) QS(8, 3, 2, 8, 8) QS(8, 3, 4, 8, 2)
   QS(4, 4, 2, 8, 2) QS(4, 4, 2, 8, 4) QS(4, 4, 2, 8, 8)
+  // C + 100 NC + 10000000 * (1 + 2 * !NTL + !NTS): load/store cache policy (nt = non-temporal)
+#define QN(KK, CC, NN, LL, SS)                                                                                   \
+  if (k == KK && C == CC + 100 * NN + 10000 + 10000000 * (1 + 2 * !LL + !SS)) {                                  \
+    hipLaunchKernelGGL((rs_apply_queue_kernel<KK, 3, CC, NN, LL, SS>), dim3(blocks), dim3(kBlock), 0, s, in, out, io, \
+                       is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z, nullptr, spread);       \
+    return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
+  }
+  QN(8, 2, 8, true, false) QN(8, 2, 8, false, true) QN(8, 2, 8, false, false)
+#undef QN
   Q(8, 4, 1, 1) Q(8, 1, 8, 1) Q(8, 2, 8, 1) Q(8, 4, 8, 1) Q(8, 8, 8, 1) Q(10, 2, 8, 1) Q(10, 4, 8, 1)
   Q(8, 2, 8, 2) Q(8, 2, 8, 4) Q(8, 1, 8, 4) Q(8, 1, 8, 8)
   // k = 4 (C2): U = 3, 2, 1

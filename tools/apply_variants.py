@@ -85,8 +85,9 @@ def main():
         VARIANTS[700 + u] = f"pipe K={args.need} U{u} (k-template kernel)"
     for c in (int(x) for x in args.queue.split(",") if x):
         QUEUE[400 + c] = c
+        pol = {1: "", 2: " plain stores", 3: " plain loads", 4: " plain loads+stores"}.get(c // 10000000, "")
         VARIANTS[400 + c] = (f"queue U{c // 100000 % 10 or 3} C{c % 100} NC{c // 100 % 100} TB{max(1, c // 10000 % 10)}"
-                             f"{' on-demand' if c >= 1000000 else ''} (dynamic schedule)")
+                             f"{' on-demand' if 1000000 <= c < 10000000 else ''}{pol} (dynamic schedule)")
     for u in (int(x) for x in args.batched.split(",") if x):
         BATCHED[300 + u] = u
         VARIANTS[300 + u] = f"pipe U{u} + all rows in registers, stores back to back"

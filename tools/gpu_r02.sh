@@ -180,6 +180,8 @@ for step in "$@"; do
              run shape2_c5 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 16 --cpu-baseline 0 --host-path 0 &&
              run shape2_c5x8 300 python bench.py --need 10 --total 14 --object-mib 1024 --objects 8 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
+    ntpol) run ntpol_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 1 --rounds 5 --queue 802,20010802,30010802,40010802 &&
+           run ntpol_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 1 --rounds 5 --queue 802,20010802,30010802,40010802 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
