@@ -13,10 +13,29 @@ namespace slime {
 namespace {
 
 constexpr uint64_t kBlocks = 256;
+// Dynamic schedule (queue kernels, rs_bytes_kernel.hpp) unless switched off
+// (slime_rs_kernel_schedule): units of C = 6 one-unit tiles, as the apply
+// kernel's k32 queue form.  In-process A/B (tools/bytes_ab.py,
+// profiles/r02/s68_bytesk32/): 20/24 encode 2.585 -> 2.464 ms, decode 2.279 ->
+// 2.180; 32/40 decode 1.905 -> 1.906 but encode 2.623 -> 2.785 (the queue
+// encode holds 484 registers at need 32), so the encode takes it up to need 24.
+constexpr int kQueueTiles = 6;
+constexpr int kQueueEncodeMaxK = 24;
 
 template <int K>
 hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t spread = K <= kQueueEncodeMaxK && a.phase == 0 && queue_mode() == 1
+                              ? queue_spread(a.nobj, ncols, 1, kQueueTiles)
+                              : 0;
+  if (spread) {
+    return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
+      hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>), dim3((uint32_t)kBlocks),
+                         dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows,
+                         a.coeff, a.out_idx, a.flags, draw, zero_next, spread);
+      return hipGetLastError();
+    });
+  }
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, 1, 0>),
@@ -34,6 +53,15 @@ hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
 template <int K>
 hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t spread = queue_mode() == 1 ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
+  if (spread) {
+    return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
+      hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>), dim3((uint32_t)kBlocks),
+                         dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows,
+                         a.coeff, a.in_idx, a.out_idx, a.mapping, draw, zero_next, spread);
+      return hipGetLastError();
+    });
+  }
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_pipe_kernel<K, 1>),
                      bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, kBlocks, 1), dim3(apply::kBlock), 0, s,

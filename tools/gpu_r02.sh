@@ -182,6 +182,8 @@ for step in "$@"; do
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     ntpol) run ntpol_enc 300 python tools/apply_variants.py --variants 15 --blocks 256 --nseg 1 --rounds 5 --queue 802,20010802,30010802,40010802 &&
            run ntpol_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 1 --rounds 5 --queue 802,20010802,30010802,40010802 ;;
+    bytesk32) run bab_20_24 300 python tools/bytes_ab.py --need 20 --total 24 --objects 32 &&
+              run bab_32_40 300 python tools/bytes_ab.py --need 32 --total 40 --objects 32 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
