@@ -25,16 +25,16 @@ constexpr int kQueueEncodeMaxK = 24;
 template <int K>
 hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const uint32_t spread = K <= kQueueEncodeMaxK && a.phase == 0 && queue_mode() == 1
-                              ? queue_spread(a.nobj, ncols, 1, kQueueTiles)
-                              : 0;
-  if (spread) {
-    return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
-      hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>), dim3((uint32_t)kBlocks),
-                         dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows,
-                         a.coeff, a.out_idx, a.flags, draw, zero_next, spread);
-      return hipGetLastError();
-    });
+  if constexpr (K <= kQueueEncodeMaxK) {
+    const uint32_t spread = a.phase == 0 && queue_mode() == 1 ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
+    if (spread) {
+      return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
+        hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>),
+                           dim3((uint32_t)kBlocks), dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                           ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, draw, zero_next, spread);
+        return hipGetLastError();
+      });
+    }
   }
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
