@@ -74,6 +74,9 @@ def parse():
                     help="batch buffers from slime_rs_device_alloc (physical chunks mapped into one range: the "
                          "placement the kernels stream well from, DESIGN.md 'Placement modes') or torch.empty "
                          "(hipMalloc through the caching allocator)")
+    ap.add_argument("--alloc-probe", type=int, default=1,
+                    help="with --allocator vmm: also time 3 encodes and decodes of the same batch in a torch.empty "
+                         "(hipMalloc) buffer, reported as allocator_probe (not value)")
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
@@ -634,6 +637,31 @@ def main():
     # After the host leg: the probe's buffers go back to the driver, whose
     # wipe of freed VRAM would slow the host leg's DMA (DESIGN.md End-to-end).
     ceilings = stream_ceilings(dev, stream) if args.ceilings else None
+    # The same batch in a hipMalloc'd (torch.empty) buffer, a few launches: what
+    # the allocator choice is worth in this process (DESIGN.md "the allocator
+    # changes the odds").  Not part of `value`.
+    alloc_probe = None
+    if args.allocator == "vmm" and args.alloc_probe:
+        alt = torch.empty(nobj * total * SS, dtype=torch.int32, device=f"cuda:{dev}")
+        D.fill_symbols(alt, 0x5113E + 7919 * rank)
+        pe, pd = [], []
+        for k in range(4):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record(stream)
+            enc(alt, lay, alt, lay, L, nobj, stream=stream, dst_offset=need * SS)
+            ev[1].record(stream)
+            dec(alt, lay, alt if args.decode_dst == "inplace" else rec, lay if args.decode_dst == "inplace" else rec_lay,
+                L, nobj, stream=stream)
+            ev[2].record(stream)
+            torch.cuda.synchronize()
+            if k:
+                pe.append(ev[0].elapsed_time(ev[1]))
+                pd.append(ev[1].elapsed_time(ev[2]))
+        del alt
+        pem, pdm = sorted(pe)[1], sorted(pd)[1]
+        alloc_probe = {"buffer": "torch.empty (hipMalloc)", "encode_ms": round(pem, 4), "decode_ms": round(pdm, 4),
+                       "frac": round((enc_alg + dec_alg) / 2 / ((pem + pdm) / 2 * 1e-3) / 1e9 / 8000.0, 4),
+                       "launches": 3}
     bytes_path = None
     if args.bytes_path:
         del buf, rec  # rec aliases buf for in-place repair
@@ -685,6 +713,7 @@ def main():
             },
             "cpu_baseline": None,
             "object_bytes_path": bytes_path,
+            "allocator_probe": alloc_probe,
         }
         line["device"] = board_info(dev)
         if host is not None:
