@@ -61,6 +61,19 @@ void set_pipelined_kernels(bool on);
 // counters, default), 0 static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
+// Whether a launch on `stream` may take the dynamic schedule: the mode is on
+// and the stream is not being captured into a graph.  A captured launch would
+// replay with the same ticket counters every time, and only the next launch's
+// set is zeroed by a launch, so captured launches take the static kernels.
+inline bool queue_allowed(hipStream_t stream) {
+  if (queue_mode() != 1) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return st == hipStreamCaptureStatusNone;
+}
 // Ticket counters of the dynamic-schedule kernels (rs_apply_queue_kernel):
 // kQueueCounters counters per set, two sets per (device, stream).  Calls
 // launch(draw, zero_next) under a lock with the set to draw from and the set

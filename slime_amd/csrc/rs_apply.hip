@@ -272,7 +272,7 @@ template <int K>
 hipError_t dispatch_vec(const ApplyLaunch& a, hipStream_t s) {
   if (!a.vec_ok) return launch_k<K, false>(a, s);
   if (!pipe_ok(a)) return launch_k<K, true>(a, s);
-  if (queue_mode() == 1) {
+  if (queue_allowed(s)) {
     bool launched = false;
     const hipError_t e = launch_queue<K>(a, s, &launched);
     if (launched || e != hipSuccess) return e;

@@ -42,7 +42,7 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
 
 template <int K>
 hipError_t launch_k32(const ApplyLaunch& a, hipStream_t stream) {
-  if (queue_mode() == 1) {
+  if (queue_allowed(stream)) {
     bool launched = false;
     const hipError_t e = launch_k32_queue<K>(a, stream, &launched);
     if (launched || e != hipSuccess) return e;

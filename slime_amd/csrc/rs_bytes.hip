@@ -73,7 +73,7 @@ template <int K>
 hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = enc_pipe_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const uint32_t spread = a.phase == 0 && queue_mode() == 1 ? queue_spread(a.nobj, ncols, U, queue_tiles<U>()) : 0;
+  const uint32_t spread = a.phase == 0 && queue_allowed(s) ? queue_spread(a.nobj, ncols, U, queue_tiles<U>()) : 0;
   if (spread) {
     return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
       hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, queue_tiles<U>(), kQueueCounters>),
@@ -106,7 +106,7 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = pipe_unroll<K>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   constexpr int QU = dec_queue_unroll<K>();
-  const uint32_t spread = queue_mode() == 1 ? queue_spread(a.nobj, ncols, QU, queue_tiles<QU>()) : 0;
+  const uint32_t spread = queue_allowed(s) ? queue_spread(a.nobj, ncols, QU, queue_tiles<QU>()) : 0;
   if (spread) {
     return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
       hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),

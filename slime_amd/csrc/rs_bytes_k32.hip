@@ -26,7 +26,7 @@ template <int K>
 hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   if constexpr (K <= kQueueEncodeMaxK) {
-    const uint32_t spread = a.phase == 0 && queue_mode() == 1 ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
+    const uint32_t spread = a.phase == 0 && queue_allowed(s) ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
     if (spread) {
       return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
         hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>),
@@ -53,7 +53,7 @@ hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
 template <int K>
 hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const uint32_t spread = queue_mode() == 1 ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
+  const uint32_t spread = queue_allowed(s) ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
   if (spread) {
     return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
       hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>), dim3((uint32_t)kBlocks),

@@ -152,3 +152,43 @@ def test_dynamic_schedule_full_batch_matches_static(torch_dev, schedule):
             first = buf.view(nobj, total, L)[:, need:].clone()
     torch.cuda.synchronize()
     assert torch.equal(first, buf.view(nobj, total, L)[:, need:])
+
+
+def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
+    """A launch captured into a graph replays with the same arguments, so it
+    must not depend on ticket counters that only the next launch zeroes:
+    captured launches take the static kernels.  Replay a captured encode and
+    repair three times over changing data, every time exact."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(1) == 0
+    need, total, nobj, L = 8, 12, 9, 3 * 768 * 4 + 5
+    erase = [0, 3, 8, 11]
+    have = [i for i in range(total) if i not in erase][:need]
+    lay = D.layout_of(total, L)
+    enc = D.Plan.encode(need, total)
+    rec = D.Plan.reconstruct(need, total, have, erase)
+    buf = torch.zeros(nobj * total * L, dtype=torch.int32, device="cuda")
+    out = torch.zeros(nobj * len(erase) * L, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm the plans' launch path outside the capture
+        enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
+        rec(buf, lay, out, D.layout_of(len(erase), L), L, nobj, stream=s)
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        h = _objects(rng, nobj, total, L)
+        buf.copy_(torch.from_numpy(h.view(np.int32).reshape(-1)))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        ref = _encode_ref(h, need, total)
+        got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+        assert np.array_equal(got, ref)
+        r = out.cpu().numpy().view(np.uint32).reshape(nobj, len(erase), L)
+        for i, t in enumerate(erase):
+            assert np.array_equal(r[:, i], (ref[:, t].astype(np.uint64) % P).astype(np.uint32)), t

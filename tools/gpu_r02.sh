@@ -30,11 +30,11 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench_nocpu) run bench_nocpu 300 python bench.py --cpu-baseline 0 --host-path 0 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
-            python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+            python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
     pmc_fetch) run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc \
-            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
     pmc_write) run pmc_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc \
-            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
     phased_enc) run phased_enc 400 python tools/apply_variants.py --variants 15 --blocks 256 --rounds 3 \
             --phased 3:700:460,3:800:530,3:900:600,6:1300:860,6:1500:1000 ;;
     phased_dec) run phased_dec 400 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 \
@@ -184,6 +184,8 @@ for step in "$@"; do
            run ntpol_dec 300 python tools/apply_variants.py --decode 1 --separate 0 --variants 15 --blocks 256 --nseg 1 --rounds 5 --queue 802,20010802,30010802,40010802 ;;
     bytesk32) run bab_20_24 300 python tools/bytes_ab.py --need 20 --total 24 --objects 32 &&
               run bab_32_40 300 python tools/bytes_ab.py --need 32 --total 40 --objects 32 ;;
+    orderab) run order_torch 300 python bench.py --allocator torch --cpu-baseline 0 --host-path 0 --bytes-path 0 &&
+             run order_vmm 300 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
