@@ -159,7 +159,7 @@ for step in "$@"; do
     vmm1g) run vmm1g 400 tools/vmm_probe malloc,vmm-id:1024,vmm-rnd:1024,malloc 5 ;;
     vmmid) run vmmid 500 tools/vmm_probe malloc,vmm-id:2,vmm-id:64,vmm-id:256,malloc 4 ;;
     vmmsz) run vmmsz 600 tools/vmm_probe malloc,vmm-id:16,vmm-id:128,vmm-id:512,vmm-id:2 3 ;;
-    vmmorder) run vmmorder 600 tools/vmm_probe vmm-id:2,malloc,malloc,vmm-id:2,vmm-id:2,malloc 3 ;;
+    vmmorder) run vmmorder 600 tools/vmm_probe vmm-id:2,malloc,malloc,vmm-id:2,malloc 3 ;;
     vmmmix) run vmmmix 500 tools/vmm_probe malloc,vmm-rnd:2,vmm-id:2,vmm-rnd:64,malloc 4 ;;
     allocab) run bench_torch 300 python bench.py --allocator torch --cpu-baseline 0 --host-path 0 &&
              run bench_vmm 300 python bench.py --cpu-baseline 0 --host-path 0 &&
