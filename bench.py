@@ -42,9 +42,26 @@ def ceil_div(a: int, b: int) -> int:
     return -(-a // b)
 
 
-def parse():
+PRESETS = {
+    # BASELINE.json configs: (need, total, object MiB, objects per GPU, global objects, erased)
+    "c2": (4, 6, 64, 32, 0, "0,1"),
+    "c3": (8, 12, 256, 128, 0, "0,1,2,3"),
+    "c5": (10, 14, 1024, 0, 64, "0,1,2,3"),  # 64 objects partitioned over the ranks (strong)
+    "ns64": (8, 12, 512, 64, 0, "0,1,2,3"),  # north star's "64 MiB shards"
+}
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node, one rank each.  Without a torchrun environment (WORLD_SIZE unset) "
+                         "and N > 1, bench.py starts the N ranks itself before anything touches a GPU")
+    ap.add_argument("--preset", choices=sorted(PRESETS), default=None,
+                    help="a BASELINE config: c2 (4/6, 32 x 64 MiB), c3 (8/12, 128 x 256 MiB, the default shape), "
+                         "c5 (10/14, 64 x 1 GiB partitioned over the ranks), ns64 (8/12, 64 x 512 MiB)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rendezvous only: every rank reports its object partition, no GPU work "
+                         "(tests the N-rank launch on a machine without GPUs)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--need", type=int, default=8)
@@ -83,7 +100,67 @@ def parse():
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
                          "used only when its config and kernel source match this run)")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.preset:
+        given = {a.split("=")[0] for a in (argv if argv is not None else sys.argv[1:]) if a.startswith("--")}
+        need, total, mib, per_gpu, glob, erase = PRESETS[args.preset]
+        for key, val in (("need", need), ("total", total), ("object_mib", mib), ("objects", per_gpu or 128),
+                         ("global_objects", glob), ("erase", erase)):
+            if "--" + key.replace("_", "-") not in given:  # explicit flags win over the preset
+                setattr(args, key, val)
+    return args
+
+
+# ---- N-rank launch without torchrun ---------------------------------------------
+
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising the GPU (on this
+    image torch.cuda.device_count() does not start the HIP runtime).
+    SLIME_BENCH_DEVICE_COUNT stands in for it under --dry-run only (tests)."""
+    fake = os.environ.get("SLIME_BENCH_DEVICE_COUNT")
+    if fake is not None and "--dry-run" in sys.argv[1:]:
+        return int(fake)
+    return torch.cuda.device_count()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) outside torchrun: start N copies of this script, one
+    per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1),
+    as child processes -- this parent never touches a GPU and never execs.
+    Rank 0's JSON line is the output; the exit status is the first failing
+    rank's (the other ranks are then stopped: they would wait at a barrier)."""
+    import subprocess
+    ndev = visible_gpus()
+    if args.gpus > ndev:
+        print(f"bench.py: --gpus {args.gpus} but {ndev} visible GPU(s); one rank per GPU", file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ, WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    procs = []
+    for r in range(args.gpus):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # the exact children this launcher started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def _cpu_model() -> str:
@@ -492,20 +569,38 @@ def kernel_source_id() -> str:
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # Start the N ranks here, before anything initialises a GPU.
+        sys.exit(launch_ranks(args))
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} under a launcher with WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         # Control plane only (barrier + max-over-ranks timing): objects are
         # independent, the data path exchanges nothing between GPUs.
         dist.init_process_group("gloo", rank=rank, world_size=world)
     # One rank per GPU.  More ranks than visible GPUs would put two ranks on
     # one device and overstate the scaling curve: refuse.
-    ndev = torch.cuda.device_count()
+    ndev = visible_gpus()
     if world > ndev or local >= ndev:
         print(f"bench.py: {world} ranks (local rank {local}) but {ndev} visible GPU(s); one rank per GPU",
               file=sys.stderr, flush=True)
         sys.exit(2)
+    if args.dry_run:
+        first, count = batch.partition(args.global_objects, world, rank) if args.global_objects else \
+            (rank * args.objects, args.objects)
+        parts = batch.gather_strings(json.dumps([rank, local, first, count]))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_ranks": world, "need": args.need, "total": args.total,
+                              "object_mib": args.object_mib, "scaling": "strong" if args.global_objects else "weak",
+                              "partitions": [json.loads(p) for p in parts]}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     dev = local
     torch.cuda.set_device(dev)
 

@@ -345,6 +345,12 @@ typedef struct slime_rs_host_stats {
 int slime_rs_host_stats(slime_rs_host_stats_t *stats, int reset);
 /* Host calls the device pool has routed to `device` so far and calls in flight there. */
 int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
+/* Ticket-counter sets of the dynamic-schedule kernels on `device`: *sets
+ * allocated so far, *held by launches not yet known to have finished plus
+ * those owned by captured graphs.  A set is reused by any stream once its
+ * launch has finished (each launch leaves its set zero; DESIGN.md "Dynamic
+ * schedule"). */
+int slime_rs_ticket_sets(int device, uint64_t *sets, uint64_t *held);
 
 /* ==== chunk and object digests ======================
  * Host computations on the library's digest threads (DESIGN.md "Chunk

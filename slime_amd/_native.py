@@ -151,6 +151,7 @@ SIGNATURES = [
     ("slime_rs_plan_cache_stats", ctypes.c_int, [ctypes.POINTER(CacheStats)]),
     ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
     ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
+    ("slime_rs_ticket_sets", ctypes.c_int, [ctypes.c_int, c_u64p, c_u64p]),
     ("slime_rs_host_stats", ctypes.c_int, [ctypes.POINTER(HostStats), ctypes.c_int]),
     # chunk and object digests (host)
     ("slime_rs_sha256", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
@@ -257,6 +258,13 @@ def digest_info() -> tuple[bool, int]:
     e, t = ctypes.c_int(), ctypes.c_int()
     check(lib.slime_rs_digest_info(ctypes.byref(e), ctypes.byref(t)))
     return bool(e.value), int(t.value)
+
+
+def ticket_sets(device: int) -> tuple[int, int]:
+    """(ticket-counter sets allocated on `device`, sets held by unfinished launches or captured graphs)."""
+    s, h = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.slime_rs_ticket_sets(device, ctypes.byref(s), ctypes.byref(h)))
+    return int(s.value), int(h.value)
 
 
 def pool_calls(device: int) -> tuple[int, int]:

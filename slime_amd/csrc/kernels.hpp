@@ -61,25 +61,25 @@ void set_pipelined_kernels(bool on);
 // counters, default), 0 static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
-// Whether a launch on `stream` may take the dynamic schedule: the mode is on
-// and the stream is not being captured into a graph.  A captured launch would
-// replay with the same ticket counters every time, and only the next launch's
-// set is zeroed by a launch, so captured launches take the static kernels.
-inline bool queue_allowed(hipStream_t stream) {
-  if (queue_mode() != 1) return false;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return st == hipStreamCaptureStatusNone;
-}
+// Whether launches may take the dynamic schedule (the mode is on).  Graph
+// capture is allowed: a launch resets its own counter set (TicketWalk::finish),
+// so a captured launch replays on the set it was captured with.
+inline bool queue_allowed(hipStream_t) { return queue_mode() == 1; }
 // Ticket counters of the dynamic-schedule kernels (rs_apply_queue_kernel):
-// kQueueCounters counters per set, two sets per (device, stream).  Calls
-// launch(draw, zero_next) under a lock with the set to draw from and the set
-// to zero for the next launch on `stream`; returns launch's result.
+// kQueueCounters draw counters + an exit counter per set (zero whenever no
+// launch holds the set).  Takes a set that no unfinished launch holds from
+// the current device's pool and calls launch(set); the set goes back to the
+// pool behind an event recorded on `stream` after the launch, or stays with
+// the graph when `stream` is capturing.  *launched = false (and hipSuccess)
+// when no set could be had -- a capture with the pool exhausted; the caller
+// then takes the static kernel.  Returns launch's result.
 constexpr int kQueueCounters = 8;
-hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*, uint32_t*)>& launch);
+hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*)>& launch, bool* launched);
+// Creates the current device's first counter sets outside any capture (plan
+// creation calls it), so a captured launch finds the pool ready.
+hipError_t warm_ticket_pool(int device);
+// Sets allocated / held by launches in flight or graphs, for `device` (tests).
+void ticket_pool_stats(int device, uint64_t* sets, uint64_t* held);
 
 // Column segments per object for a launch over nobj objects of ncols
 // columns (the apply and byte kernels cut each object into this many

@@ -19,10 +19,12 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <deque>
 #include <functional>
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 #include "kernels.hpp"
 #include "rs_apply_kernel.hpp"
@@ -182,63 +184,151 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
   *launched = false;
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
-  *launched = true;
   const Geometry& geo = geometry();
   const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
-  return with_tickets(stream, [&](uint32_t* draw, uint32_t* zero_next) {
-    hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
-                       dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride,
-                       a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols,
-                       a.nobj, a.rows, a.k, draw, zero_next, nullptr, spread);
-    return hipGetLastError();
-  });
+  return with_tickets(
+      stream,
+      [&](uint32_t* set) {
+        hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, kNtLoads, kNtStores>),
+                           dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a.in, a.out, a.in_obj_stride,
+                           a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx,
+                           a.ncols, a.nobj, a.rows, a.k, set, nullptr, spread);
+        return hipGetLastError();
+      },
+      launched);
 }
 
 }  // namespace
 
-// Two ticket-counter sets per (device, stream): a launch draws from set
-// `parity` and zeroes set `parity ^ 1` for the next launch on its stream,
-// which runs after it (stream order); other streams have sets of their own.
-// The stream's lock is held across the launch so that launches reach each
-// stream in parity order; launches on different streams do not contend.
-// Sets live for the process (4 KiB per stream used).
+// ---- ticket-counter sets -------------------------------------------------------
+// A queue launch resets its own set before it ends (TicketWalk::finish), so
+// a set is reusable as soon as the launch that held it has finished -- on any
+// stream.  Per device: a pool of sets, each with an event recorded after the
+// launch that last took it; a set is free when that event has completed.
+// Nothing depends on the identity of the launch stream, so hipStreamPerThread,
+// the per-thread null stream, and a stream destroyed while its last launch
+// runs (its handle then reused by hipStreamCreate) are all safe.  A launch
+// captured into a graph keeps its set for the graph's life: every replay
+// leaves it zero for the next.  Sets come in slabs of kSlabSets, zeroed
+// synchronously when created; creation never happens inside a capture.
 namespace {
-struct TicketSets {
-  std::mutex mu;
-  uint32_t* base = nullptr;  // 2 x kQueueCounters x kTicketStride words
-  uint32_t parity = 0;
+constexpr uint32_t kSetWords = apply::ticket_set_words(kQueueCounters);
+constexpr int kSlabSets = 64;
+struct TicketSet {
+  uint32_t* p = nullptr;
+  hipEvent_t ev = nullptr;
 };
-std::mutex g_ticket_map_mu;
-std::map<std::pair<int, hipStream_t>, TicketSets>& ticket_sets() {
-  static auto* m = new std::map<std::pair<int, hipStream_t>, TicketSets>();
-  return *m;
-}
-}  // namespace
+struct TicketPool {
+  std::mutex mu;
+  std::vector<TicketSet> free_sets;  // zero, no launch holds them
+  std::deque<TicketSet> busy;        // held by a launch, oldest first
+  uint64_t sets = 0, graph_held = 0;
 
-hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*, uint32_t*)>& launch) {
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return e;
-  TicketSets* ts;
-  {
-    std::lock_guard<std::mutex> lock(g_ticket_map_mu);
-    ts = &ticket_sets()[{dev, stream}];  // std::map: the entry's address is stable
-  }
-  std::lock_guard<std::mutex> lock(ts->mu);
-  const size_t set_words = (size_t)kQueueCounters * apply::kTicketStride;
-  if (!ts->base) {
+  hipError_t grow() {  // mu held; not inside a capture
     void* p = nullptr;
-    if (hipError_t e = hipMalloc(&p, 2 * set_words * sizeof(uint32_t))) return e;
-    // On the launch stream: a plain hipMemset (null stream) is not ordered
-    // before launches on non-blocking streams.
-    if (hipError_t e = hipMemsetAsync(p, 0, 2 * set_words * sizeof(uint32_t), stream)) {
+    const size_t bytes = (size_t)kSlabSets * kSetWords * sizeof(uint32_t);
+    if (hipError_t e = hipMalloc(&p, bytes)) return e;
+    // The null stream, then a wait for it: the zeroes are in memory before
+    // any stream (blocking or not) can launch on a set of this slab.
+    hipError_t e = hipMemset(p, 0, bytes);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
       (void)hipFree(p);
       return e;
     }
-    ts->base = (uint32_t*)p;
+    for (int i = 0; i < kSlabSets; ++i) {
+      TicketSet s;
+      s.p = (uint32_t*)p + (size_t)i * kSetWords;
+      if ((e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming)) != hipSuccess) return e;  // slab stays partly used
+      free_sets.push_back(s);
+      ++sets;
+    }
+    return hipSuccess;
   }
-  const hipError_t e = launch(ts->base + ts->parity * set_words, ts->base + (ts->parity ^ 1) * set_words);
-  if (e == hipSuccess) ts->parity ^= 1;  // a launch that never started zeroed nothing
-  return e;
+  // A free set, reclaiming finished launches' sets first.  false: none (and
+  // `may_grow` forbade a new slab).
+  void reclaim() {  // mu held: every set whose launch has finished goes back
+    for (auto it = busy.begin(); it != busy.end();) {
+      const hipError_t q = hipEventQuery(it->ev);
+      if (q == hipSuccess) {
+        free_sets.push_back(*it);
+        it = busy.erase(it);
+      } else {
+        if (q != hipErrorNotReady) (void)hipGetLastError();
+        ++it;
+      }
+    }
+  }
+  bool take(TicketSet* out, bool may_grow, hipError_t* err) {
+    *err = hipSuccess;
+    if (free_sets.empty()) reclaim();
+    if (free_sets.empty() && may_grow) *err = grow();
+    if (free_sets.empty()) return false;
+    *out = free_sets.back();
+    free_sets.pop_back();
+    return true;
+  }
+};
+TicketPool& ticket_pool(int dev) {
+  static std::mutex mu;
+  static auto* pools = new std::map<int, TicketPool>();  // never destroyed (see plan cache)
+  std::lock_guard<std::mutex> lock(mu);
+  return (*pools)[dev];  // std::map: the entry's address is stable
+}
+bool capturing(hipStream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;  // unknown: behave as inside a capture (no slab creation, no event)
+  }
+  return st != hipStreamCaptureStatusNone;
+}
+}  // namespace
+
+hipError_t warm_ticket_pool(int device) {
+  TicketPool& tp = ticket_pool(device);
+  std::lock_guard<std::mutex> lock(tp.mu);
+  return tp.sets ? hipSuccess : tp.grow();
+}
+
+void ticket_pool_stats(int device, uint64_t* sets, uint64_t* held) {
+  TicketPool& tp = ticket_pool(device);
+  std::lock_guard<std::mutex> lock(tp.mu);
+  tp.reclaim();
+  *sets = tp.sets;
+  *held = tp.busy.size() + tp.graph_held;
+}
+
+hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*)>& launch, bool* launched) {
+  *launched = false;
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  const bool cap = capturing(stream);
+  TicketPool& tp = ticket_pool(dev);
+  TicketSet set;
+  {
+    std::lock_guard<std::mutex> lock(tp.mu);
+    hipError_t e;
+    if (!tp.take(&set, !cap, &e)) return e;  // hipSuccess + !launched: static kernel
+  }
+  const hipError_t e = launch(set.p);
+  std::lock_guard<std::mutex> lock(tp.mu);
+  if (e != hipSuccess) {  // never started: the set is still zero
+    tp.free_sets.push_back(set);
+    return e;
+  }
+  *launched = true;
+  if (cap) {
+    ++tp.graph_held;  // the graph owns it from now on
+    return hipSuccess;
+  }
+  if (const hipError_t r = hipEventRecord(set.ev, stream)) {
+    // Without the event the set's release cannot be observed: leave it held.
+    ++tp.graph_held;
+    return r;
+  }
+  tp.busy.push_back(set);
+  return hipSuccess;
 }
 
 // Kernel form (process-wide): the software-pipelined kernels (default) or

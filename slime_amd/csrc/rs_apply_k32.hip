@@ -28,16 +28,18 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
   *launched = false;
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
-  *launched = true;
   const ApplyGeometry& geo = apply_geometry();
   const uint64_t blocks = geo.target ? geo.target : 256;
-  return with_tickets(stream, [&](uint32_t* draw, uint32_t* zero_next) {
-    hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true>), dim3((uint32_t)blocks),
-                       dim3(apply::kBlock), 0, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
-                       a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows,
-                       a.k, draw, zero_next, nullptr, spread);
-    return hipGetLastError();
-  });
+  return with_tickets(
+      stream,
+      [&](uint32_t* set) {
+        hipLaunchKernelGGL((apply::rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true>),
+                           dim3((uint32_t)blocks), dim3(apply::kBlock), 0, stream, a.in, a.out, a.in_obj_stride,
+                           a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.coeff, a.in_idx, a.out_idx,
+                           a.ncols, a.nobj, a.rows, a.k, set, nullptr, spread);
+        return hipGetLastError();
+      },
+      launched);
 }
 
 template <int K>

@@ -362,15 +362,22 @@ __global__ __launch_bounds__(kBlock) void rs_apply_pipe_kernel(
 // 1.4M tickets took 16.6 ms at C3), so the groups are dealt over NC counters
 // (partition p owns groups g = p (mod NC)), each on its own 256-byte line.  A
 // wave draws from its XCD's partition and, once that is exhausted, from the
-// next ones in turn; a wave is done when all NC have run dry.  Counters are
-// zero at launch: the host alternates two counter sets per stream, and each
-// launch zeroes the set the next launch on its stream will use
-// (`zero_next`; the previous launch that used it has finished by stream
-// order).  The ticket for a wave's next unit is requested when it
-// enters a unit and read one unit later, so its latency is hidden (the
-// compiler still waits vmcnt(0) before reading it: atomics and loads share the
-// counter).
+// next ones in turn; a wave is done when all NC have run dry.  The ticket for
+// a wave's next unit is requested when it enters a unit and read one unit
+// later, so its latency is hidden (the compiler still waits vmcnt(0) before
+// reading it: atomics and loads share the counter).
+//
+// A launch leaves its counter set as it found it, zero: every wave bumps the
+// set's exit counter once it has found every partition dry (its last draw
+// has returned by then), and the wave that brings it to the launch's wave
+// count -- no draw can follow -- zeroes the NC counters and the exit counter.
+// So a set needs no host-side reset between launches: the host hands each
+// launch a set no unfinished launch holds (rs_apply.hip, TicketPool), and a
+// set captured into a graph is reset by every replay itself.
 constexpr uint32_t kTicketStride = 64;  // words between counters
+// Words of one counter set of NC partitions: NC draw counters, then the exit
+// counter, each on its own 256-byte line.
+__host__ __device__ constexpr uint32_t ticket_set_words(int nc) { return (uint32_t)(nc + 1) * kTicketStride; }
 
 __device__ __forceinline__ uint32_t hw_xcc_id() {
   uint32_t v;
@@ -459,6 +466,19 @@ struct TicketWalk {
   __device__ __forceinline__ void advance() {
     if (++i >= cnt) next_unit();
   }
+  // Once per wave, after the walk ended (live == false): count the wave out;
+  // the launch's last wave returns the set to zero (see kTicketStride).
+  // Zeroed with atomics, which execute at the memory side like the draws.
+  __device__ __forceinline__ void finish() {
+    if (lane == 0) {
+      uint32_t* const done = ticket + NC * kTicketStride;
+      if (atomicAdd(done, 1u) == gridDim.x * gridDim.y * (blockDim.x >> 6) - 1) {
+#pragma unroll
+        for (int q = 0; q < NC; ++q) atomicExch(ticket + q * kTicketStride, 0u);
+        atomicExch(done, 0u);
+      }
+    }
+  }
 };
 
 // Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
@@ -469,13 +489,11 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
-    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
-    uint64_t* __restrict__ stamps, uint32_t spread) {
+    uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint64_t* __restrict__ stamps, uint32_t spread) {
   static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
   uint64_t t_start = 0;
   uint32_t walked = 0;
   if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
-  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * kTicketStride] = 0;
   // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
   const uint32_t nvec = (uint32_t)(ncols >> 2);
   const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
@@ -515,6 +533,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
       if (!w.live) break;
     }
   }
+  w.finish();
   if constexpr (STAMP) {
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {

@@ -75,12 +75,17 @@ hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t spread = a.phase == 0 && queue_allowed(s) ? queue_spread(a.nobj, ncols, U, queue_tiles<U>()) : 0;
   if (spread) {
-    return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
-      hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, queue_tiles<U>(), kQueueCounters>),
-                         dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols,
-                         a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, draw, zero_next, spread);
-      return hipGetLastError();
-    });
+    bool launched = false;
+    const hipError_t e = with_tickets(
+        s,
+        [&](uint32_t* set) {
+          hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, queue_tiles<U>(), kQueueCounters>),
+                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                             ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, set, spread);
+          return hipGetLastError();
+        },
+        &launched);
+    if (launched || e != hipSuccess) return e;
   }
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
@@ -108,12 +113,17 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int QU = dec_queue_unroll<K>();
   const uint32_t spread = queue_allowed(s) ? queue_spread(a.nobj, ncols, QU, queue_tiles<QU>()) : 0;
   if (spread) {
-    return with_tickets(s, [&](uint32_t* draw, uint32_t* zero_next) {
-      hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),
-                         dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols,
-                         a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, draw, zero_next, spread);
-      return hipGetLastError();
-    });
+    bool launched = false;
+    const hipError_t e = with_tickets(
+        s,
+        [&](uint32_t* set) {
+          hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),
+                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                             ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, set, spread);
+          return hipGetLastError();
+        },
+        &launched);
+    if (launched || e != hipSuccess) return e;
   }
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_pipe_kernel<K, U>),

@@ -577,8 +577,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t* __restrict__ ticket,
-    uint32_t* __restrict__ zero_next, uint32_t spread) {
-  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
+    uint32_t spread) {
   const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nvec = (uint32_t)(ncols >> 2);
@@ -624,6 +623,7 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
       if (!w.live) break;
     }
   }
+  w.finish();
   // Columns past the last whole vector of each object, one per lane.
   const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x, nthr = (uint64_t)gridDim.x * kBlock;
@@ -647,9 +647,7 @@ template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t* __restrict__ zero_next,
-    uint32_t spread) {
-  if (blockIdx.x == 0 && threadIdx.x < NC) zero_next[threadIdx.x * apply::kTicketStride] = 0;
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread) {
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
@@ -706,6 +704,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
         if (!w.live) break;
       }
     }
+    w.finish();
   }
   if (fobj != 0xFFFFFFFFu) flush();
   // Edge tiles [nint, ntiles) of every object (encode_bytes_kernel's edge step).

@@ -186,6 +186,13 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   }
   plan->table = (uint32_t*)p;
   g_tables_live.fetch_add(1, std::memory_order_relaxed);
+  // The device's first ticket-counter sets, created here (never inside a
+  // capture) so that a launch of this plan captured into a graph finds them.
+  if (hipError_t e = warm_ticket_pool(device)) {
+    (void)hipFree(p);
+    g_tables_live.fetch_sub(1, std::memory_order_relaxed);
+    return fail_hip(e, "ticket counter sets");
+  }
   plan->d_coeff = plan->table;
   plan->d_in_idx = plan->table + ncoef;
   plan->d_out_idx = plan->table + ncoef + n_in;
@@ -790,6 +797,13 @@ int slime_rs_kernel_schedule(int mode) {
   if (mode < 0) return queue_mode();
   if (mode > 1) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0 (static) or 1 (dynamic)");
   set_queue_mode(mode);
+  return 0;
+}
+
+int slime_rs_ticket_sets(int device, uint64_t* sets, uint64_t* held) {
+  if (!sets || !held) return fail(Status::InvalidArg, "ticket_sets: null output");
+  if (int rc = check_device(device)) return rc;
+  ticket_pool_stats(device, sets, held);
   return 0;
 }
 

@@ -19,7 +19,11 @@ from . import _native as N
 lib = N.lib
 
 
-def _stream_handle(device: int, stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+def _stream_handle(device: int, stream) -> ctypes.c_void_p:
+    """A torch stream (default: the device's current one), or a raw hipStream_t
+    handle given as an int (e.g. 2 = hipStreamPerThread)."""
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
     s = stream if stream is not None else torch.cuda.current_stream(device)
     return ctypes.c_void_p(s.cuda_stream)
 

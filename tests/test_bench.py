@@ -29,6 +29,55 @@ def test_bench_refuses_more_ranks_than_gpus():
     assert "one rank per GPU" in r.stderr
 
 
+def _bench(args, **env):
+    e = dict(os.environ, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if k not in env:
+            e.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, env=e)
+
+
+def test_gpus_n_launches_n_ranks_that_agree_on_the_partition():
+    """`bench.py --gpus 2` outside torchrun starts two ranks itself (a stub
+    device count under --dry-run: no GPU here); both rendezvous and report
+    their share.  Weak scaling: 128 objects each; the C5 preset: 64 objects
+    split 32 + 32."""
+    r = _bench(["--gpus", "2", "--dry-run"], SLIME_BENCH_DEVICE_COUNT="2")
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_ranks"] == 2 and line["scaling"] == "weak"
+    assert line["partitions"] == [[0, 0, 0, 128], [1, 1, 128, 128]]
+    r = _bench(["--gpus", "2", "--dry-run", "--preset", "c5"], SLIME_BENCH_DEVICE_COUNT="2")
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (line["need"], line["total"], line["object_mib"], line["scaling"]) == (10, 14, 1024, "strong")
+    assert line["partitions"] == [[0, 0, 0, 32], [1, 1, 32, 32]]
+
+
+def test_gpus_n_beyond_visible_devices_exits_2():
+    """--gpus 2 with fewer visible GPUs: exit 2 with a message, never a line
+    claiming one GPU for a multi-GPU request."""
+    r = _bench(["--gpus", "2", "--dry-run"], SLIME_BENCH_DEVICE_COUNT="1")
+    assert r.returncode == 2 and "one rank per GPU" in r.stderr, r.stdout + r.stderr
+    assert r.stdout.strip() == ""
+    import torch
+    if torch.cuda.device_count() < 2:
+        r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+        assert r.returncode == 2 and "one rank per GPU" in r.stderr, r.stdout + r.stderr
+        assert "n_gpus" not in r.stdout
+
+
+def test_presets_fill_the_baseline_shapes_and_flags_win():
+    bench = _load("bench.py", "bench_mod3")
+    a = bench.parse(["--preset", "c2"])
+    assert (a.need, a.total, a.object_mib, a.objects, a.global_objects, a.erase) == (4, 6, 64, 32, 0, "0,1")
+    a = bench.parse(["--preset", "c5", "--global-objects", "16"])
+    assert (a.need, a.total, a.object_mib, a.global_objects) == (10, 14, 1024, 16)
+    a = bench.parse([])
+    assert (a.need, a.total, a.object_mib, a.objects) == (8, 12, 256, 128)
+
+
 def test_shape_labels_name_baseline_configs():
     bench = _load("bench.py", "bench_mod")
     assert bench.shape_label(8, 12, 256).startswith("C3+C4")

@@ -7,9 +7,11 @@ sample and not a round trip.
   C4: the same objects, data shards {0,1,2,3} erased, and the mixed set
       {0,3,8,11} (RecoverData, vector.go:50-88, + CreateParity for parity rows)
   C5: need=10 total=14, 1 GiB objects (L = 26843546, 4 padding symbols)
+  C2: need=4 total=6, 64 MiB objects in a batch of 32 (the queue kernels'
+      4-tile units and 2-segment spread), decodes of {0,1} and {0,5}
 and the fused byte path (writeChunks / reconstruct framing,
-multi_store.go:526-557 and :194-242) at C3 and C5, including objects mapped
-with 1<<31 (map.go:47-62).  The oracle runs threaded over column ranges
+multi_store.go:526-557 and :194-242) at C3, C5 and C2 (in its 32-object
+batch), including objects mapped with 1<<31 (map.go:47-62).  The oracle runs threaded over column ranges
 (every output column is independent), so a 1 GiB object checks in seconds.
 """
 import ctypes
@@ -82,7 +84,7 @@ def oracle_recover(chunks, have):
     return outs
 
 
-def _symbol_case(torch, need, total, mib, nobj, check_obj):
+def _symbol_case(torch, need, total, mib, nobj, check_obj, erasures=None):
     from slime_amd import device as D
     L = -(-(-(-(mib << 20) // 4)) // need)
     SS = -(-L // 64) * 64  # bench.py's device layout (256 B shard stride)
@@ -101,7 +103,7 @@ def _symbol_case(torch, need, total, mib, nobj, check_obj):
         assert np.array_equal(shards[need + i], ref[i]), f"parity row {need + i}"
     del ref
     # decode: two erasure sets, rebuilt into a separate buffer
-    for erase in ([0, 1, 2, 3], [0, 3, need, total - 1]):
+    for erase in erasures or ([0, 1, 2, 3], [0, 3, need, total - 1]):
         have = [i for i in range(total) if i not in erase][:need]
         out = torch.empty(nobj * len(erase) * SS, dtype=torch.int32, device="cuda")
         D.Plan.reconstruct(need, total, have, erase)(buf, lay, out, D.layout_of(len(erase), L, SS), L, nobj)
@@ -128,6 +130,13 @@ def test_c5_every_symbol_vs_oracle(torch_dev):
     _symbol_case(torch_dev, 10, 14, 1024, 1, 0)
 
 
+def test_c2_every_symbol_vs_oracle(torch_dev):
+    """C2 (4/6, 64 MiB objects, a batch of 32: the launch geometry of
+    BASELINE's C2) encode + decodes of {0,1} and {0,5}, every symbol of
+    in-batch object 17."""
+    _symbol_case(torch_dev, 4, 6, 64, 32, 17, erasures=([0, 1], [0, 5]))
+
+
 # ------------------------------------------------------------ fused byte path
 
 def _oracle_chunks_threaded(obj: bytes, need: int, total: int, cands=()):
@@ -139,54 +148,68 @@ def _oracle_chunks_threaded(obj: bytes, need: int, total: int, cands=()):
     return m, [OC.map_from_gf(m, p) for p in parts + parity]
 
 
-def _bytes_case(torch, need, total, mib):
+def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None):
+    """Objects at[0] (uniform random) and at[1] (forced to mapping 1<<31) of an
+    nobj-object batch, every chunk byte against the oracle's framing; the
+    other objects are random bytes drawn on the device."""
     from slime_amd import device as D
     S = mib << 20
     L, chunk, slot = D.slot_geometry(S, need, total)
     rng = np.random.default_rng(mib * 131 + need)
     objs = [rng.integers(0, 256, size=S, dtype=np.uint8) for _ in range(2)]
-    # Object 1: a word >= p and no word that 1<<31 would map to >= p, so
-    # MapToGF picks 1<<31 (map.go:47-62).  Object 0 stays uniform random (at
-    # 1 GiB about a quarter of such objects need 1<<31 or the random fallback).
+    # at[1]: a word >= p and no word that 1<<31 would map to >= p, so MapToGF
+    # picks 1<<31 (map.go:47-62).  at[0] stays uniform random (at 1 GiB about
+    # a quarter of such objects need 1<<31 or the random fallback).
     w = objs[1].view(">u4")
     w[(w >= 0x7FFFFFFB) & (w <= 0x7FFFFFFF)] = 0x12345678
     w[0] = 0xFFFFFFFF
-    host = np.zeros(2 * slot, dtype=np.uint8)
-    for o in range(2):
-        host[o * slot: o * slot + S] = objs[o]
-    slots = torch.from_numpy(host).cuda()
-    del host
+    if nobj == 2:
+        host = np.zeros(2 * slot, dtype=np.uint8)
+        slots = None
+    else:
+        gen = torch.Generator(device="cuda").manual_seed(mib + nobj)
+        slots = torch.randint(0, 256, (nobj * slot,), dtype=torch.uint8, device="cuda", generator=gen)
+    for i, o in enumerate(at):
+        if slots is None:
+            host[o * slot: o * slot + S] = objs[i]
+        else:
+            slots[o * slot: o * slot + S].copy_(torch.from_numpy(objs[i]))
+    if slots is None:
+        slots = torch.from_numpy(host).cuda()
+        del host
     enc = D.Plan.encode(need, total)
-    mapping = torch.empty(2, dtype=torch.int32, device="cuda")
-    status = torch.empty(2, dtype=torch.int32, device="cuda")
-    D.encode_objects(enc, slots, slot, S, 2, mapping, status)
+    mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    D.encode_objects(enc, slots, slot, S, nobj, mapping, status)
     torch.cuda.synchronize()
     st = status.cpu().numpy().tolist()
-    assert st[1] == 0
-    if st[0]:  # MapToGF's random fallback (map.go:64-66): resolved on the device
-        assert D.resolve_fallbacks(enc, slots, slot, S, 2, mapping, status) == 1
+    assert st[at[1]] == 0
+    if any(st):  # MapToGF's random fallback (map.go:64-66): resolved on the device
+        assert D.resolve_fallbacks(enc, slots, slot, S, nobj, mapping, status) == sum(st)
     ms = mapping.cpu().numpy().view(np.uint32).tolist()
-    for o in range(2):
+    truth = {}
+    for i, o in enumerate(at):
         cands = [ms[o]] if ms[o] not in (0, 1 << 31) else []
-        m, want = _oracle_chunks_threaded(objs[o].tobytes(), need, total, cands)
+        m, want = _oracle_chunks_threaded(objs[i].tobytes(), need, total, cands)
         assert ms[o] == m, o
         got = slots[o * slot: (o + 1) * slot].cpu().numpy()
         for c in range(total):
             assert got[c * chunk:(c + 1) * chunk].tobytes() == want[c], (o, c)
-        if o == 1:
+        if i == 1:
             assert m == 1 << 31
-        truth = want
-    # repair (C4 erasures) of both objects; compare the rebuilt chunk bytes of object 1
-    for erase in ([0, 1, 2, 3], [0, 3, need, total - 1]):
+        truth[o] = want
+    # repair of every object; compare the rebuilt chunk bytes of both checked objects
+    for erase in erasures or ([0, 1, 2, 3], [0, 3, need, total - 1]):
         have = [i for i in range(total) if i not in erase][:need]
         rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
-        v = slots.view(2, slot)[:, : total * chunk].view(2, total, chunk)
+        v = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)
         v[:, erase, :] = 0x5A
-        D.decode_objects(rec, slots, slot, L, 2, mapping)
+        D.decode_objects(rec, slots, slot, L, nobj, mapping)
         torch.cuda.synchronize()
-        got = slots[slot: 2 * slot].cpu().numpy()
-        for c in erase:
-            assert got[c * chunk:(c + 1) * chunk].tobytes() == truth[c], (erase, c)
+        for o in at:
+            got = slots[o * slot: (o + 1) * slot].cpu().numpy()
+            for c in erase:
+                assert got[c * chunk:(c + 1) * chunk].tobytes() == truth[o][c], (o, erase, c)
     del slots
     torch.cuda.empty_cache()
 
@@ -197,3 +220,9 @@ def test_c3_bytes_every_byte_vs_oracle(torch_dev):
 
 def test_c5_bytes_every_byte_vs_oracle(torch_dev):
     _bytes_case(torch_dev, 10, 14, 1024)
+
+
+def test_c2_bytes_every_byte_vs_oracle(torch_dev):
+    """C2's batch (4/6, 32 x 64 MiB): objects 5 (random) and 22 (1<<31) of the
+    batch, encode and the repairs of {0,1} and {0,5}, every byte."""
+    _bytes_case(torch_dev, 4, 6, 64, nobj=32, at=(5, 22), erasures=([0, 1], [0, 5]))

@@ -6,9 +6,15 @@ internal/rs/vector.go:90-102) and against each other, bit-exact.
 The dynamic schedule deals units of tiles over eight ticket counters; the cases
 here cover units that straddle object ends, empty sub-units, objects shorter
 than one tile (only column tails), many objects per counter, and consecutive
-launches on one stream and on two streams (each launch zeroes the counter set
-the next launch on its stream uses).
+launches on one stream and on two streams.  Every launch leaves its counter
+set zero and the library hands a set only to a launch no unfinished launch
+shares it with, whatever the stream: hipStreamPerThread from two threads, a
+stream destroyed with its launch in flight and its handle reused, and a
+launch captured into a graph and replayed are all exact.
 """
+import ctypes
+import threading
+
 import numpy as np
 import pytest
 
@@ -155,10 +161,11 @@ def test_dynamic_schedule_full_batch_matches_static(torch_dev, schedule):
 
 
 def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
-    """A launch captured into a graph replays with the same arguments, so it
-    must not depend on ticket counters that only the next launch zeroes:
-    captured launches take the static kernels.  Replay a captured encode and
-    repair three times over changing data, every time exact."""
+    """A captured launch replays with the same arguments, its ticket counter
+    set included: each replay leaves the set zero for the next, so captured
+    launches keep the dynamic schedule (the graph holds one set per captured
+    queue launch).  Replay a captured encode and repair three times over
+    changing data, every time exact."""
     torch = torch_dev
     from slime_amd import device as D
     assert schedule(1) == 0
@@ -175,10 +182,14 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
     with torch.cuda.stream(s):  # warm the plans' launch path outside the capture
         enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
     torch.cuda.synchronize()
+    _, held0 = N.ticket_sets(0)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
         rec(buf, lay, out, D.layout_of(len(erase), L), L, nobj, stream=s)
+    torch.cuda.synchronize()
+    _, held1 = N.ticket_sets(0)
+    assert held1 == held0 + 2, "both captured launches took the dynamic schedule"
     rng = np.random.default_rng(5)
     for _ in range(3):
         h = _objects(rng, nobj, total, L)
@@ -192,3 +203,124 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
         r = out.cpu().numpy().view(np.uint32).reshape(nobj, len(erase), L)
         for i, t in enumerate(erase):
             assert np.array_equal(r[:, i], (ref[:, t].astype(np.uint64) % P).astype(np.uint32)), t
+
+
+HIP_STREAM_PER_THREAD = 2  # (hipStream_t)2, hip_runtime_api.h
+
+
+def _hip():
+    """The HIP runtime torch loaded (same soname, so dlopen returns it)."""
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def test_stream_per_thread_from_two_threads(torch_dev, schedule):
+    """Two host threads launch interleaved encodes on hipStreamPerThread: one
+    handle, a different stream per thread, so the launches are unordered
+    against each other.  Every object exact, and every counter set is back in
+    the pool once the device is idle."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(1) == 0
+    need, total = 8, 12
+    plan = D.Plan.encode(need, total)
+    rng = np.random.default_rng(21)
+    shapes = [(7, 3 * 768 * 4 + 11), (3, 96 * 1024 + 5), (12, 2 * 768 * 4), (1, 4099)]
+    jobs = []
+    for t in range(2):
+        mine = []
+        for rep in range(6):
+            nobj, L = shapes[(t + rep) % len(shapes)]
+            h = _objects(rng, nobj, total, L)
+            mine.append((h, torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda(), nobj, L))
+        jobs.append(mine)
+    torch.cuda.synchronize()
+    _, held0 = N.ticket_sets(0)
+    errors = []
+    barrier = threading.Barrier(2)
+
+    def run(mine):
+        try:
+            torch.cuda.set_device(0)
+            barrier.wait()
+            for h, buf, nobj, L in mine:
+                lay = D.layout_of(total, L)
+                plan(buf, lay, buf, lay, L, nobj, stream=HIP_STREAM_PER_THREAD, dst_offset=need * L)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(mine,)) for mine in jobs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for mine in jobs:
+        for h, buf, nobj, L in mine:
+            got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+            assert np.array_equal(got, _encode_ref(h, need, total)), (nobj, L)
+    # The device is idle: every set the 12 launches took is back in the pool.
+    _, held1 = N.ticket_sets(0)
+    assert held1 == held0
+
+
+def test_stream_destroyed_in_flight_and_handle_reused(torch_dev, schedule):
+    """A stream destroyed while its launch still runs, then a new stream (the
+    runtime may hand back the same handle) launching at once: the two launches
+    are unordered, and both results are exact."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(1) == 0
+    hip = _hip()
+    need, total = 8, 12
+    plan = D.Plan.encode(need, total)
+    rng = np.random.default_rng(33)
+    big_n, big_L = 24, 256 * 1024  # a launch long enough to still run at the destroy
+    big = _objects(rng, big_n, total, big_L)
+    small = [(_objects(rng, n, total, L), n, L) for n, L in [(5, 3 * 768 * 4 + 1), (9, 40000), (2, 7)]]
+    bufs = [torch.from_numpy(big.view(np.int32).reshape(-1).copy()).cuda()]
+    bufs += [torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda() for h, _, _ in small]
+    torch.cuda.synchronize()
+    handles = []
+    for rep in range(3):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0  # hipStreamNonBlocking
+        handles.append(s.value)
+        if rep == 0:
+            plan(bufs[0], D.layout_of(total, big_L), bufs[0], D.layout_of(total, big_L), big_L, big_n,
+                 stream=s.value, dst_offset=need * big_L)
+        h, n, L = small[rep]
+        plan(bufs[1 + rep], D.layout_of(total, L), bufs[1 + rep], D.layout_of(total, L), L, n, stream=s.value,
+             dst_offset=need * L)
+        assert hip.hipStreamDestroy(ctypes.c_void_p(s.value)) == 0  # launches still in flight
+    torch.cuda.synchronize()
+    got = bufs[0].cpu().numpy().view(np.uint32).reshape(big_n, total, big_L)
+    assert np.array_equal(got, _encode_ref(big, need, total))
+    for (h, n, L), buf in zip(small, bufs[1:]):
+        got = buf.cpu().numpy().view(np.uint32).reshape(n, total, L)
+        assert np.array_equal(got, _encode_ref(h, need, total)), (n, L)
+
+
+def test_counter_sets_are_reused_not_grown(torch_dev, schedule):
+    """Sequential launches on one stream reuse the pool's sets: 200 launches
+    allocate no new slab once the first exists."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(1) == 0
+    need, total, nobj, L = 4, 6, 3, 4096
+    plan = D.Plan.encode(need, total)
+    buf = torch.zeros(nobj * total * L, dtype=torch.int32, device="cuda")
+    D.fill_symbols(buf, seed=3)
+    lay = D.layout_of(total, L)
+    plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    sets0, _ = N.ticket_sets(0)
+    for _ in range(200):
+        plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    sets1, _ = N.ticket_sets(0)
+    assert sets1 == sets0

@@ -298,7 +298,7 @@ extern "C" int av_launch_timed(const uint32_t* in, uint32_t* out, uint64_t io, u
 
 // Dynamic-schedule walk (rs_apply_queue_kernel<K, 3, C, NC, .., TB, STAMP>), k = 8 or 10.
 // C argument = C + 100 * NC + 10000 * TB + 100000 * U (TB = tickets per atomic, 1 when 0; U = 3 when 0);
-// tickets (16 x 64 words, then the zero_next set) zeroed by the caller;
+// tickets: a counter set of NC + 1 lines (64 words each), zero at launch (each launch leaves it zero);
 // stamps (3 words per wave) recorded when non-null.
 extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo,
                                uint64_t os, const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi,
@@ -306,17 +306,16 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
                                void* ticket, void* stamps, uint32_t spread) {
   hipStream_t s = (hipStream_t)stream;
   uint32_t* t = (uint32_t*)ticket;
-  uint32_t* z = t + 16 * kTicketStride;
   if ((C / 10000) % 10 == 0) C += 10000;  // TB defaults to 1
 #define QU(KK, UU, CC, NN, TT)                                                                                   \
   if (k == KK && C == CC + 100 * NN + 10000 * TT + 100000 * (UU == 3 ? 0 : UU)) {                              \
     if (stamps)                                                                                                 \
       hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, true>), dim3(blocks), dim3(kBlock), \
-                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
+                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t,    \
                          (uint64_t*)stamps, spread);                                                            \
     else                                                                                                        \
       hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, false>), dim3(blocks), dim3(kBlock), \
-                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z,    \
+                         0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t,    \
                          nullptr, spread);                                                                      \
     return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
@@ -326,7 +325,7 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
   if (k == KK && C == CC + 100 * NN + 10000 * TT + 100000 * (UU == 3 ? 0 : UU) + 1000000) {                    \
     hipLaunchKernelGGL((rs_apply_queue_kernel<KK, UU, CC, NN, true, true, TT, false, true>), dim3(blocks),        \
                        dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, \
-                       t, z, nullptr, spread);                                                                  \
+                       t, nullptr, spread);                                                                  \
     return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
   QS(8, 3, 2, 8, 1) QS(8, 3, 2, 8, 2) QS(8, 3, 2, 8, 4) QS(8, 3, 2, 8, 8) QS(8, 3, 4, 8, 2)
@@ -335,7 +334,7 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
 #define QN(KK, CC, NN, LL, SS)                                                                                   \
   if (k == KK && C == CC + 100 * NN + 10000 + 10000000 * (1 + 2 * !LL + !SS)) {                                  \
     hipLaunchKernelGGL((rs_apply_queue_kernel<KK, 3, CC, NN, LL, SS>), dim3(blocks), dim3(kBlock), 0, s, in, out, io, \
-                       is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, z, nullptr, spread);       \
+                       is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)KK, t, nullptr, spread);       \
     return hipGetLastError() == hipSuccess ? 0 : -3;                                                            \
   }
   QN(8, 2, 8, true, false) QN(8, 2, 8, false, true) QN(8, 2, 8, false, false)

@@ -1,0 +1,64 @@
+#!/usr/bin/env bash
+# Round-3 GPU-box session: every GPU step under its own time limit; the first
+# crash/abort/timeout ends the session (nothing more runs on the GPU).
+# Usage (repo root, on the box):  bash tools/gpu_r03.sh <step> [<step>...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0"
+
+run() {  # run <name> <limit-seconds> <command...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then
+    echo "!!! $name ended with rc=$rc: stopping the session" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+}
+
+nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+for step in "$@"; do
+  case "$step" in
+    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    tests_sched) run pytest_sched 400 python -u -m pytest tests/test_gpu_schedule.py -x -v --timeout 120 --timeout-method thread ;;
+    tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
+            python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
+    pmc_fetch) run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
+    pmc_write) run pmc_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
+    # byte-path kernels (object_bytes_path leg) at C3 and C5: kernel stats + traffic passes
+    bprof_c3) run bprof_c3 600 rocprofv3 --kernel-trace --stats -d "$OUT/bprof_c3" -o bench --output-format csv -- \
+            python3 bench.py --steps 5 --warmup 1 $NOLEGS ;;
+    bprof_c5) run bprof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/bprof_c5" -o bench --output-format csv -- \
+            python3 bench.py --preset c5 --global-objects 16 --steps 5 --warmup 1 $NOLEGS ;;
+    bpmc_c3) run bpmc_c3_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/bpmc_c3_fetch" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 $NOLEGS &&
+          run bpmc_c3_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/bpmc_c3_write" -o pmc \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 $NOLEGS ;;
+    bpmc_c5) run bpmc_c5_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/bpmc_c5_fetch" -o pmc \
+            --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
+          run bpmc_c5_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/bpmc_c5_write" -o pmc \
+            --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
+    shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
+            run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
+            run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
+    c5_64) run c5_64 600 python bench.py --preset c5 $NOLEGS ;;
+    c2tail) run c2tail 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 2 --rounds 5 --queue 400802 --timed 3 ;;
+    torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
+    gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session done" | tee -a "$OUT/session.log"

@@ -5,7 +5,8 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): counters are in KiB; FETCH_SIZE
 reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
 so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r02/pmc_traffic.json
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r03/pmc_traffic.json
+    python tools/pmc_traffic.py --all <fetch_dir> <write_dir>    # every kernel: HBM bytes per dispatch
 
 `kernel_source` (hash of the apply kernel sources, as bench.py's
 kernel_source_id) ties the summary to the build it was measured on: bench.py
@@ -42,7 +43,32 @@ def per_dispatch(d, counter):
     return vals, seen
 
 
+def all_kernels(fetch_dir, write_dir):
+    """Per kernel (template name up to '<'): dispatches and mean read / write
+    bytes per dispatch, with the same gfx950 corrections."""
+    acc = {}
+    for d, counter in ((fetch_dir, "FETCH_SIZE"), (write_dir, "WRITE_SIZE")):
+        for path in glob.glob(f"{d}/*counter_collection.csv"):
+            for r in csv.DictReader(open(path)):
+                if r["Counter_Name"] != counter:
+                    continue
+                name = r["Kernel_Name"].split("(")[0]
+                e = acc.setdefault(name, {"FETCH_SIZE": [], "WRITE_SIZE": []})
+                e[counter].append(float(r["Counter_Value"]))
+    out = {}
+    for name, e in sorted(acc.items()):
+        f, w = e["FETCH_SIZE"], e["WRITE_SIZE"]
+        rd = 2 * 1024 * sum(f) / len(f) if f else None
+        wr = 1024 * sum(w) / len(w) if w else None
+        out[name] = {"dispatches": [len(f), len(w)], "read_bytes": int(rd) if rd is not None else None,
+                     "write_bytes": int(wr) if wr is not None else None,
+                     "hbm_bytes": int(rd + wr) if rd is not None and wr is not None else None}
+    print(json.dumps(out, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--all":
+        return all_kernels(sys.argv[2], sys.argv[3])
     fetch_dir, write_dir, config = sys.argv[1:4]
     session = sys.argv[4] if len(sys.argv) > 4 else "?"
     f, fk = per_dispatch(fetch_dir, "FETCH_SIZE")
