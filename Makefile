@@ -14,8 +14,13 @@ HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 CXXTEST  := tests/cpp/rs_host_test
 CACHETEST := tests/cpp/plan_cache_test
 COPYTEST := tests/cpp/copy_pool_test
+POOLTEST := tests/cpp/device_pool_test
 
-all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST)
+
+# Device routing of host calls (device_pool.hpp) with a fixed device count, CPU only.
+$(POOLTEST): tests/cpp/device_pool_test.cpp $(SRC)/device_pool.hpp $(SRC)/plan_cache.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -I$(SRC) -o $@ tests/cpp/device_pool_test.cpp
 
 # The host copy pool under concurrent callers, CPU only.
 $(COPYTEST): tests/cpp/copy_pool_test.cpp $(SRC)/host_copy.cpp $(SRC)/host_copy.hpp
@@ -47,7 +52,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST)
+	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -725,7 +725,11 @@ def main():
     def run_host_leg():
         if args.host_delay > 0:
             time.sleep(args.host_delay)
-        return dict(host_leg(need, total, erase), order=args.host_order, delay_s=args.host_delay)
+        # This rank's GPU only: the library's device pool would otherwise spread
+        # the host calls over every visible GPU (include/slime_rs.h).
+        from slime_amd import _native as N
+        with N.on_device(dev):
+            return dict(host_leg(need, total, erase), order=args.host_order, delay_s=args.host_delay, device=dev)
 
     if want_host and args.host_order == "before-free":
         host = run_host_leg()

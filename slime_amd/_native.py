@@ -11,8 +11,10 @@ loaded runtime and device pointers/streams from torch tensors are valid here.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import threading
 
 try:  # noqa: SIM105 - see module docstring
     import torch  # noqa: F401
@@ -265,6 +267,30 @@ def ticket_sets(device: int) -> tuple[int, int]:
     s, h = ctypes.c_uint64(), ctypes.c_uint64()
     check(lib.slime_rs_ticket_sets(device, ctypes.byref(s), ctypes.byref(h)))
     return int(s.value), int(h.value)
+
+
+_selected = threading.local()
+
+
+@contextlib.contextmanager
+def on_device(device: int | None):
+    """Route the calling thread's host entry points (rs.*, gf.*, objects.*) to
+    `device` for the block (slime_rs_select_device); None leaves the routing as
+    it is (the device pool picks).  A rank that owns one GPU wraps its host
+    calls in this, so they never spread onto other ranks' devices."""
+    if device is None:
+        yield
+        return
+    stack = getattr(_selected, "stack", None)
+    if stack is None:
+        stack = _selected.stack = []
+    check(lib.slime_rs_select_device(int(device)))
+    stack.append(int(device))
+    try:
+        yield
+    finally:
+        stack.pop()
+        check(lib.slime_rs_select_device(stack[-1] if stack else ANY_DEVICE))
 
 
 def pool_calls(device: int) -> tuple[int, int]:

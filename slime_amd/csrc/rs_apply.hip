@@ -205,23 +205,36 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
 // a set is reusable as soon as the launch that held it has finished -- on any
 // stream.  Per device: a pool of sets, each with an event recorded after the
 // launch that last took it; a set is free when that event has completed.
-// Nothing depends on the identity of the launch stream, so hipStreamPerThread,
-// the per-thread null stream, and a stream destroyed while its last launch
-// runs (its handle then reused by hipStreamCreate) are all safe.  A launch
-// captured into a graph keeps its set for the graph's life: every replay
-// leaves it zero for the next.  Sets come in slabs of kSlabSets, zeroed
-// synchronously when created; creation never happens inside a capture.
+// Nothing trusts the identity of the launch stream: hipStreamPerThread, the
+// per-thread null stream, and a stream destroyed while its last launch runs
+// (its handle then reused by hipStreamCreate) are all safe.
+//
+// When every set is held (more launches queued than sets), a launch takes
+// the set of the latest launch queued under its own stream handle and makes
+// its stream wait for that launch's event first: on a true in-order stream
+// the wait is already implied by stream order, and under a shared or reused
+// handle it orders the two launches.  So a deep queue on one stream runs on a
+// fixed number of sets.  Other streams' launches get new sets (up to
+// kMaxSets, then they too wait for the oldest holder).
+//
+// A launch captured into a graph keeps its set for the graph's life: every
+// replay leaves it zero for the next.  Captured launches never wait on
+// events from outside the capture and never create slabs: with no free set
+// they take the static kernel.  Sets come in slabs of kSlabSets, zeroed
+// synchronously when created.
 namespace {
 constexpr uint32_t kSetWords = apply::ticket_set_words(kQueueCounters);
 constexpr int kSlabSets = 64;
+constexpr uint64_t kMaxSets = 1024;
 struct TicketSet {
   uint32_t* p = nullptr;
   hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;  // stream handle of the launch that last took it
 };
 struct TicketPool {
   std::mutex mu;
   std::vector<TicketSet> free_sets;  // zero, no launch holds them
-  std::deque<TicketSet> busy;        // held by a launch, oldest first
+  std::deque<TicketSet> busy;        // held by a launch, in launch order
   uint64_t sets = 0, graph_held = 0;
 
   hipError_t grow() {  // mu held; not inside a capture
@@ -245,8 +258,6 @@ struct TicketPool {
     }
     return hipSuccess;
   }
-  // A free set, reclaiming finished launches' sets first.  false: none (and
-  // `may_grow` forbade a new slab).
   void reclaim() {  // mu held: every set whose launch has finished goes back
     for (auto it = busy.begin(); it != busy.end();) {
       const hipError_t q = hipEventQuery(it->ev);
@@ -259,10 +270,27 @@ struct TicketPool {
       }
     }
   }
-  bool take(TicketSet* out, bool may_grow, hipError_t* err) {
+  // Hand `stream` the busy set at `it` once its holder is done (see above).
+  bool take_busy(std::deque<TicketSet>::iterator it, hipStream_t stream, TicketSet* out, hipError_t* err) {
+    if ((*err = hipStreamWaitEvent(stream, it->ev, 0)) != hipSuccess) return false;
+    *out = *it;
+    busy.erase(it);
+    return true;
+  }
+  // A set for a launch on `stream`.  false: none to be had (*err says why,
+  // hipSuccess for a capture with no free set).
+  bool take(hipStream_t stream, bool cap, TicketSet* out, hipError_t* err) {
     *err = hipSuccess;
     if (free_sets.empty()) reclaim();
-    if (free_sets.empty() && may_grow) *err = grow();
+    if (free_sets.empty() && !cap) {
+      for (auto it = busy.rbegin(); it != busy.rend(); ++it)
+        if (it->last == stream) return take_busy(std::next(it).base(), stream, out, err);
+      if (sets < kMaxSets) {
+        if ((*err = grow()) != hipSuccess) return false;
+      } else if (!busy.empty()) {
+        return take_busy(busy.begin(), stream, out, err);
+      }
+    }
     if (free_sets.empty()) return false;
     *out = free_sets.back();
     free_sets.pop_back();
@@ -305,16 +333,15 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
   if (hipError_t e = hipGetDevice(&dev)) return e;
   const bool cap = capturing(stream);
   TicketPool& tp = ticket_pool(dev);
-  TicketSet set;
-  {
-    std::lock_guard<std::mutex> lock(tp.mu);
-    hipError_t e;
-    if (!tp.take(&set, !cap, &e)) return e;  // hipSuccess + !launched: static kernel
-  }
-  const hipError_t e = launch(set.p);
+  // The pool's lock is held across the launch: a set handed over behind an
+  // event wait must see its event re-recorded before anyone else looks.
   std::lock_guard<std::mutex> lock(tp.mu);
-  if (e != hipSuccess) {  // never started: the set is still zero
-    tp.free_sets.push_back(set);
+  TicketSet set;
+  hipError_t e;
+  if (!tp.take(stream, cap, &set, &e)) return e;  // hipSuccess + !launched: static kernel
+  e = launch(set.p);
+  if (e != hipSuccess) {  // never started: the set is zero again once its holder (if any) is done
+    tp.busy.push_back(set);
     return e;
   }
   *launched = true;
@@ -327,6 +354,7 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
     ++tp.graph_held;
     return r;
   }
+  set.last = stream;
   tp.busy.push_back(set);
   return hipSuccess;
 }

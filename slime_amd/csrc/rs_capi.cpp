@@ -26,6 +26,7 @@
 #include <tuple>
 #include <vector>
 
+#include "device_pool.hpp"
 #include "digest.hpp"
 #include "gfp_host.hpp"
 #include "host_copy.hpp"
@@ -104,56 +105,29 @@ struct DeviceScope {
 };
 
 // ---- device pool (host entry points) -------------------------------------------
-//
-// The reference's callers are concurrent (up to `parallel-requests` HTTP
-// goroutines, main.go:107-109, plus scrubbers, multi.go:54-58), and objects
-// are independent.  A host call that does not name a
-// device takes the visible GPU with the fewest calls in flight (ties: round
-// robin), so concurrent callers spread over every GPU of the node with no
-// data-path exchange.  Each device has its own workspaces and plans.
-struct DevicePool {
-  static constexpr int kMax = 64;
-  std::atomic<int> inflight[kMax] = {};
-  std::atomic<uint64_t> calls[kMax] = {};
-  std::atomic<uint64_t> next{0};
-  int pick() {
-    const int n = std::min(visible_devices(), kMax);
-    const int start = (int)(next.fetch_add(1, std::memory_order_relaxed) % (uint64_t)n);
-    int best = start;
-    for (int i = 1; i < n; ++i) {
-      const int d = (start + i) % n;
-      if (inflight[d].load(std::memory_order_relaxed) < inflight[best].load(std::memory_order_relaxed)) best = d;
-    }
-    return best;
-  }
-};
+// Routing policy and its CPU test: device_pool.hpp.  Each device has its own
+// workspaces and plans (plan keys and workspaces carry the device).
 DevicePool g_pool;
+
+const std::vector<int>& pool_devices() {
+  static const std::vector<int> devs = DevicePool::allowed(visible_devices(), getenv("SLIME_RS_DEVICES"));
+  return devs;
+}
 
 // The device of one host call: the *_ex call's explicit device, else the
 // thread's selected device, else the pool's pick.  Holds the pool slot for
 // the life of the call.
 struct DeviceLease {
+  PoolLease lease;
   int device = -1;
-  bool pooled = false;
   int acquire() {
-    int want = t_call ? t_call->device : SLIME_RS_ANY_DEVICE;
-    if (want == SLIME_RS_ANY_DEVICE && !t_call) want = t_device;
-    if (want != SLIME_RS_ANY_DEVICE) {
-      if (int rc = check_device(want)) return rc;
-      device = want;
-    } else {
-      if (int rc = check_device(0)) return rc;
-      device = g_pool.pick();
-    }
-    if (device < DevicePool::kMax) {
-      pooled = true;
-      g_pool.inflight[device].fetch_add(1, std::memory_order_relaxed);
-      g_pool.calls[device].fetch_add(1, std::memory_order_relaxed);
-    }
+    const int call = t_call ? t_call->device : SLIME_RS_ANY_DEVICE;
+    const int thread = t_call ? SLIME_RS_ANY_DEVICE : t_device;
+    const int want = call != SLIME_RS_ANY_DEVICE ? call : thread;
+    if (int rc = check_device(want != SLIME_RS_ANY_DEVICE ? want : 0)) return rc;
+    lease.take(g_pool, call, thread, pool_devices());
+    device = lease.device;
     return 0;
-  }
-  ~DeviceLease() {
-    if (pooled) g_pool.inflight[device].fetch_sub(1, std::memory_order_relaxed);
   }
 };
 
@@ -361,22 +335,12 @@ struct Workspace {
   }
 };
 
-std::mutex g_ws_mu;
-std::vector<Workspace*> g_ws_free;
+PerDeviceFreeList<Workspace> g_ws_free;  // most recently released first (device_pool.hpp)
 
-// Most recently released first: a caller's next call gets the workspace its
-// last call grew (buffers sized, pages warm), instead of cycling through every
-// workspace that a burst of concurrent calls once created and regrowing each.
 int acquire_ws(int device, Workspace** out) {
-  {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (size_t i = g_ws_free.size(); i-- > 0;) {
-      if (g_ws_free[i]->device == device) {
-        *out = g_ws_free[i];
-        g_ws_free.erase(g_ws_free.begin() + (long)i);
-        return 0;
-      }
-    }
+  if (Workspace* ws = g_ws_free.take(device)) {
+    *out = ws;
+    return 0;
   }
   auto ws = std::make_unique<Workspace>();
   ws->device = device;
@@ -386,10 +350,7 @@ int acquire_ws(int device, Workspace** out) {
   return 0;
 }
 
-void release_ws(Workspace* ws) {
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  g_ws_free.push_back(ws);
-}
+void release_ws(Workspace* ws) { g_ws_free.give(ws); }
 
 struct WsLease {
   Workspace* ws = nullptr;

@@ -37,12 +37,34 @@ def _dev_index(t: torch.Tensor) -> int:
 _TYPESTR = {torch.int32: "<i4", torch.uint8: "|u1", torch.int64: "<i8", torch.uint32: "<u4"}
 
 
+_deferred_frees: list = []  # buffers dropped while a graph capture was running
+
+
+def _capturing() -> bool:
+    try:
+        return bool(torch.cuda.is_current_stream_capturing())
+    except Exception:  # pragma: no cover - no device / interpreter shutdown
+        return False
+
+
+def release_deferred() -> None:
+    """Free the device buffers whose last tensor died during a graph capture
+    (called on the next allocation or drop outside a capture)."""
+    while _deferred_frees and not _capturing():
+        lib.slime_rs_device_free(ctypes.c_void_p(_deferred_frees.pop()))
+
+
 class _DeviceBuffer:
     """A slime_rs_device_alloc buffer exposed through __cuda_array_interface__;
     freed when the last tensor viewing it is gone (torch.as_tensor keeps its
-    source object alive for the tensor's lifetime)."""
+    source object alive for the tensor's lifetime).  The free waits for the
+    device (hipDeviceSynchronize: work queued on any stream may still touch
+    the range), which a graph capture forbids: a buffer dropped during a
+    capture on this thread's current stream is freed at the next allocation
+    or drop outside one (release_deferred)."""
 
     def __init__(self, device: int, numel: int, dtype: torch.dtype):
+        release_deferred()
         itemsize = torch.empty((), dtype=dtype).element_size()
         p = ctypes.c_void_p()
         N.check(lib.slime_rs_device_alloc(device, max(1, numel * itemsize), ctypes.byref(p)))
@@ -53,7 +75,11 @@ class _DeviceBuffer:
     def __del__(self):
         if getattr(self, "ptr", None):
             try:
-                lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))  # waits for the device, then unmaps
+                if _capturing():
+                    _deferred_frees.append(self.ptr)
+                else:
+                    lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))  # waits for the device, then unmaps
+                    release_deferred()
             except Exception:  # pragma: no cover - interpreter shutdown
                 pass
             self.ptr = None

@@ -28,10 +28,15 @@ def Raise(x: int, n: int) -> int:
 
 
 def _bytes(b) -> np.ndarray:
-    """A uint8 view of b (bytes, bytearray, memoryview, ndarray) without copying it."""
+    """A uint8 view of b (bytes, bytearray, memoryview, ndarray) without
+    copying it; other byte sequences (e.g. a list of ints) go through bytes()."""
     if isinstance(b, np.ndarray):
         return np.ascontiguousarray(b).view(np.uint8).reshape(-1)
-    return np.frombuffer(memoryview(b).cast("B"), dtype=np.uint8) if len(b) else np.zeros(0, dtype=np.uint8)
+    try:
+        mv = memoryview(b).cast("B")
+    except TypeError:
+        mv = memoryview(bytes(b))
+    return np.frombuffer(mv, dtype=np.uint8) if mv.nbytes else np.zeros(0, dtype=np.uint8)
 
 
 def MapToGF(data) -> tuple[int, np.ndarray]:
@@ -54,8 +59,12 @@ def MapToGFWith(data, n: int) -> np.ndarray:
 
 
 def MapFromGF(n: int, v) -> bytearray:
-    """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v)); a
-    bytearray, Go's mutable []byte, written in place by the library."""
+    """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v)).
+
+    Returns a bytearray: Go's []byte is mutable (and, like a bytearray, not
+    usable as a map key), and the library writes the result in place with no
+    extra 4*len(v)-byte copy.  Use bytes(...) where an immutable, hashable
+    value is needed."""
     words = np.ascontiguousarray(v, dtype=np.uint32)
     out = bytearray(words.size * 4)
     ptr = (ctypes.c_char * len(out)).from_buffer(out) if out else None

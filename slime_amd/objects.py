@@ -51,18 +51,21 @@ def _bytes_view(data) -> np.ndarray:
     return np.frombuffer(memoryview(data), dtype=np.uint8)
 
 
-def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None = None, alias: bool = False
-                 ) -> tuple[int, list[np.ndarray]]:
+def write_chunks(data, need: int, total: int, out: Sequence[np.ndarray] | None = None, alias: bool = False,
+                 device: int | None = None) -> tuple[int, list[np.ndarray]]:
     """(MappingValue, [total chunk byte arrays]) for an object, as writeChunks
     stores them.  `out`: caller-owned uint8 chunk buffers (>= chunk_size bytes
     each) written in place and returned as views.  alias=True returns the data
-    chunks that lie wholly inside the object as views of `data` (no copy)."""
+    chunks that lie wholly inside the object as views of `data` (no copy).
+    `device`: run on that GPU (default: the thread's selection, else the
+    library's device pool)."""
     buf = _bytes_view(data)
     chunks = _chunk_out(buf, need, total, out, alias)
     ptrs = (ctypes.c_void_p * max(len(chunks), 1))(*[c.ctypes.data for c in chunks])
     m = ctypes.c_uint32(0)
-    N.check(lib.slime_rs_write_chunks(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
-                                      ctypes.byref(m)))
+    with N.on_device(device):
+        N.check(lib.slime_rs_write_chunks(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
+                                          ctypes.byref(m)))
     return int(m.value), chunks
 
 
@@ -85,7 +88,7 @@ def _chunk_out(buf: np.ndarray, need: int, total: int, out, alias: bool = False)
 
 
 def write_chunks_digest(data, need: int, total: int, out: Sequence[np.ndarray] | None = None,
-                        headers: bool = False, alias: bool = False
+                        headers: bool = False, alias: bool = False, device: int | None = None
                         ) -> tuple[int, list[np.ndarray], list[bytes], list[bytes] | None]:
     """write_chunks plus each chunk's SHA-256 (what writeChunks' store.DataV
     stores, multi_store.go:554-556) and, with headers=True, each chunk file's
@@ -97,9 +100,10 @@ def write_chunks_digest(data, need: int, total: int, out: Sequence[np.ndarray] |
     sha = np.zeros(max(total, 1) * 32, dtype=np.uint8)
     hdr = np.zeros(max(total, 1) * 8, dtype=np.uint8) if headers else None
     m = ctypes.c_uint32(0)
-    N.check(lib.slime_rs_write_chunks_digest(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
-                                             ctypes.byref(m), sha.ctypes.data,
-                                             hdr.ctypes.data if hdr is not None else None))
+    with N.on_device(device):
+        N.check(lib.slime_rs_write_chunks_digest(buf.ctypes.data if buf.size else None, buf.size, need, total, ptrs,
+                                                 ctypes.byref(m), sha.ctypes.data,
+                                                 hdr.ctypes.data if hdr is not None else None))
     shas = [sha[32 * i:32 * i + 32].tobytes() for i in range(max(total, 0))]
     hdrs = [hdr[8 * i:8 * i + 8].tobytes() for i in range(max(total, 0))] if hdr is not None else None
     return int(m.value), chunks, shas, hdrs
@@ -128,7 +132,7 @@ def chunk_digests(chunks: Sequence, headers: bool = False) -> tuple[list[bytes],
 
 
 def reconstruct(chunks: Sequence, indices: Sequence[int], mapping: int, size: int,
-                out: np.ndarray | None = None, sha: bytes | None = None) -> np.ndarray:
+                out: np.ndarray | None = None, sha: bytes | None = None, device: int | None = None) -> np.ndarray:
     """The object's bytes (uint8 array) from `need` surviving chunks
     (reconstruct's slow path).  `out`: caller-owned uint8 buffer of >= size bytes.
     With `sha` (the file's SHA256) the result is verified and a mismatch
@@ -146,13 +150,14 @@ def reconstruct(chunks: Sequence, indices: Sequence[int], mapping: int, size: in
     elif out.dtype != np.uint8 or not out.flags.c_contiguous or not out.flags.writeable or out.size < size:
         raise ValueError("reconstruct: out must be a writeable contiguous uint8 array of >= size bytes")
     out = out[:size]
-    if sha is not None:
-        want = np.frombuffer(bytes(sha), dtype=np.uint8)
-        if want.size != 32:
-            raise ValueError("reconstruct: sha must be 32 bytes")
-        N.check(lib.slime_rs_reconstruct_verify(ptrs, idx, len(arrs), cb, mapping & 0xFFFFFFFF, size,
-                                                out.ctypes.data if size else None, want.ctypes.data))
-        return out
-    N.check(lib.slime_rs_reconstruct(ptrs, idx, len(arrs), cb, mapping & 0xFFFFFFFF, size,
-                                     out.ctypes.data if size else None))
+    with N.on_device(device):
+        if sha is not None:
+            want = np.frombuffer(bytes(sha), dtype=np.uint8)
+            if want.size != 32:
+                raise ValueError("reconstruct: sha must be 32 bytes")
+            N.check(lib.slime_rs_reconstruct_verify(ptrs, idx, len(arrs), cb, mapping & 0xFFFFFFFF, size,
+                                                    out.ctypes.data if size else None, want.ctypes.data))
+            return out
+        N.check(lib.slime_rs_reconstruct(ptrs, idx, len(arrs), cb, mapping & 0xFFFFFFFF, size,
+                                         out.ctypes.data if size else None))
     return out

@@ -1,0 +1,151 @@
+// CPU test of the host calls' device routing (slime_amd/csrc/device_pool.hpp)
+// with a fixed device count -- the product's DevicePool, PoolLease and
+// PerDeviceFreeList, and its LruCache keyed by device as rs_capi.cpp keys plans:
+//
+//   - SLIME_RS_DEVICES parsing (allowed set, bad entries dropped);
+//   - 25 concurrent callers (the reference's default parallel-requests,
+//     main.go:107-109) on 8 devices spread evenly, and every workspace and
+//     plan a call gets belongs to the call's device;
+//   - a device named by the call or selected by the thread is honoured;
+//   - an allowed set of one device takes every unpinned call;
+//   - in-flight counts return to zero.
+// Usage: device_pool_test   (exit 0 = pass)
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <random>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "device_pool.hpp"
+#include "plan_cache.hpp"
+
+using namespace slime;
+
+#define CHECK(cond)                                               \
+  do {                                                            \
+    if (!(cond)) {                                                \
+      std::printf("FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      std::exit(1);                                               \
+    }                                                             \
+  } while (0)
+
+struct FakeWorkspace {
+  int device;
+  std::atomic<int> users{0};  // must never exceed 1: a workspace serves one call at a time
+};
+struct FakePlan {
+  int device;
+};
+using Key = std::tuple<int, char, int, int, std::vector<int>>;
+
+static int make_plan(const Key& key, FakePlan** out) {
+  *out = new FakePlan{std::get<0>(key)};
+  return 0;
+}
+static void del_plan(FakePlan* p) { delete p; }
+
+int main() {
+  {  // allowed sets
+    CHECK((DevicePool::allowed(8, nullptr) == std::vector<int>{0, 1, 2, 3, 4, 5, 6, 7}));
+    CHECK((DevicePool::allowed(8, "3") == std::vector<int>{3}));
+    CHECK((DevicePool::allowed(8, "1,1,9,x,2,-1") == std::vector<int>{1, 2}));
+    CHECK((DevicePool::allowed(4, "7") == std::vector<int>{0, 1, 2, 3}));  // nothing valid: all
+    CHECK(DevicePool::allowed(0, nullptr).empty());
+    std::printf("ok   TestAllowedDevices\n");
+  }
+  const int ndev = 8;
+  const std::vector<int> all = DevicePool::allowed(ndev, nullptr);
+  {  // 25 concurrent callers over 8 devices
+    DevicePool pool;
+    PerDeviceFreeList<FakeWorkspace> wsl;
+    LruCache<Key, FakePlan> plans(64);
+    std::vector<std::unique_ptr<FakeWorkspace>> owned;
+    std::mutex owned_mu;
+    std::atomic<int> bad{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 25; ++t)
+      ts.emplace_back([&, t] {
+        std::mt19937 rng(t);
+        for (int c = 0; c < 400; ++c) {
+          PoolLease lease;
+          lease.take(pool, kAnyDevice, kAnyDevice, all);
+          const int dev = lease.device;
+          FakeWorkspace* ws = wsl.take(dev);
+          if (!ws) {
+            auto w = std::make_unique<FakeWorkspace>();
+            w->device = dev;
+            ws = w.get();
+            std::lock_guard<std::mutex> lk(owned_mu);
+            owned.push_back(std::move(w));
+          }
+          if (ws->device != dev || ws->users.fetch_add(1) != 0) ++bad;
+          std::shared_ptr<FakePlan> plan;
+          const std::vector<int> have = {0, 1, 2, 3, 4, 5, 6, 7 + (int)(rng() % 5)};
+          if (plans.get(Key{dev, 'R', 8, 12, have}, &plan, make_plan, del_plan) != 0 || plan->device != dev) ++bad;
+          std::this_thread::sleep_for(std::chrono::microseconds(20 + rng() % 200));
+          ws->users.fetch_sub(1);
+          wsl.give(ws);
+        }
+      });
+    for (auto& th : ts) th.join();
+    CHECK(bad.load() == 0);
+    uint64_t lo = ~0ull, hi = 0, sum = 0;
+    for (int d = 0; d < ndev; ++d) {
+      const uint64_t c = pool.calls[d].load();
+      lo = std::min(lo, c);
+      hi = std::max(hi, c);
+      sum += c;
+      CHECK(pool.inflight[d].load() == 0);
+    }
+    CHECK(sum == 25 * 400);
+    CHECK(hi - lo <= sum / ndev / 5);  // within 20% of the mean share
+    // At most one workspace per caller and device was ever created.
+    CHECK(owned.size() <= (size_t)25 * ndev);
+    std::printf("ok   TestPoolSpreadsConcurrentCallers (25 callers x 400 calls: %llu..%llu per device, %zu workspaces)\n",
+                (unsigned long long)lo, (unsigned long long)hi, owned.size());
+  }
+  {  // pinned devices are honoured: the call's over the thread's over the pool
+    DevicePool pool;
+    for (int c = 0; c < 100; ++c) {
+      PoolLease a;
+      a.take(pool, kAnyDevice, 5, all);
+      CHECK(a.device == 5);
+      PoolLease b;
+      b.take(pool, 2, 5, all);
+      CHECK(b.device == 2);
+    }
+    CHECK(pool.calls[5].load() == 100 && pool.calls[2].load() == 100);
+    const std::vector<int> only3 = DevicePool::allowed(ndev, "3");
+    for (int c = 0; c < 50; ++c) {
+      PoolLease l;
+      l.take(pool, kAnyDevice, kAnyDevice, only3);
+      CHECK(l.device == 3);
+    }
+    CHECK(pool.calls[3].load() == 50);
+    for (int d = 0; d < ndev; ++d) CHECK(pool.inflight[d].load() == 0);
+    std::printf("ok   TestPinnedDevices\n");
+  }
+  {  // the least-loaded device wins while others are busy
+    DevicePool pool;
+    std::vector<std::unique_ptr<PoolLease>> held;
+    for (int i = 0; i < 3 * ndev; ++i) {
+      held.push_back(std::make_unique<PoolLease>());
+      held.back()->take(pool, kAnyDevice, kAnyDevice, all);
+    }
+    for (int d = 0; d < ndev; ++d) CHECK(pool.inflight[d].load() == 3);
+    held.erase(held.begin());  // frees one slot on the first call's device
+    int freed = -1;
+    for (int d = 0; d < ndev; ++d)
+      if (pool.inflight[d].load() == 2) freed = d;
+    PoolLease next;
+    next.take(pool, kAnyDevice, kAnyDevice, all);
+    CHECK(next.device == freed);
+    std::printf("ok   TestLeastLoaded\n");
+  }
+  std::printf("4/4 passed\n");
+  return 0;
+}

@@ -7,10 +7,15 @@
 //     and every evicted plan's table is released;
 //   - 8 threads sharing the cache with a small cap: a plan a caller holds stays
 //     intact while other threads evict it, and is released once let go;
-//   - a failed build (singular survivor set, matrix.go:68) caches nothing.
+//   - a failed build (singular survivor set, matrix.go:68) caches nothing;
+//   - builds run outside the cache lock: 8 threads missing 8 different keys
+//     with a 50 ms build finish in about 50 ms, not 400; 8 threads missing
+//     the SAME key share one build;
+//   - evicted values are released outside the lock (the deleter checks).
 // Usage: plan_cache_test   (exit 0 = pass)
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -151,6 +156,80 @@ int main() {
     CHECK(cache.size() <= 16 && g_tables.load() == (long)cache.size());
     std::printf("ok   TestPlanCacheConcurrent (8 threads, cap 16)\n");
   }
-  std::printf("3/3 passed\n");
+  {  // slow builds of different keys overlap; the builder never holds the lock
+    LruCache<Key, FakePlan> cache(64);
+    std::atomic<int> builds{0}, locked_builds{0};
+    auto slow = [&](const Key& key, FakePlan** out) {
+      if (cache.held_by_this_thread()) ++locked_builds;
+      ++builds;
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      return build(key, out);
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 8; ++t)
+      ts.emplace_back([&, t] {
+        std::vector<int> have(8);
+        for (int i = 0; i < 8; ++i) have[i] = i + (i >= t ? 1 : 0);  // 8 distinct survivor sets of 8/9
+        std::shared_ptr<FakePlan> p;
+        CHECK(cache.get(Key{t, 'R', 8, 0, have}, &p, slow, del) == 0 && p->have == have);
+      });
+    for (auto& th : ts) th.join();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    CHECK(builds.load() == 8 && locked_builds.load() == 0);
+    CHECK(ms < 200.0);  // serialised builds would take >= 400 ms
+    std::printf("ok   TestPlanCacheBuildsOutsideLock (8 x 50 ms builds in %.0f ms)\n", ms);
+  }
+  {  // one key, 8 concurrent callers: one build, one shared value
+    LruCache<Key, FakePlan> cache(4);
+    std::atomic<int> builds{0};
+    auto slow = [&](const Key& key, FakePlan** out) {
+      ++builds;
+      std::this_thread::sleep_for(std::chrono::milliseconds(30));
+      return build(key, out);
+    };
+    std::vector<int> have = {0, 1, 2, 3, 4, 5, 6, 8};
+    std::vector<std::shared_ptr<FakePlan>> got(8);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 8; ++t)
+      ts.emplace_back([&, t] { CHECK(cache.get(Key{0, 'R', 8, 0, have}, &got[t], slow, del) == 0); });
+    for (auto& th : ts) th.join();
+    CHECK(builds.load() == 1);
+    for (int t = 1; t < 8; ++t) CHECK(got[t] == got[0]);
+    // waiters on a failed build fail too (each retrying as the builder)
+    std::vector<int> dup = {0, 0, 2, 3, 4, 5, 6, 7};
+    std::atomic<int> fails{0};
+    ts.clear();
+    for (int t = 0; t < 4; ++t)
+      ts.emplace_back([&] {
+        std::shared_ptr<FakePlan> p;
+        if (cache.get(Key{0, 'R', 8, 0, dup}, &p, slow, del) == (int)Status::SingularNonzero && !p) ++fails;
+      });
+    for (auto& th : ts) th.join();
+    CHECK(fails.load() == 4 && cache.size() == 1);
+    std::printf("ok   TestPlanCacheSharedBuild (8 callers, 1 build; failed builds cache nothing)\n");
+  }
+  {  // eviction releases values after the lock is dropped
+    LruCache<Key, FakePlan> cache(2);
+    std::atomic<int> deleted{0}, locked{0};
+    auto checked_del = [&](FakePlan* p) {
+      if (cache.held_by_this_thread()) ++locked;
+      ++deleted;
+      delete p;
+    };
+    std::mt19937_64 rng(7);
+    std::set<std::vector<int>> seen;
+    while (seen.size() < 50) {
+      const std::vector<int> have = random_set(rng, 6, 12);
+      if (!seen.insert(have).second) continue;
+      std::shared_ptr<FakePlan> p;
+      CHECK(cache.get(Key{0, 'R', 6, 0, have}, &p, build, checked_del) == 0);
+    }
+    cache.set_capacity(1);
+    cache.clear();
+    CHECK(deleted.load() == 50 && locked.load() == 0 && g_tables.load() == 0);
+    std::printf("ok   TestPlanCacheReleaseOutsideLock (50 evictions, no deleter under the lock)\n");
+  }
+  std::printf("6/6 passed\n");
   return 0;
 }

@@ -42,11 +42,15 @@ CACHE_BIN = os.path.join(ROOT, "tests", "cpp", "plan_cache_test")
 def test_plan_cache_is_bounded_and_safe_under_eviction():
     """slime_amd/csrc/plan_cache.hpp over the product's host matrix code:
     10,000 distinct 20/40 survivor sets keep the live plan count at the cap
-    and release every evicted table; held plans survive concurrent eviction."""
+    and release every evicted table; held plans survive concurrent eviction;
+    builds run outside the cache lock (8 slow builds of different keys
+    overlap, one key's concurrent callers share one build) and evicted plans
+    are released after it is dropped."""
     subprocess.run(["make", "-C", ROOT, "tests/cpp/plan_cache_test"], check=True, capture_output=True)
     r = subprocess.run([CACHE_BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    for name in ("TestPlanCacheBounded", "TestPlanCacheFailedBuild", "TestPlanCacheConcurrent"):
+    for name in ("TestPlanCacheBounded", "TestPlanCacheFailedBuild", "TestPlanCacheConcurrent",
+                 "TestPlanCacheBuildsOutsideLock", "TestPlanCacheSharedBuild", "TestPlanCacheReleaseOutsideLock"):
         assert f"ok   {name}" in r.stdout
 
 
@@ -65,3 +69,18 @@ def test_copy_pool_under_concurrent_callers(threads):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
 
+
+
+POOL_BIN = os.path.join(ROOT, "tests", "cpp", "device_pool_test")
+
+
+def test_device_pool_routing_with_a_fixed_device_count():
+    """device_pool.hpp (the routing rs_capi.cpp uses) on 8 stand-in devices:
+    25 concurrent callers spread within 20% of an even share, every workspace
+    and plan a call gets is its device's, pinned devices (per call, per
+    thread, SLIME_RS_DEVICES) are honoured, and the least-loaded device wins."""
+    subprocess.run(["make", "-C", ROOT, "tests/cpp/device_pool_test"], check=True, capture_output=True)
+    r = subprocess.run([POOL_BIN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestAllowedDevices", "TestPoolSpreadsConcurrentCallers", "TestPinnedDevices", "TestLeastLoaded"):
+        assert f"ok   {name}" in r.stdout
