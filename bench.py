@@ -33,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 from slime_amd import batch  # noqa: E402
 from slime_amd import device as D  # noqa: E402
+from slime_amd.codeobj import kernel_code_id  # noqa: E402
 
 GIB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -97,7 +98,7 @@ def parse(argv=None):
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
-    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
+    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
                          "used only when its config and kernel source match this run)")
     args = ap.parse_args(argv)
@@ -557,16 +558,6 @@ def stream_ceilings(dev: int, stream, gib: int = 4, reps: int = 5) -> dict:
     return {"torch_copy_gbs": copy, "torch_fill_gbs": fill, "bytes": f"{gib} GiB per pass, median of {reps}"}
 
 
-def kernel_source_id() -> str:
-    """Hash of the apply kernel's sources: PMC traffic measured on one build
-    is only replayed into a bench line of the same kernel source."""
-    import hashlib
-    h = hashlib.sha256()
-    for f in ("rs_apply_kernel.hpp", "rs_apply.hip", "gfp.hpp"):
-        h.update(open(os.path.join(ROOT, "slime_amd", "csrc", f), "rb").read())
-    return h.hexdigest()[:16]
-
-
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -704,16 +695,16 @@ def main():
     # --pmc passes of their own).  It is replayed from the summary of such
     # passes only when they were taken on this config AND this kernel source,
     # and the line says where it came from.
-    traffic, traffic_source = None, "not measured for this kernel source/config"
-    src_id = kernel_source_id()
-    if os.path.exists(args.traffic):
+    traffic, traffic_source = None, "not measured for this kernel's machine code/config"
+    code_id = kernel_code_id(D.N.LIB_PATH, (f"{kname}ILi{need}E",))
+    if os.path.exists(args.traffic) and code_id:
         try:
             tj = json.load(open(args.traffic))
             if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}" and tj.get("kernel") == kname \
-                    and tj.get("kernel_source") == src_id:
+                    and tj.get("kernel_code") == code_id:
                 traffic = tj.get("hbm_bytes_per_launch")
                 traffic_source = (f"replayed: {os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE / "
-                                  f"WRITE_SIZE passes, session {tj.get('session', '?')}, kernel source {src_id})")
+                                  f"WRITE_SIZE passes, session {tj.get('session', '?')}, kernel code {code_id})")
         except (OSError, ValueError):
             traffic = None
     # Distinct devices across ranks (n_gpus), by PCI address.

@@ -128,8 +128,19 @@ struct BytesLaunch {
   const uint32_t* mapping;
   uint64_t col0 = 0;   // column window [col0, col0 + ncols) of every chunk; col0 % 4 == 0
   uint64_t ncols = 0;  // 0: the whole chunk (L columns)
+  // Mid-object mapping switch (encode_bytes_queue_kernel): device scratch of
+  // encode_switch_bytes(a) bytes, or null.  Phase 0 with scratch records each
+  // unit's mapping there and sets *switched when it ran the switching kernel;
+  // phase 1 given the same scratch (only if *switched) redoes just the units
+  // that used the wrong mapping.  Null: phase 1 re-encodes whole objects.
+  uint8_t* scratch = nullptr;
+  bool* switched = nullptr;
 };
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
+// Scratch bytes the mid-object switch needs for this launch; 0 when its
+// phase 0 would not run the switching (dynamic-schedule) kernel.
+uint64_t encode_switch_bytes(const BytesLaunch& a, hipStream_t stream);
+uint64_t encode_switch_bytes_k32(const BytesLaunch& a, hipStream_t stream);
 // 17 <= need <= 32 through the pipelined k-template byte kernels (rs_bytes_k32.hip).
 hipError_t launch_encode_bytes_k32(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_decode_bytes_k32(const BytesLaunch& a, hipStream_t stream);

@@ -462,6 +462,10 @@ struct TicketWalk {
     }
   }
   __device__ __forceinline__ uint32_t tile() const { return tb + 4 * i; }
+  // The current unit's index within its object (group * 4 + sub; see
+  // unit_tile_base) and whether the current tile is the unit's first.
+  __device__ __forceinline__ uint32_t unit() const { return (tb / (4 * C)) * 4 + tb % (4 * C); }
+  __device__ __forceinline__ bool unit_start() const { return i == 0; }
   // Step to the next tile (the next unit's first after the last of this one).
   __device__ __forceinline__ void advance() {
     if (++i >= cnt) next_unit();
@@ -478,6 +482,57 @@ struct TicketWalk {
         atomicExch(done, 0u);
       }
     }
+  }
+};
+
+// First tile of unit u (group u / 4, sub u % 4) of a C-tile-unit walk, and
+// the units of an object of `ntiles` tiles walked with `spread` segments
+// (TicketWalk's numbering: every (group, sub) pair, empty ones included).
+template <int C>
+__host__ __device__ __forceinline__ uint32_t unit_tile_base(uint32_t u) {
+  return (u / 4) * (4 * C) + u % 4;
+}
+template <int C>
+__host__ __device__ inline uint32_t walk_units(uint32_t ntiles, uint32_t spread) {
+  const uint32_t s = spread ? spread : 1;
+  const uint32_t groups = (ntiles + 4 * C - 1) / (4 * C);
+  return s * ((groups + s - 1) / s) * 4;
+}
+
+// A static walk over a device-built list of units (entries obj * units +
+// unit, `*count` of them): wave w takes entries w, w + nwaves, ...  Same
+// interface as TicketWalk, for kernels that redo a chosen subset of a
+// TicketWalk launch's units.
+template <int C>
+struct ListWalk {
+  const uint32_t* list;
+  uint32_t n, e, step, units, ntiles;
+  uint32_t obj = 0, tb = 0, cnt = 0, i = 0;
+  bool live = true;
+  __device__ __forceinline__ ListWalk(const uint32_t* list_, uint32_t n_, uint32_t first, uint32_t step_,
+                                      uint32_t units_, uint32_t ntiles_)
+      : list(list_), n(n_), e(first - step_), step(step_), units(units_), ntiles(ntiles_) {
+    next_unit();
+  }
+  __device__ __forceinline__ void next_unit() {
+    for (;;) {
+      e += step;
+      if (e >= n) {
+        live = false;
+        return;
+      }
+      const uint32_t v = list[e];
+      obj = v / units;
+      tb = unit_tile_base<C>(v % units);
+      i = 0;
+      cnt = tb < ntiles ? (ntiles - tb + 3) / 4 : 0;
+      if (cnt > C) cnt = C;
+      if (cnt) return;
+    }
+  }
+  __device__ __forceinline__ uint32_t tile() const { return tb + 4 * i; }
+  __device__ __forceinline__ void advance() {
+    if (++i >= cnt) next_unit();
   }
 };
 

@@ -2,8 +2,11 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 #include "rs_bytes_kernel.hpp"
+#include "rs_bytes_launch.hpp"
 
 namespace slime {
 namespace bytes {
@@ -69,25 +72,21 @@ constexpr int queue_tiles() {
   return U >= 3 ? 2 : 6 / U;
 }
 
+}  // namespace
+
+
+namespace {
+
 template <int K>
 hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
   constexpr int U = enc_pipe_unroll<K>();
+  constexpr int C = queue_tiles<U>();
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
-  const uint32_t spread = a.phase == 0 && queue_allowed(s) ? queue_spread(a.nobj, ncols, U, queue_tiles<U>()) : 0;
-  if (spread) {
-    bool launched = false;
-    const hipError_t e = with_tickets(
-        s,
-        [&](uint32_t* set) {
-          hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, queue_tiles<U>(), kQueueCounters>),
-                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
-                             ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, set, spread);
-          return hipGetLastError();
-        },
-        &launched);
-    if (launched || e != hipSuccess) return e;
-  }
+  if (a.phase == 1 && a.scratch) return bytes::launch_redo<K, U, C>(a, ncols, s);
   if (a.phase == 0) {
+    bool launched = false;
+    const hipError_t e = bytes::launch_encode_queue<K, U, C>(a, ncols, s, &launched);
+    if (launched || e != hipSuccess) return e;
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, U, 0>),
                        grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, pipe_blocks<K>(), U), dim3(kBlock), 0, s,
@@ -99,6 +98,13 @@ hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
                        a.out_idx, a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
+}
+
+template <int K>
+uint64_t enc_switch_bytes(const BytesLaunch& a, hipStream_t s) {
+  if (!pipe_ok(a)) return 0;
+  constexpr int U = enc_pipe_unroll<K>();
+  return bytes::switch_layout<K, U, queue_tiles<U>()>(a, a.ncols ? a.ncols : a.L, s).bytes;
 }
 
 template <int K>
@@ -261,6 +267,29 @@ hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
   }
 
 }  // namespace
+
+uint64_t encode_switch_bytes(const BytesLaunch& a, hipStream_t s) {
+  if (a.nobj == 0 || a.L == 0 || a.phase != 0) return 0;
+  switch (a.k) {
+    case 1: return enc_switch_bytes<1>(a, s);
+    case 2: return enc_switch_bytes<2>(a, s);
+    case 3: return enc_switch_bytes<3>(a, s);
+    case 4: return enc_switch_bytes<4>(a, s);
+    case 5: return enc_switch_bytes<5>(a, s);
+    case 6: return enc_switch_bytes<6>(a, s);
+    case 7: return enc_switch_bytes<7>(a, s);
+    case 8: return enc_switch_bytes<8>(a, s);
+    case 9: return enc_switch_bytes<9>(a, s);
+    case 10: return enc_switch_bytes<10>(a, s);
+    case 11: return enc_switch_bytes<11>(a, s);
+    case 12: return enc_switch_bytes<12>(a, s);
+    case 13: return enc_switch_bytes<13>(a, s);
+    case 14: return enc_switch_bytes<14>(a, s);
+    case 15: return enc_switch_bytes<15>(a, s);
+    case 16: return enc_switch_bytes<16>(a, s);
+    default: return a.k <= 32 && pipe_ok(a) && k32_kernels() ? encode_switch_bytes_k32(a, s) : 0;
+  }
+}
 
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread

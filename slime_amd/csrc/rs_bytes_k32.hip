@@ -8,6 +8,7 @@
 
 #include "kernels.hpp"
 #include "rs_bytes_kernel.hpp"
+#include "rs_bytes_launch.hpp"
 
 namespace slime {
 namespace {
@@ -26,18 +27,10 @@ template <int K>
 hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   if constexpr (K <= kQueueEncodeMaxK) {
-    const uint32_t spread = a.phase == 0 && queue_allowed(s) ? queue_spread(a.nobj, ncols, 1, kQueueTiles) : 0;
-    if (spread) {
+    if (a.phase == 1 && a.scratch) return bytes::launch_redo<K, 1, kQueueTiles>(a, ncols, s);
+    if (a.phase == 0) {
       bool launched = false;
-      const hipError_t e = with_tickets(
-          s,
-          [&](uint32_t* set) {
-            hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>),
-                               dim3((uint32_t)kBlocks), dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
-                               ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, set, spread);
-            return hipGetLastError();
-          },
-          &launched);
+      const hipError_t e = bytes::launch_encode_queue<K, 1, kQueueTiles>(a, ncols, s, &launched);
       if (launched || e != hipSuccess) return e;
     }
   }
@@ -53,6 +46,13 @@ hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
                        a.coeff, a.out_idx, a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
+}
+
+template <int K>
+uint64_t enc_switch_bytes(const BytesLaunch& a, hipStream_t s) {
+  if constexpr (K <= kQueueEncodeMaxK)
+    return bytes::switch_layout<K, 1, kQueueTiles>(a, a.ncols ? a.ncols : a.L, s).bytes;
+  return 0;
 }
 
 template <int K>
@@ -104,6 +104,7 @@ hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_encode_bytes_k32(const BytesLaunch& a, hipStream_t s) { SLIME_K32_SWITCH(enc_k32) }
+uint64_t encode_switch_bytes_k32(const BytesLaunch& a, hipStream_t s) { SLIME_K32_SWITCH(enc_switch_bytes) }
 hipError_t launch_decode_bytes_k32(const BytesLaunch& a, hipStream_t s) { SLIME_K32_SWITCH(dec_k32) }
 
 }  // namespace slime

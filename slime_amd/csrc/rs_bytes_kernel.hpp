@@ -637,17 +637,40 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
   }
 }
 
-// MODE 0 (speculative, mapping 0) encode on the ticket walk: the interior
-// tiles (encode_bytes_pipe_kernel's pipelined prefix, the same count for
-// every object) are dealt as units; MapToGF's flags are OR-ed into
-// flags[obj] whenever a wave's tiles move to another object.  The few edge
-// tiles and column tails of every object follow, spread over all waves.
-// (Phase 1 re-encodes a handful of objects and keeps the static kernel.)
+// Interior tiles of an encode window (encode_bytes_pipe_kernel's pipelined
+// prefix, the same count for every object): tiles t with (t+1)*64U <= nvec
+// whose highest word (last data chunk, last unit) is below the object's last
+// word.  Host and device compute it alike (the redo list needs the count).
+__host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L, uint64_t col0, uint64_t ncols, int K,
+                                                          int U) {
+  const uint64_t nw = (S + 3) / 4;
+  const uint64_t first_tail_word = nw ? nw - 1 : 0;
+  const uint64_t lim = (uint64_t)(K - 1) * L + col0;
+  uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+  const uint64_t nvec = ncols >> 2;
+  if (end_max > nvec) end_max = nvec;
+  return (uint32_t)(end_max / (64 * (uint64_t)U));
+}
+
+// MODE 0 (speculative) encode on the ticket walk: the interior tiles are
+// dealt as units; the few edge tiles and column tails of every object follow,
+// spread over all waves (mapping 0).  MapToGF's flags (map.go:35-62) are OR-ed
+// into flags[obj] as soon as a tile shows a new bit.
+//
+// Mid-object switch (record != nullptr): a wave entering a unit reads its
+// object's flags; once some word >= p has been seen, the object cannot keep
+// mapping 0, so the unit is encoded with 1<<31 straight away, and
+// record[obj * units + unit] says which mapping it used.  Phase 1
+// (encode_bytes_redo_kernel) then redoes only the units whose mapping differs
+// from the one the object ends with -- the units encoded before the first
+// word >= p was seen -- instead of the whole object.  A stale flag read only
+// delays the switch: the record always tells what the unit wrote.
 template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
-    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread) {
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
+    uint32_t units) {
   const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
@@ -656,11 +679,8 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
   const uint32_t nvec = (uint32_t)(ncols >> 2);
   const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
-  // Interior tiles t < nint: (t+1)*64U <= nvec and (K-1)L + col0 + 4*end < first_tail_word.
-  const uint64_t lim = (uint64_t)(K - 1) * L + col0;
-  uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
-  if (end_max > nvec) end_max = nvec;
-  const uint32_t nint = (uint32_t)(end_max / (64 * U));
+  const uint32_t nint = encode_interior_tiles(S, L, col0, ncols, K, U);
+  const bool sw = record != nullptr;
   auto window = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
   auto load = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
     const uint8_t* cb[K];
@@ -668,49 +688,73 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     for (int j = 0; j < K; ++j) cb[j] = window(o) + (uint64_t)j * chunk;
     load_raw_tile<K, U>(r, cb, t * (64 * U) + lane, nvec);
   };
-  Flags fl;
-  uint32_t fobj = 0xFFFFFFFFu;  // the object fl belongs to
-  auto flush = [&] {
-    const uint32_t f = fl.bits();
-    const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
-    const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
-    if (wf && lane == 0) atomicOr(&flags[fobj], wf);
-    fl = Flags();
+  // The mapping a unit of object o starts with: 1<<31 once bit 0 is set.
+  // Every lane loads the word (one request); the value stays in a VGPR and
+  // is waited for only when the unit's first tile is computed.
+  auto unit_mapping = [&](uint32_t o) -> uint32_t {
+    const uint32_t f = __hip_atomic_load(flags + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (f & 1u) ? 0x80000000u : 0u;
   };
-  auto compute = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
-    if (o != fobj) {
-      if (fobj != 0xFFFFFFFFu) flush();
-      fobj = o;
+  Flags fl;
+  uint32_t fobj = 0xFFFFFFFFu, sent = 0;  // the object fl belongs to, bits already OR-ed into flags[fobj]
+  auto publish = [&] {  // OR the wave's new flag bits into flags[fobj] (wave-uniform)
+    const uint32_t f = fl.bits();
+    const uint32_t wf = (__ballot(f & 1u) ? 1u : 0u) | (__ballot(f & 2u) ? 2u : 0u);
+    if (wf & ~sent) {
+      if (lane == 0) atomicOr(&flags[fobj], wf);
+      sent |= wf;
     }
-    encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, 0u, rows, coeff, out_idx,
+  };
+  auto compute = [&](uint4(&r)[U][K], uint32_t o, uint32_t t, uint32_t m, bool first, uint32_t unit) {
+    if (o != fobj) {
+      fl = Flags();
+      fobj = o;
+      sent = 0;
+    }
+    if (sw && first && lane == 0) record[(uint64_t)o * units + unit] = m ? 1 : 0;
+    encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, m, rows, coeff, out_idx,
                                      t * (64 * U) + lane, nvec, fl);
+    publish();
   };
   {
     apply::TicketWalk<C, NC> w(ticket, nobj, nint, lane, spread);
     if (w.live) {
       uint4 ra[U][K], rb[U][K];
+      uint32_t ma = sw ? unit_mapping(w.obj) : 0u, mb = 0;
+      uint32_t ua = w.unit(), ub = 0;
+      bool fa = true, fb = false;
       load(ra, w.obj, w.tile());
       for (;;) {
         uint32_t co = w.obj, ct = w.tile();
         w.advance();
+        fb = w.live && w.unit_start();
+        mb = sw && fb ? unit_mapping(w.obj) : ma;
+        ub = w.unit();
         load(rb, w.live ? w.obj : co, w.live ? w.tile() : ct);
-        compute(ra, co, ct);
+        compute(ra, co, ct, ma, fa, ua);
         if (!w.live) break;
         co = w.obj;
         ct = w.tile();
         w.advance();
+        fa = w.live && w.unit_start();
+        ma = sw && fa ? unit_mapping(w.obj) : mb;
+        ua = w.unit();
         load(ra, w.live ? w.obj : co, w.live ? w.tile() : ct);
-        compute(rb, co, ct);
+        compute(rb, co, ct, mb, fb, ub);
         if (!w.live) break;
       }
     }
     w.finish();
   }
-  if (fobj != 0xFFFFFFFFu) flush();
   // Edge tiles [nint, ntiles) of every object (encode_bytes_kernel's edge step).
   const uint32_t nedge = ntiles - nint;
   for (uint64_t e = wave; e < (uint64_t)nobj * nedge; e += nwaves) {
     const uint32_t o = (uint32_t)(e / nedge);
+    if (o != fobj) {
+      fl = Flags();
+      fobj = o;
+      sent = 0;
+    }
     uint8_t* const slot = window(o);
     const uint64_t g0 = (uint64_t)(nint + (uint32_t)(e % nedge)) * (64 * U) + lane;
     uint32_t x[U][K][4];
@@ -728,8 +772,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
       if ((uint64_t)(K - 1) * L + col0 + b + 4 > first_tail_word) fix_data_tail<K>(slot, chunk, L, col0, b, 4, ow, 0u, x[u]);
     }
     rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, g0, 0u);
-    fobj = o;
-    flush();
+    publish();
   }
   // Columns past the last whole vector of each object, one per lane.
   const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
@@ -745,6 +788,125 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     rows_out<K>(x, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, 4 * b, 0u, 1);
     const uint32_t f = f1.bits();
     if (f) atomicOr(&flags[o], f);  // per lane: tails are a handful of columns per object
+  }
+}
+
+// The redo list of a switched phase 0: every interior unit of an object whose
+// mapping came out 1<<31 (status 0) that phase 0 encoded with mapping 0,
+// as entries obj * units + unit, appended in any order; *count (zero on
+// entry) receives their number.
+template <int C>
+__global__ __launch_bounds__(kBlock) void redo_list_kernel(const uint8_t* __restrict__ record,
+                                                           const uint32_t* __restrict__ mapping,
+                                                           const uint32_t* __restrict__ status, uint32_t nobj,
+                                                           uint32_t units, uint32_t nint, uint32_t* __restrict__ list,
+                                                           uint32_t* __restrict__ count) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t total = (uint64_t)nobj * units;
+  for (uint64_t base = wave * 64; base < total; base += nwaves * 64) {
+    const uint64_t e = base + lane;
+    bool need = false;
+    if (e < total) {
+      const uint32_t o = (uint32_t)(e / units), u = (uint32_t)(e % units);
+      need = mapping[o] != 0 && status[o] == 0 && apply::unit_tile_base<C>(u) < nint && record[e] == 0;
+    }
+    const uint64_t mask = __ballot(need);
+    if (!mask) continue;
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
+    at = __builtin_amdgcn_readfirstlane(at);
+    if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
+  }
+}
+
+// Phase 1 after a switched phase 0: re-encode with the object's mapping the
+// listed interior units (redo_list_kernel), then every edge tile and column
+// tail of the objects mapped with 1<<31 (phase 0 wrote those with mapping 0).
+// The interior walk is the queue kernel's pipeline over a static share of the
+// list.
+template <int K, int U, int C>
+__global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    const uint32_t* __restrict__ status, const uint32_t* __restrict__ mapping, const uint32_t* __restrict__ list,
+    const uint32_t* __restrict__ count, uint32_t units) {
+  const uint64_t chunk = 4 * L;
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint32_t nvec = (uint32_t)(ncols >> 2);
+  const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  const uint32_t nint = encode_interior_tiles(S, L, col0, ncols, K, U);
+  auto window = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
+  auto load = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
+    const uint8_t* cb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) cb[j] = window(o) + (uint64_t)j * chunk;
+    load_raw_tile<K, U>(r, cb, t * (64 * U) + lane, nvec);
+  };
+  Flags unused;
+  auto compute = [&](uint4(&r)[U][K], uint32_t o, uint32_t t) {
+    encode_interior_tile<K, U, false>(r, window(o) + (uint64_t)K * chunk, chunk, mapping[o], rows, coeff, out_idx,
+                                      t * (64 * U) + lane, nvec, unused);
+  };
+  apply::ListWalk<C> w(list, *count, wave, nwaves, units, nint);
+  if (w.live) {
+    uint4 ra[U][K], rb[U][K];
+    load(ra, w.obj, w.tile());
+    for (;;) {
+      uint32_t co = w.obj, ct = w.tile();
+      w.advance();
+      load(rb, w.live ? w.obj : co, w.live ? w.tile() : ct);
+      compute(ra, co, ct);
+      if (!w.live) break;
+      co = w.obj;
+      ct = w.tile();
+      w.advance();
+      load(ra, w.live ? w.obj : co, w.live ? w.tile() : ct);
+      compute(rb, co, ct);
+      if (!w.live) break;
+    }
+  }
+  // Edge tiles and column tails of the objects mapped with 1<<31.
+  const uint32_t nedge = ntiles - nint;
+  for (uint64_t e = wave; e < (uint64_t)nobj * nedge; e += nwaves) {
+    const uint32_t o = (uint32_t)(e / nedge);
+    const uint32_t m = mapping[o];
+    if (m == 0 || status[o] != 0) continue;  // wave-uniform
+    uint8_t* const slot = window(o);
+    const uint64_t g0 = (uint64_t)(nint + (uint32_t)(e % nedge)) * (64 * U) + lane;
+    uint32_t x[U][K][4];
+    int n = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (g0 + 64 * u < nvec) {
+        load_data_symbols<K, false, false>(slot, chunk, L, col0, (g0 + 64 * u) << 2, 4, ow, m, x[u], nullptr);
+        n = u + 1;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u >= n) break;
+      const uint64_t b = (g0 + 64 * u) << 2;
+      if ((uint64_t)(K - 1) * L + col0 + b + 4 > first_tail_word) fix_data_tail<K>(slot, chunk, L, col0, b, 4, ow, m, x[u]);
+    }
+    rows_out_units<K, U>(x, n, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, g0, m);
+  }
+  const uint32_t tailc = (uint32_t)(ncols - ((uint64_t)nvec << 2));
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x, nthr = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t t = tid; tailc && t < (uint64_t)nobj * tailc; t += nthr) {
+    const uint32_t o = (uint32_t)(t / tailc);
+    const uint32_t m = mapping[o];
+    if (m == 0 || status[o] != 0) continue;
+    uint8_t* const slot = window(o);
+    const uint64_t b = ((uint64_t)nvec << 2) + t % tailc;
+    uint32_t x[K][4];
+    load_data_symbols<K, false, false>(slot, chunk, L, col0, b, 1, ow, m, x, nullptr);
+    fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
+    rows_out<K>(x, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, 4 * b, m, 1);
   }
 }
 

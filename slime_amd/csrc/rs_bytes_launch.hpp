@@ -1,0 +1,81 @@
+// Host launch templates of the fused byte encode's mid-object mapping switch
+// (kernels: rs_bytes_kernel.hpp encode_bytes_queue_kernel, redo_list_kernel,
+// encode_bytes_redo_kernel), shared by rs_bytes.hip (need <= 16) and
+// rs_bytes_k32.hip (17 <= need <= 24).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernels.hpp"
+#include "rs_bytes_kernel.hpp"
+
+namespace slime {
+// Mid-object switch scratch (BytesLaunch::scratch): the redo count, the redo
+// list (nobj x units words) and the per-unit mapping record (nobj x units
+// bytes) of a phase 0 on the ticket walk with C-tile units of U vectors.
+namespace bytes {
+struct SwitchLayout {
+  uint32_t spread = 0, nint = 0, units = 0;
+  uint64_t bytes = 0;
+  uint32_t* count(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p); }
+  uint32_t* list(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p + 256); }
+  uint8_t* record(uint8_t* p, uint32_t nobj) const { return p + 256 + 4ull * nobj * units; }
+};
+template <int K, int U, int C>
+SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
+  SwitchLayout l;
+  if (!queue_allowed(s)) return l;
+  l.spread = queue_spread(a.nobj, ncols, U, C);
+  if (!l.spread) return l;
+  l.nint = encode_interior_tiles(a.S, a.L, a.col0, ncols, K, U);
+  l.units = apply::walk_units<C>(l.nint, l.spread);
+  l.bytes = 256 + 5ull * a.nobj * l.units;
+  return l;
+}
+
+// Phase 1 after a switched phase 0: build the redo list, then re-encode the
+// listed units plus the edge tiles and column tails of the objects mapped
+// with 1<<31.
+template <int K, int U, int C>
+hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
+  const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
+  if (!l.spread) return hipErrorInvalidValue;  // phase 0 cannot have switched
+  uint32_t* count = l.count(a.scratch);
+  if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
+  const uint64_t entries = (uint64_t)a.nobj * l.units;
+  const uint64_t lblocks = std::min<uint64_t>(1024, (entries + apply::kBlock - 1) / apply::kBlock);
+  hipLaunchKernelGGL(redo_list_kernel<C>, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(apply::kBlock), 0, s,
+                     l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
+                     count);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(256), dim3(apply::kBlock), 0, s, a.slots,
+                     a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping,
+                     l.list(a.scratch), count, l.units);
+  return hipGetLastError();
+}
+
+// Phase 0 on the ticket walk (the mid-object switch when a.scratch is given).
+// *launched = false when the batch has too many units for 32-bit tickets or
+// no counter set could be had (the caller takes the static kernel).
+template <int K, int U, int C>
+hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t s, bool* launched) {
+  *launched = false;
+  const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
+  if (!l.spread) return hipSuccess;
+  uint8_t* record = a.scratch ? l.record(a.scratch, a.nobj) : nullptr;
+  const hipError_t e = with_tickets(
+      s,
+      [&](uint32_t* set) {
+        hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(256), dim3(apply::kBlock), 0, s,
+                           a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
+                           a.flags, set, l.spread, record, l.units);
+        return hipGetLastError();
+      },
+      launched);
+  if (*launched && record && a.switched) *a.switched = true;
+  return e;
+}
+}  // namespace bytes
+
+}  // namespace slime

@@ -967,6 +967,88 @@ static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint6
   return a;
 }
 
+// Device scratch for asynchronous launch sequences (the encode's
+// mid-object-switch record and redo list): per device, buffers handed to one
+// sequence at a time and returned behind an event recorded after its last
+// launch, so a buffer is reused only once that sequence has finished --
+// whatever stream ran it.  Inside a graph capture no buffer is handed out
+// (the caller runs without scratch).
+namespace {
+struct ScratchBuf {
+  uint8_t* p = nullptr;
+  uint64_t bytes = 0;
+  hipEvent_t ev = nullptr;
+};
+struct ScratchPool {
+  std::mutex mu;
+  std::vector<ScratchBuf> bufs;  // free when ev has completed
+};
+ScratchPool& scratch_pool(int dev) {
+  static std::mutex mu;
+  static auto* pools = new std::map<int, ScratchPool>();  // never destroyed (see plans())
+  std::lock_guard<std::mutex> lock(mu);
+  return (*pools)[dev];
+}
+bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;
+  }
+  return st != hipStreamCaptureStatusNone;
+}
+struct ScratchLease {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  ScratchBuf buf;
+  bool held = false;
+  // A free buffer of >= bytes on `dev` (current device), or none (ok = false,
+  // no error) inside a capture.
+  int take(int device, uint64_t bytes, hipStream_t s) {
+    dev = device;
+    stream = s;
+    if (bytes == 0 || stream_capturing(s)) return 0;
+    ScratchPool& sp = scratch_pool(dev);
+    std::lock_guard<std::mutex> lock(sp.mu);
+    for (size_t i = 0; i < sp.bufs.size(); ++i) {
+      if (sp.bufs[i].bytes < bytes) continue;
+      const hipError_t q = hipEventQuery(sp.bufs[i].ev);
+      if (q == hipErrorNotReady) continue;
+      if (q != hipSuccess) (void)hipGetLastError();
+      buf = sp.bufs[i];
+      sp.bufs.erase(sp.bufs.begin() + (long)i);
+      held = true;
+      return 0;
+    }
+    const uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 1u << 20);
+    HIP_TRY(hipMalloc((void**)&buf.p, want));
+    buf.bytes = want;
+    if (hipError_t e = hipEventCreateWithFlags(&buf.ev, hipEventDisableTiming)) {
+      (void)hipFree(buf.p);
+      return fail_hip(e, "scratch event");
+    }
+    held = true;
+    return 0;
+  }
+  uint8_t* ptr() const { return held ? buf.p : nullptr; }
+  // Back to the pool behind an event on `s` (after the sequence's last launch).
+  void release(hipStream_t s) {
+    if (!held) return;
+    held = false;
+    if (hipEventRecord(buf.ev, s) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(s);  // cannot observe the release: wait for it here
+    }
+    ScratchPool& sp = scratch_pool(dev);
+    std::lock_guard<std::mutex> lock(sp.mu);
+    sp.bufs.push_back(buf);
+  }
+  ~ScratchLease() {
+    if (held) release(stream);  // error paths: behind whatever the sequence queued
+  }
+};
+}  // namespace
+
 extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
                                        uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
                                        void* stream) {
@@ -981,9 +1063,21 @@ extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uin
   HIP_TRY(hipMemsetAsync(status, 0, nobj * sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(mapping, 0, nobj * sizeof(uint32_t), s));
   if (L == 0) return 0;
-  HIP_TRY(launch_encode_bytes(bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 0, status, mapping), s));
+  // Phase 0 with the mid-object mapping switch where the dynamic schedule
+  // runs (a scratch record of each unit's mapping), so phase 1 redoes only
+  // the units encoded before an object's first word >= p was seen.
+  BytesLaunch a0 = bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 0, status, mapping);
+  ScratchLease sc;
+  if (int rc = sc.take(plan->device, encode_switch_bytes(a0, s), s)) return rc;
+  bool switched = false;
+  a0.scratch = sc.ptr();
+  a0.switched = &switched;
+  HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
-  HIP_TRY(launch_encode_bytes(bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 1, status, mapping), s));
+  BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 1, status, mapping);
+  if (switched) a1.scratch = sc.ptr();
+  HIP_TRY(launch_encode_bytes(a1, s));
+  sc.release(s);
   return 0;
 }
 

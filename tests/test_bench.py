@@ -87,13 +87,19 @@ def test_shape_labels_name_baseline_configs():
     assert bench.shape_label(3, 5, 7) == ""
 
 
-def test_committed_traffic_matches_shipped_kernel_source():
-    bench = _load("bench.py", "bench_mod2")
-    tool = _load("tools/pmc_traffic.py", "pmc_traffic")
-    assert bench.kernel_source_id() == tool.kernel_source_id()
-    tj = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")))
-    assert tj["kernel_source"] == bench.kernel_source_id(), \
-        "apply kernel changed since its PMC passes: re-run tools/gpu_r02.sh pmc_fetch pmc_write"
+def test_committed_traffic_matches_shipped_kernel_code():
+    """The PMC summary bench.py replays was measured on the machine code the
+    built library runs (slime_amd/codeobj.py hashes the kernel's gfx950
+    instructions), and its traffic is the algorithmic bytes."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from slime_amd.codeobj import kernel_code_id
+    tj = json.load(open(os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")))
     assert tj["config"] == "8/12 L=8388608 nobj=128" and tj["kernel"] == "rs_apply_queue_kernel"
+    lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
+    code = kernel_code_id(lib, ("rs_apply_queue_kernelILi8E",))
+    assert code is not None
+    assert tj["kernel_code"] == code, \
+        "apply kernel's machine code changed since its PMC passes: re-run tools/gpu_r03.sh pmc_fetch pmc_write"
     alg = 128 * 4 * 8388608 * 12
     assert abs(tj["hbm_bytes_per_launch"] / alg - 1) < 0.01  # no wasted re-reads

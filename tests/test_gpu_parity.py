@@ -566,6 +566,67 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total
         assert ms[1] == 1 << 31
 
 
+@pytest.mark.parametrize("need,total,S,nobj", [(8, 12, 16 << 20, 12), (10, 14, (8 << 20) + 5, 12),
+                                               (4, 6, (6 << 20) + 3, 18), (20, 24, (4 << 20) + 1, 6),
+                                               (3, 5, 1 << 20, 36), (16, 20, (5 << 20) + 2, 6)])
+def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
+    """The dynamic-schedule encode switches an object to 1<<31 as soon as a
+    word >= p has been seen and the second pass redoes only the units encoded
+    before that (rs_bytes_kernel.hpp).  Objects with that word at the start,
+    a quarter, half, 90 % and the last whole word, two such words, none, and
+    one that needs the random fallback (a word >= p after a word 1<<31 cannot
+    map); every chunk byte against the reference framing (map.go:15-67,
+    multi_store.go:526-554)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert N.lib.slime_rs_kernel_pipeline(-1) == 1 and N.lib.slime_rs_kernel_schedule(-1) == 1
+    rng = np.random.default_rng(S + nobj)
+    nfull = S // 4  # whole words
+    kinds = [None, 0.0, 0.25, 0.5, 0.9, "last", (0.3, 0.8), "fallback"]
+    objs = []
+    for o in range(nobj):
+        b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+        w = np.frombuffer(b, dtype=">u4", count=nfull).copy()
+        w[(w >= 0x7FFFFFFB) & (w < 0x80000000)] ^= 0x00100000  # no accidental fallback
+        w[w >= 4294967291] = 0x01020304  # no accidental 1<<31 either
+        b[:4 * nfull] = w.astype(">u4").tobytes()
+        k = kinds[o % len(kinds)]
+        at = []
+        if k == "last":
+            at = [nfull - 1]
+        elif k == "fallback":
+            at = [int(0.6 * (nfull - 1))]
+            b[4 * int(0.1 * nfull): 4 * int(0.1 * nfull) + 4] = b"\x7f\xff\xff\xfd"
+        elif isinstance(k, tuple):
+            at = [int(f * (nfull - 1)) for f in k]
+        elif k is not None:
+            at = [int(k * (nfull - 1))]
+        for a in at:
+            b[4 * a: 4 * a + 4] = b"\xff\xff\xff\xfd"
+        objs.append(bytes(b))
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total, extra=64)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, nobj, mapping, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().tolist()
+    assert st == [1 if kinds[o % len(kinds)] == "fallback" else 0 for o in range(nobj)]
+    if any(st):
+        assert D.resolve_fallbacks(plan, slots, stride, S, nobj, mapping, status) == sum(st)
+    ms = mapping.cpu().numpy().view(np.uint32)
+    h = slots.cpu().numpy()
+    for o, obj in enumerate(objs):
+        k = kinds[o % len(kinds)]
+        cands = [int(ms[o])] if k == "fallback" else []
+        m, chunks = _oracle_chunks(obj, need, total, cands)
+        assert ms[o] == m and (k is None) == (m == 0), (o, k)
+        for c in range(total):
+            got = h[o * stride + c * chunk: o * stride + (c + 1) * chunk].tobytes()
+            assert got == chunks[c], (o, k, c)
+        assert (h[o * stride + total * chunk: (o + 1) * stride] == 0xA5).all(), "wrote past the chunks"
+
+
 def test_encode_objects_random_fallback(torch_dev):
     torch = torch_dev
     from slime_amd import device as D

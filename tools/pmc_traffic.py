@@ -8,9 +8,11 @@ so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r03/pmc_traffic.json
     python tools/pmc_traffic.py --all <fetch_dir> <write_dir>    # every kernel: HBM bytes per dispatch
 
-`kernel_source` (hash of the apply kernel sources, as bench.py's
-kernel_source_id) ties the summary to the build it was measured on: bench.py
-replays `hbm_bytes_per_launch` only into lines of the same kernel source.
+`kernel_code` (slime_amd/codeobj.py: a hash of the measured kernel's gfx950
+machine code in the built library) ties the summary to the build it was
+measured on: bench.py replays `hbm_bytes_per_launch` only into lines whose
+build runs the same machine code.  Run it against the library that ran the
+passes (the tree the GPU session was sent).
 """
 import csv
 import glob
@@ -66,6 +68,12 @@ def all_kernels(fetch_dir, write_dir):
     print(json.dumps(out, indent=1))
 
 
+def kernel_code(kernel: str, need: int) -> str | None:
+    sys.path.insert(0, ROOT)
+    from slime_amd.codeobj import kernel_code_id
+    return kernel_code_id(os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so"), (f"{kernel}ILi{need}E",))
+
+
 def main():
     if sys.argv[1] == "--all":
         return all_kernels(sys.argv[2], sys.argv[3])
@@ -82,6 +90,7 @@ def main():
         "config": config,
         "session": session,
         "kernel_source": kernel_source_id(),
+        "kernel_code": kernel_code(next(iter(fk | wk)), int(config.split("/")[0])),
         "kernel": (fk | wk).pop(),
         "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
         "fetch_size_kib_avg": fetch_kib,
