@@ -265,13 +265,15 @@ ALLOCATOR_NOTE = {"vmm": "slime_rs_device_alloc: HIP virtual memory, physical ch
 
 def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int) -> dict:
     """writeChunks / reconstruct on device from object bytes (rs_bytes.hip): one
-    speculative encode pass that also picks gf.MapToGF's mapping, a re-encode
-    pass for objects mapped with 1<<31, and an in-place repair of the erased
-    chunks from chunk bytes.  Objects that would need MapToGF's random
+    speculative encode pass that also picks gf.MapToGF's mapping (switching an
+    object to 1<<31 once one of its words >= p has been seen), a redo pass over
+    the units encoded before that, and an in-place repair of the erased chunks
+    from chunk bytes.  Objects that would need MapToGF's random
     fallback are re-drawn before timing and counted."""
     S = args.object_mib << 20
     L, chunk, slot = D.slot_geometry(S, need, total)
     slots = batch_empty(args, nobj * slot, torch.uint8, dev)
+    placement = D.placement(slots) if args.allocator == "vmm" else None
     words = slots.view(torch.int32)
     D.fill_symbols(words, 0xB17E5 + 7919 * rank)
     enc = D.Plan.encode(need, total, dev)
@@ -320,15 +322,56 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     elapsed, = batch.max_over_ranks([elapsed])
     del slots, words, truth
     torch.cuda.empty_cache()
+    # Roofline of each leg (SURVEY.md §8(d) algorithmic bytes: encode 4L(k+r),
+    # decode 4L(k+e) per object) over its kernel time, and the PMC traffic of
+    # the same kernels' machine code when a committed summary has it.
+    alg_enc = nobj * 4 * L * total
+    alg_dec = nobj * 4 * L * (need + len(erase))
+    kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
+    replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj}", need)
+
+    def leg(what, alg, ms):
+        ach = alg / (ms * 1e-3) / 1e9
+        t = replay.get(what)
+        return {"kernels": [f"{k}<{need},...>" for k in kernels[what]], "alg_bytes": alg,
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": t, "traffic_over_alg": round(t / alg, 4) if t else None}
     return {"value": round(2 * nobj * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
             "encode_gibs": round(nobj * S / GIB / (enc_ms * 1e-3), 2),
             "decode_gibs": round(nobj * S / GIB / (dec_ms * 1e-3), 2),
             "kernel_ms": {"encode_both_passes": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+            "roofline": {"encode": leg("encode", alg_enc, enc_ms), "decode": leg("decode", alg_dec, dec_ms),
+                         "traffic_source": replay.get("source")},
             "mappings": {"0": int((ms == 0).sum()), "1<<31": int((ms == 0x80000000).sum()),
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
-            "fallback_redraws": redraws, "verified": ok,
-            "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative mapping-0 pass + "
-                    "1<<31 re-encode pass) and repair of erased chunks from chunk bytes"}
+            "fallback_redraws": redraws, "verified": ok, "placement": placement,
+            "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
+                    "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
+                    "erased chunks from chunk bytes"}
+
+
+def _bytes_traffic(args, config: str, need: int) -> dict:
+    """PMC bytes per step of the byte path's kernels at `config`, replayed from
+    profiles/r03/pmc_bytes.json only where every kernel's machine code matches
+    this build (slime_amd/codeobj.py); {} otherwise."""
+    path = os.path.join(ROOT, "profiles", "r03", "pmc_bytes.json")
+    try:
+        entries = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    e = next((x for x in entries if x.get("config") == config), None)
+    if not e:
+        return {}
+    ks = e.get("kernels", {})
+    out = {}
+    for what, names in (("encode", ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"]),
+                        ("decode", ["decode_bytes_queue_kernel"])):
+        if not all(n in ks and ks[n].get("kernel_code") == kernel_code_id(D.N.LIB_PATH, (f"{n}ILi{need}E",))
+                   for n in names):
+            return {}
+        out[what] = sum(ks[n]["hbm_bytes"] for n in names)
+    out["source"] = f"replayed: profiles/r03/pmc_bytes.json (session {e.get('session', '?')}, matching machine code)"
+    return out
 
 
 def host_leg(need, total, erase, obj_mib=64, reps=5):
@@ -617,6 +660,9 @@ def main():
     lay = D.layout_of(total, L, SS)
 
     buf = batch_empty(args, nobj * total * SS, torch.int32, dev)
+    # How the library placed the batch buffer: probed placements and retries
+    # (slime_rs_device_alloc, DESIGN.md "Placement").
+    placement = D.placement(buf) if args.allocator == "vmm" else None
     # Data shards: deterministic symbols, distinct per rank (synthetic objects).
     D.fill_symbols(buf, 0x5113E + 7919 * rank)
     enc = D.Plan.encode(need, total, dev)
@@ -781,6 +827,7 @@ def main():
                 "symbols_per_shard": L, "shard_stride_symbols": SS, "erased": erase, "decode_dst": args.decode_dst,
                 "parallelism": f"object-partition x{world} (no RCCL)",
                 "allocator": ALLOCATOR_NOTE[args.allocator],
+                "placement": placement,
             },
             "encode_gibs": round(obj_bytes / GIB / (enc_ms * 1e-3), 2),
             "decode_gibs": round(obj_bytes / GIB / (dec_ms * 1e-3), 2),

@@ -285,6 +285,22 @@ int slime_gf_unpack_device(int device, const uint32_t *words, uint64_t count, ui
  * Returns 0, SLIME_RS_ERR_INVALID_ARG, SLIME_RS_ERR_NO_DEVICE or
  * SLIME_RS_ERR_HIP (out of memory). */
 int slime_rs_device_alloc(int device, uint64_t bytes, void **ptr);
+/* How a slime_rs_device_alloc buffer was placed.  Buffers of at least
+ * SLIME_RS_PLACEMENT_PROBE_GIB GiB (default 16; 0 disables) are probed when
+ * created: the apply kernel's C3-shaped read/write walk over the whole buffer
+ * (GB/s of algorithmic traffic).  Below SLIME_RS_PLACEMENT_MIN_GBS (default
+ * 6100) the allocator tries up to two other placements (1 GiB chunks, then
+ * one hipMalloc), holding the first meanwhile, and keeps the fastest
+ * (DESIGN.md "Placement"). */
+typedef struct slime_rs_alloc_info {
+  int kind;                /* kept placement: 0 = physical chunks mapped into one range, 1 = hipMalloc */
+  int probes;              /* placements probed (0: buffer too small, not probed) */
+  int chosen;              /* index into probe_* of the kept placement */
+  uint64_t chunk_bytes;    /* kept placement's chunk size (0 for hipMalloc) */
+  double probe_gbs[4];     /* each probed placement's rate */
+  uint64_t probe_chunk[4]; /* each probed placement's chunk size (0: hipMalloc) */
+} slime_rs_alloc_info_t;
+int slime_rs_device_alloc_info(const void *ptr, slime_rs_alloc_info_t *info);
 /* Frees a buffer from slime_rs_device_alloc (its base).  Waits for the device
  * first (hipDeviceSynchronize), so work still queued on it cannot fault.
  * Returns SLIME_RS_ERR_INVALID_ARG for other pointers. */

@@ -54,6 +54,13 @@ class HostStats(ctypes.Structure):
                                                 "copy_out_us", "total_us")]
 
 
+class AllocInfo(ctypes.Structure):
+    """slime_rs_alloc_info_t: how slime_rs_device_alloc placed a buffer."""
+    _fields_ = [("kind", ctypes.c_int), ("probes", ctypes.c_int), ("chosen", ctypes.c_int),
+                ("chunk_bytes", ctypes.c_uint64), ("probe_gbs", ctypes.c_double * 4),
+                ("probe_chunk", ctypes.c_uint64 * 4)]
+
+
 class Layout(ctypes.Structure):
     """slime_rs_layout_t: shard s of object o at base + o*obj_stride + s*shard_stride."""
     _fields_ = [("obj_stride", ctypes.c_uint64), ("shard_stride", ctypes.c_uint64)]
@@ -71,6 +78,7 @@ SIGNATURES = [
     ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_device_alloc", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("slime_rs_device_free", ctypes.c_int, [ctypes.c_void_p]),
+    ("slime_rs_device_alloc_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AllocInfo)]),
     ("slime_gf_max_val", ctypes.c_uint32, []),
     ("slime_gf_minverse", ctypes.c_uint32, [ctypes.c_uint32]),
     ("slime_gf_raise", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
@@ -260,6 +268,17 @@ def digest_info() -> tuple[bool, int]:
     e, t = ctypes.c_int(), ctypes.c_int()
     check(lib.slime_rs_digest_info(ctypes.byref(e), ctypes.byref(t)))
     return bool(e.value), int(t.value)
+
+
+def alloc_info(ptr: int) -> dict:
+    """Placement of a slime_rs_device_alloc buffer (its base): probed rates and the one kept."""
+    st = AllocInfo()
+    check(lib.slime_rs_device_alloc_info(ctypes.c_void_p(ptr), ctypes.byref(st)))
+    n = st.probes
+    kinds = ["hipMalloc" if st.probe_chunk[i] == 0 else f"{st.probe_chunk[i] >> 20} MiB chunks" for i in range(n)]
+    return {"kept": ("hipMalloc" if st.kind == 1 else f"{st.chunk_bytes >> 20} MiB chunks"),
+            "probes": [{"placement": kinds[i], "probe_gbs": round(st.probe_gbs[i], 1)} for i in range(n)],
+            "retries": max(0, n - 1), "chosen": st.chosen if n else None}
 
 
 def ticket_sets(device: int) -> tuple[int, int]:

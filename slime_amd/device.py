@@ -99,6 +99,12 @@ def device_empty(numel: int, dtype: torch.dtype = torch.int32, device: int = 0) 
     return t
 
 
+def placement(t: torch.Tensor) -> dict:
+    """How device_empty placed t's buffer (slime_rs_device_alloc_info): the
+    placements probed, their probe rates and the one kept."""
+    return N.alloc_info(t.data_ptr())
+
+
 def layout_of(nshards: int, L: int, shard_stride: Optional[int] = None) -> N.Layout:
     ss = L if shard_stride is None else shard_stride
     return N.Layout(obj_stride=ss * nshards, shard_stride=ss)

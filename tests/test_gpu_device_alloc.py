@@ -99,3 +99,49 @@ def test_concurrent_alloc_free(torch_dev):
     for t in ts:
         t.join()
     assert not errors
+
+
+def test_placement_probe_keeps_the_fastest_candidate(torch_dev, monkeypatch):
+    """A 16 GiB buffer with an unreachable probe target: the allocator probes
+    its first placement and both alternatives (1 GiB chunks, hipMalloc), keeps
+    the fastest, releases the others, and the buffer it returns computes
+    exactly like any other."""
+    torch = torch_dev
+    from slime_amd import device as D
+    monkeypatch.setenv("SLIME_RS_PLACEMENT_MIN_GBS", "1e9")
+    free0, _ = torch.cuda.mem_get_info()
+    buf = D.device_empty(4 << 30, torch.int32)  # 16 GiB
+    info = D.placement(buf)
+    assert info["retries"] == 2 and len(info["probes"]) == 3, info
+    rates = [p["probe_gbs"] for p in info["probes"]]
+    assert all(r > 1000 for r in rates), info
+    assert info["chosen"] == rates.index(max(rates))
+    assert info["kept"] == info["probes"][info["chosen"]]["placement"]
+    free1, _ = torch.cuda.mem_get_info()
+    assert free0 - free1 < (16 << 30) + (2 << 30), "the losing placements were released"
+    need, total, L, nobj = 8, 12, 4099, 5
+    rng = np.random.default_rng(3)
+    h = rng.integers(0, 2**32, size=(nobj, total, L), dtype=np.uint64).astype(np.uint32)
+    off = (3 << 30) + 12345  # somewhere past the first GiB
+    buf[off: off + h.size].copy_(torch.from_numpy(h.view(np.int32).reshape(-1)))
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, src_offset=off, dst_offset=off + need * L)
+    torch.cuda.synchronize()
+    got = buf[off: off + h.size].cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+    for o in range(nobj):
+        ref = np.ascontiguousarray(h[o])
+        OC.encode_object(ref, need, total)
+        assert np.array_equal(got[o], ref), o
+    del buf
+    torch.cuda.synchronize()
+
+
+def test_placement_probe_skips_small_buffers_and_fast_ones(torch_dev, monkeypatch):
+    torch = torch_dev
+    from slime_amd import device as D
+    small = D.device_empty(1 << 20, torch.int32)
+    assert D.placement(small)["probes"] == [] and D.placement(small)["retries"] == 0
+    monkeypatch.setenv("SLIME_RS_PLACEMENT_MIN_GBS", "1")  # any placement is fast enough
+    big = D.device_empty(4 << 30, torch.int32)
+    info = D.placement(big)
+    assert len(info["probes"]) == 1 and info["retries"] == 0 and info["chosen"] == 0

@@ -7,6 +7,8 @@ so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
 
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r03/pmc_traffic.json
     python tools/pmc_traffic.py --all <fetch_dir> <write_dir>    # every kernel: HBM bytes per dispatch
+    python tools/pmc_traffic.py --bytes <fetch_dir> <write_dir> <config> <session> [<existing json>]
+        # the fused byte path's kernels (bench.py object_bytes_path), appended to a list
 
 `kernel_code` (slime_amd/codeobj.py: a hash of the measured kernel's gfx950
 machine code in the built library) ties the summary to the build it was
@@ -74,9 +76,39 @@ def kernel_code(kernel: str, need: int) -> str | None:
     return kernel_code_id(os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so"), (f"{kernel}ILi{need}E",))
 
 
+BYTE_KERNELS = ("encode_bytes_queue_kernel", "encode_bytes_redo_kernel", "decode_bytes_queue_kernel")
+
+
+def byte_kernels(fetch_dir, write_dir, config, session, existing=None):
+    """HBM bytes per dispatch of the byte path's product kernels at `config`
+    ("need/total S=<bytes> nobj=<n>"), with each kernel's machine code."""
+    need = int(config.split("/")[0])
+    sums = {}
+    for d, counter in ((fetch_dir, "FETCH_SIZE"), (write_dir, "WRITE_SIZE")):
+        for path in glob.glob(f"{d}/*counter_collection.csv"):
+            for r in csv.DictReader(open(path)):
+                name = next((k for k in BYTE_KERNELS if k + "<" in r["Kernel_Name"]), None)
+                if name and r["Counter_Name"] == counter:
+                    sums.setdefault(name, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
+    entry = {"config": config, "session": session, "kernels": {}}
+    for name, c in sums.items():
+        f, w = c.get("FETCH_SIZE", []), c.get("WRITE_SIZE", [])
+        if not f or not w:
+            continue
+        entry["kernels"][name] = {"kernel_code": kernel_code(name, need), "dispatches": [len(f), len(w)],
+                                  "read_bytes": int(2 * 1024 * sum(f) / len(f)),
+                                  "write_bytes": int(1024 * sum(w) / len(w)),
+                                  "hbm_bytes": int(2 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w))}
+    entries = json.load(open(existing)) if existing and os.path.exists(existing) else []
+    entries = [e for e in entries if e.get("config") != config] + [entry]
+    print(json.dumps(entries, indent=1))
+
+
 def main():
     if sys.argv[1] == "--all":
         return all_kernels(sys.argv[2], sys.argv[3])
+    if sys.argv[1] == "--bytes":
+        return byte_kernels(*sys.argv[2:7])
     fetch_dir, write_dir, config = sys.argv[1:4]
     session = sys.argv[4] if len(sys.argv) > 4 else "?"
     f, fk = per_dispatch(fetch_dir, "FETCH_SIZE")
