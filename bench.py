@@ -148,6 +148,16 @@ def launch_ranks(args) -> int:
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
+    import signal
+
+    def stop(signum, _frame):  # the launcher is being stopped: stop the ranks it started, then exit
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
     rc = 0
     live = list(procs)
     while live:
