@@ -341,8 +341,9 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
 #undef QN
   Q(8, 4, 1, 1) Q(8, 1, 8, 1) Q(8, 2, 8, 1) Q(8, 4, 8, 1) Q(8, 8, 8, 1) Q(10, 2, 8, 1) Q(10, 4, 8, 1)
   Q(8, 2, 8, 2) Q(8, 2, 8, 4) Q(8, 1, 8, 4) Q(8, 1, 8, 8)
-  // k = 4 (C2): U = 3, 2, 1
+  // k = 4 (C2): U = 3, 2, 1; round 3: U = 5, 6, 8 (more bytes in flight per wave)
   Q(4, 2, 8, 1) Q(4, 4, 8, 1) QU(4, 2, 3, 8, 1) QU(4, 1, 6, 8, 1) QU(4, 1, 12, 8, 1) QU(4, 4, 2, 8, 1)
+  QU(4, 5, 1, 8, 1) QU(4, 6, 1, 8, 1) QU(4, 6, 2, 8, 1) QU(4, 8, 1, 8, 1) QU(4, 4, 1, 8, 1)
   // k = 8: U = 4, 2
   QU(8, 4, 2, 8, 1) QU(8, 4, 1, 8, 1) QU(8, 2, 3, 8, 1) QU(8, 2, 2, 8, 1) Q(8, 3, 8, 1)
   // k = 16: U = 1, 2
