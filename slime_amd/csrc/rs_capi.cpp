@@ -511,7 +511,7 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
-  double t_in = 0, t_wait = 0, t_out = 0, t_enq = 0;
+  double t_in = 0, t_wait = 0, t_out = 0, t_enq = 0, t_h2d = 0, t_launch = 0;
   const int S = (int)std::min<uint64_t>(Workspace::kStages, n);
   if (int rc = ws->reserve_pinned(stage_bytes * S)) return rc;
   if (int rc = ws->ensure_stages()) return rc;
@@ -562,10 +562,14 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       t0 = clk::now();
       hipStream_t st = ws->sst[s];
       if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;
+      const double a = ms_since(t0);
       if (int rc = launch(c, s, st)) return rc;
+      const double b = ms_since(t0);
       if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) return rc;
       HIP_TRY(hipEventRecord(ws->sev[s], st));
       t_enq += ms_since(t0);
+      t_h2d += a;
+      t_launch += b - a;
     }
     for (uint64_t c = n > (uint64_t)S ? n - S : 0; c < n; ++c)
       if (int rc = land((int)(c % S))) return rc;
@@ -583,8 +587,11 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   g_host_stats.copy_out_us.fetch_add(us(t_out), std::memory_order_relaxed);
   g_host_stats.total_us.fetch_add(us(t_total), std::memory_order_relaxed);
   if (trace)
-    fprintf(stderr, "slime_rs %s windows=%llu copy_in=%.3f enqueue=%.3f wait=%.3f copy_out=%.3f total=%.3f ms\n", what,
-            (unsigned long long)n, t_in, t_enq, t_wait, t_out, t_total);
+    fprintf(stderr,
+            "slime_rs %s windows=%llu copy_in=%.3f enqueue=%.3f (h2d %.3f launch %.3f d2h %.3f) wait=%.3f "
+            "copy_out=%.3f total=%.3f ms\n",
+            what, (unsigned long long)n, t_in, t_enq, t_h2d, t_launch, t_enq - t_h2d - t_launch, t_wait, t_out,
+            t_total);
   return rc;
 }
 
