@@ -478,8 +478,46 @@ struct Window {
 size_t round64(size_t n) { return (n + 63) & ~(size_t)63; }
 
 // DMA spans one by one, merging neighbours contiguous on both sides.
+// Runs of equal-length spans at constant device and pinned strides (a
+// window's rows: one per chunk) go as one pitched copy when SLIME_RS_DMA_2D=1.
+bool dma_2d() {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_DMA_2D");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
               hipStream_t st) {
+  if (dma_2d() && sp.size() >= 2) {
+    for (size_t i = 0; i < sp.size();) {
+      size_t j = i + 1;
+      const uint64_t bytes = sp[i].bytes;
+      const int64_t dd = j < sp.size() ? (int64_t)sp[j].dev_off - (int64_t)sp[i].dev_off : 0;
+      const int64_t dp = j < sp.size() ? (int64_t)off[j] - (int64_t)off[i] : 0;
+      if (dd >= (int64_t)bytes && dp >= (int64_t)bytes)
+        while (j < sp.size() && sp[j].bytes == bytes && (int64_t)sp[j].dev_off - (int64_t)sp[j - 1].dev_off == dd &&
+               (int64_t)off[j] - (int64_t)off[j - 1] == dp)
+          ++j;
+      if (j - i >= 2) {
+        if (h2d)
+          HIP_TRY(hipMemcpy2DAsync(dev + sp[i].dev_off, (size_t)dd, pin + off[i], (size_t)dp, bytes, j - i,
+                                   hipMemcpyHostToDevice, st));
+        else
+          HIP_TRY(hipMemcpy2DAsync(pin + off[i], (size_t)dp, dev + sp[i].dev_off, (size_t)dd, bytes, j - i,
+                                   hipMemcpyDeviceToHost, st));
+      } else {
+        j = i + 1;
+        if (h2d)
+          HIP_TRY(hipMemcpyAsync(dev + sp[i].dev_off, pin + off[i], bytes, hipMemcpyHostToDevice, st));
+        else
+          HIP_TRY(hipMemcpyAsync(pin + off[i], dev + sp[i].dev_off, bytes, hipMemcpyDeviceToHost, st));
+      }
+      i = j;
+    }
+    return 0;
+  }
   for (size_t i = 0; i < sp.size();) {
     size_t j = i + 1, bytes = sp[i].bytes;
     while (j < sp.size() && sp[j].dev_off == sp[i].dev_off + bytes && off[j] == off[i] + bytes) bytes += sp[j++].bytes;

@@ -58,7 +58,9 @@ for step in "$@"; do
     c2tail) run c2tail 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256 --nseg 2 --rounds 5 --queue 400802 --timed 3 ;;
     c2u) run c2u_enc 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 256,512 --nseg 2 --rounds 5 --queue 400802,400801,500801,600801,600802,800801 &&
          run c2u_dec 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --decode 1 --separate 0 --variants 13 --blocks 256,512 --nseg 2 --rounds 5 --queue 400802,400801,500801,600801,600802,800801 ;;
-    hosttrace) run hosttrace 300 python tools/host_trace.py ;;
+    hosttrace) run hosttrace 300 python tools/host_trace.py &&
+               run hosttrace_2d 300 env SLIME_RS_DMA_2D=1 python tools/host_trace.py &&
+               run hosttrace_b 300 python tools/host_trace.py ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
