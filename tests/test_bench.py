@@ -103,3 +103,21 @@ def test_committed_traffic_matches_shipped_kernel_code():
         "apply kernel's machine code changed since its PMC passes: re-run tools/gpu_r03.sh pmc_fetch pmc_write"
     alg = 128 * 4 * 8388608 * 12
     assert abs(tj["hbm_bytes_per_launch"] / alg - 1) < 0.01  # no wasted re-reads
+
+
+def test_kernel_code_ids_name_one_kernel_each():
+    """slime_amd/codeobj.py finds exactly one gfx950 kernel per fragment bench.py
+    asks for (the apply and byte-path kernels of the BASELINE shapes), and
+    distinct kernels hash differently."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from slime_amd.codeobj import kernel_code_id
+    lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
+    ids = {}
+    for need in (4, 8, 10):
+        for k in ("rs_apply_queue_kernel", "encode_bytes_queue_kernel", "encode_bytes_redo_kernel",
+                  "decode_bytes_queue_kernel"):
+            ids[(k, need)] = kernel_code_id(lib, (f"{k}ILi{need}E",))
+            assert ids[(k, need)] is not None, (k, need)
+    assert len(set(ids.values())) == len(ids)
+    assert kernel_code_id(lib, ("no_such_kernel",)) is None
