@@ -100,7 +100,7 @@ def parse(argv=None):
                          "starts on a cache-line boundary; 1 = packed, stride L)")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
-                         "used only when its config and kernel source match this run)")
+                         "used only when its config and the kernel's machine code match this build)")
     args = ap.parse_args(argv)
     if args.preset:
         given = {a.split("=")[0] for a in (argv if argv is not None else sys.argv[1:]) if a.startswith("--")}
@@ -407,15 +407,22 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     have = [i for i in range(total) if i not in erase][:need]
     r = total - need
 
+    last_split = {}
+
     def med(fn):
+        """Median wall time of `reps` calls after a warm one; last_split gets the
+        pipeline split (slime_rs_host_stats) of the median call itself."""
         fn()
         N.host_stats(reset=True)  # the pipeline split covers the timed calls only
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
             fn()
-            ts.append(time.perf_counter() - t0)
-        return sorted(ts)[len(ts) // 2]
+            ts.append((time.perf_counter() - t0, N.host_stats(reset=True)))
+        t, st = sorted(ts, key=lambda x: x[0])[len(ts) // 2]
+        last_split.clear()
+        last_split.update(st)
+        return t
 
     def split(st):  # ms per call of the windowed pipeline, from slime_rs_host_stats
         c = max(1, st["calls"])
@@ -424,11 +431,11 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
 
     box = {}
     t_w = med(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
-    split_w = split(N.host_stats(reset=True))
+    split_w = split(last_split)
     t_wz = med(lambda: objects.write_chunks(data, need, total, out=chunks, alias=True))
     surv = [chunks[i] for i in have]
     t_r = med(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
-    split_r = split(N.host_stats(reset=True))
+    split_r = split(last_split)
     ok = bool(np.array_equal(out, data))
 
     # The unchanged caller, call by call (Go API mirrors, slime_amd.rs / .gf).
@@ -464,7 +471,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "write_chunks_zero_copy_gibs": g(t_wz),
             "link": link_probe(obj_mib),
             "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
-                               "what": "mean per call: host copies in/out, launches, waits on the device/link side "
+                               "what": "the median call's split: host copies in/out, launches, waits on the device/link side "
                                        "(a large wait with normal copies = DMA contention, DESIGN.md End-to-end)"},
             "unchanged_caller": {
                 "write_gibs": g(t_uw), "read_gibs": g(t_ur),
