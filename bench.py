@@ -124,6 +124,14 @@ def visible_gpus() -> int:
     return torch.cuda.device_count()
 
 
+def shared_gpu_rehearsal() -> bool:
+    """SLIME_BENCH_SHARE_GPU=1: let more ranks than GPUs share them (rank r on
+    GPU r % n) -- a rehearsal of the multi-rank path on a 1-GPU box, never a
+    scaling number: the line then says "rehearsal" and n_gpus counts the
+    distinct GPUs actually used."""
+    return os.environ.get("SLIME_BENCH_SHARE_GPU") == "1"
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -139,7 +147,7 @@ def launch_ranks(args) -> int:
     rank's (the other ranks are then stopped: they would wait at a barrier)."""
     import subprocess
     ndev = visible_gpus()
-    if args.gpus > ndev:
+    if args.gpus > ndev and not shared_gpu_rehearsal():
         print(f"bench.py: --gpus {args.gpus} but {ndev} visible GPU(s); one rank per GPU", file=sys.stderr, flush=True)
         return 2
     env = dict(os.environ, WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
@@ -637,7 +645,7 @@ def main():
     # One rank per GPU.  More ranks than visible GPUs would put two ranks on
     # one device and overstate the scaling curve: refuse.
     ndev = visible_gpus()
-    if world > ndev or local >= ndev:
+    if (world > ndev or local >= ndev) and not (shared_gpu_rehearsal() and ndev > 0):
         print(f"bench.py: {world} ranks (local rank {local}) but {ndev} visible GPU(s); one rank per GPU",
               file=sys.stderr, flush=True)
         sys.exit(2)
@@ -652,7 +660,7 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    dev = local
+    dev = local % max(1, ndev)
     torch.cuda.set_device(dev)
 
     need, total = args.need, args.total
@@ -866,6 +874,8 @@ def main():
                 "measured_streams": ceilings,
             },
             "cpu_baseline": None,
+            "rehearsal": (f"{world} ranks sharing {len(set(bdfs))} GPU(s) (SLIME_BENCH_SHARE_GPU=1): "
+                          "a test of the multi-rank path, not a scaling number") if shared_gpu_rehearsal() else None,
             "object_bytes_path": bytes_path,
             "allocator_probe": alloc_probe,
         }
