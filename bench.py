@@ -95,6 +95,9 @@ def parse(argv=None):
     ap.add_argument("--alloc-probe", type=int, default=1,
                     help="with --allocator vmm: also time 3 encodes and decodes of the same batch in a torch.empty "
                          "(hipMalloc) buffer, reported as allocator_probe (not value)")
+    ap.add_argument("--chunk-align", type=int, default=1,
+                    help="byte path: chunk stride alignment in bytes (1: the wire layout, chunks 4L apart; "
+                         "256: every chunk on a line boundary)")
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
@@ -289,7 +292,8 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     from chunk bytes.  Objects that would need MapToGF's random
     fallback are re-drawn before timing and counted."""
     S = args.object_mib << 20
-    L, chunk, slot = D.slot_geometry(S, need, total)
+    L, cs, slot = D.slot_geometry(S, need, total, chunk_align=args.chunk_align)
+    chunk_stride = cs if args.chunk_align > 1 else 0
     slots = batch_empty(args, nobj * slot, torch.uint8, dev)
     placement = D.placement(slots) if args.allocator == "vmm" else None
     words = slots.view(torch.int32)
@@ -302,22 +306,26 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     stream = torch.cuda.current_stream(dev)
     redraws = 0
     for attempt in range(64):
-        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream)
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream, chunk_stride)
         bad = status.nonzero().flatten().tolist()
         if not bad:
             break
         for o in bad:  # re-draw the object from another seed
-            D.fill_symbols(words[o * slot // 4:(o * slot + S) // 4], 0xB17E5 + (attempt + 1) * 2**32 + o)
+            D.fill_symbols(words[o * slot // 4:(o * slot + need * cs) // 4], 0xB17E5 + (attempt + 1) * 2**32 + o)
         redraws += len(bad)
-    truth = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)[:, erase, :].clone()
+
+    def erased():
+        return slots.view(nobj, slot)[:, : total * cs].view(nobj, total, cs)[:, erase, : 4 * L]
+
+    truth = erased().clone()
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream)
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream, chunk_stride)
         if ev is not None:
             ev[1].record(stream)
-        D.decode_objects(dec, slots, slot, L, nobj, mapping, stream)
+        D.decode_objects(dec, slots, slot, L, nobj, mapping, stream, chunk_stride)
         if ev is not None:
             ev[2].record(stream)
 
@@ -334,8 +342,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
-    got = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)[:, erase, :]
-    ok = bool(torch.equal(got, truth)) and int(status.sum().item()) == 0
+    ok = bool(torch.equal(erased(), truth)) and int(status.sum().item()) == 0
     ms = mapping.cpu().numpy().view("uint32")
     elapsed, = batch.max_over_ranks([elapsed])
     del slots, words, truth
@@ -363,6 +370,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
             "mappings": {"0": int((ms == 0).sum()), "1<<31": int((ms == 0x80000000).sum()),
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
             "fallback_redraws": redraws, "verified": ok, "placement": placement,
+            "chunk_stride": cs, "chunk_bytes": 4 * L,
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
                     "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
                     "erased chunks from chunk bytes"}

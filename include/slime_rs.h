@@ -228,6 +228,20 @@ int slime_rs_resolve_fallbacks(slime_rs_plan_t encode_plan, uint8_t *slots, uint
  * object's mapping value (meta.File.MappingValue).  Asynchronous. */
 int slime_rs_decode_objects(slime_rs_plan_t reconstruct_plan, uint8_t *slots, uint64_t slot_stride, uint64_t L,
                             uint64_t nobj, const uint32_t *mapping, void *stream);
+/* The same three over a slot layout whose chunks are chunk_stride bytes apart
+ * (chunk c at slot + c*chunk_stride; chunk_stride >= 4L, a multiple of 4; 0
+ * selects 4L, the forms above).  Object byte i then lives in chunk i / 4L at
+ * offset i % 4L: the device-resident layout the caller fills chunk by chunk
+ * (e.g. 256 B-aligned chunk_stride, every chunk on a line boundary). */
+int slime_rs_encode_objects_chunked(slime_rs_plan_t encode_plan, uint8_t *slots, uint64_t slot_stride,
+                                    uint64_t chunk_stride, uint64_t object_size, uint64_t nobj, uint32_t *mapping,
+                                    uint32_t *status, void *stream);
+int slime_rs_resolve_fallbacks_chunked(slime_rs_plan_t encode_plan, uint8_t *slots, uint64_t slot_stride,
+                                       uint64_t chunk_stride, uint64_t object_size, uint64_t nobj, uint32_t *mapping,
+                                       uint32_t *status, void *stream, int *resolved);
+int slime_rs_decode_objects_chunked(slime_rs_plan_t reconstruct_plan, uint8_t *slots, uint64_t slot_stride,
+                                    uint64_t chunk_stride, uint64_t L, uint64_t nobj, const uint32_t *mapping,
+                                    void *stream);
 
 /* ---- Object entry points over host memory (the callers' data paths) ----
  *

@@ -119,6 +119,15 @@ SIGNATURES = [
     ("slime_rs_decode_objects", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
       ctypes.c_void_p]),
+    ("slime_rs_encode_objects_chunked", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_resolve_fallbacks_chunked", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_intp]),
+    ("slime_rs_decode_objects_chunked", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_chunk_size", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int]),
     ("slime_rs_write_chunks", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, c_u32p]),

@@ -109,7 +109,7 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
 }
 
 // --- fused byte-domain encode/decode over object slots (rs_bytes.hip) --------
-// Slot o at slots + o*slot_stride bytes; chunk c at slot + c*4L.  coeff /
+// Slot o at slots + o*slot_stride bytes; chunk c at slot + c*cstride (4L by default).  coeff /
 // in_idx / out_idx are a plan's device tables.  Encode: phase 0 = speculative
 // (mapping 0, OR MapToGF flag bits into flags[obj]); select_mapping turns the
 // flags into mapping[] and a fallback status in place; phase 1 re-encodes the
@@ -135,7 +135,9 @@ struct BytesLaunch {
   // that used the wrong mapping.  Null: phase 1 re-encodes whole objects.
   uint8_t* scratch = nullptr;
   bool* switched = nullptr;
+  uint64_t cstride = 0;  // bytes between a slot's chunks (0: 4L, the wire layout)
 };
+inline uint64_t chunk_stride(const BytesLaunch& a) { return a.cstride ? a.cstride : 4 * a.L; }
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
 // Scratch bytes the mid-object switch needs for this launch; 0 when its
 // phase 0 would not run the switching (dynamic-schedule) kernel.

@@ -90,11 +90,11 @@ hipError_t enc_pipe(const BytesLaunch& a, hipStream_t s) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, U, 0>),
                        grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, pipe_blocks<K>(), U), dim3(kBlock), 0, s,
-                       a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
+                       a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
                        a.mapping, nseg);
   } else {
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, U, 1>), grid_for(ncols, 1, 1, pipe_blocks<K>(), U),
-                       dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
+                       dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                        a.out_idx, a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
@@ -124,7 +124,7 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
         s,
         [&](uint32_t* set) {
           hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),
-                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
                              ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, set, spread);
           return hipGetLastError();
         },
@@ -134,7 +134,7 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_pipe_kernel<K, U>),
                      grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, pipe_blocks<K>(), U), dim3(kBlock), 0, s, a.slots,
-                     a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, nseg);
+                     a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, nseg);
   return hipGetLastError();
 }
 
@@ -149,11 +149,11 @@ hipError_t enc_k(const BytesLaunch& a, hipStream_t s) {
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((encode_bytes_kernel<K, U, 0>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock),
-                       0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
+                       0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
                        a.flags, a.mapping, nseg);
   } else {
     hipLaunchKernelGGL((encode_bytes_kernel<K, U, 1>), grid_for(ncols, 1, 1), dim3(kBlock), 0, s, a.slots,
-                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
+                       a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
                        a.mapping, 1u);
   }
   return hipGetLastError();
@@ -166,7 +166,7 @@ hipError_t dec_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((decode_bytes_kernel<K, U>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock), 0, s,
-                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx,
+                     a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx,
                      a.mapping, nseg);
   return hipGetLastError();
 }
@@ -185,11 +185,11 @@ hipError_t enc_wide_pipe(const BytesLaunch& a, hipStream_t s) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_wide_pipe_kernel<RB, 0>),
                        grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), 0, s, a.slots,
-                       a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
+                       a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags,
                        a.mapping, nseg);
   } else {
     hipLaunchKernelGGL((bytes::encode_bytes_wide_pipe_kernel<RB, 1>), grid_for(ncols, 1, 1, blocks, 1), dim3(kBlock),
-                       0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
+                       0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
                        a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
@@ -202,10 +202,10 @@ hipError_t enc_wide_k(const BytesLaunch& a, hipStream_t s) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 0>),
                        grid_for(ncols, (uint64_t)a.nobj * nseg, nseg), dim3(kBlock), 0, s, a.slots, a.slot_stride,
-                       a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping, nseg);
+                       a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx, a.flags, a.mapping, nseg);
   } else {
     hipLaunchKernelGGL((bytes::encode_bytes_wide_kernel<KC, kWideRows, 1>), grid_for(ncols, 1, 1), dim3(kBlock), 0,
-                       s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
+                       s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.coeff, a.out_idx,
                        a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
@@ -219,7 +219,7 @@ hipError_t dec_wide_pipe(const BytesLaunch& a, hipStream_t s) {
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_wide_pipe_kernel<RB>),
                      grid_for(ncols, (uint64_t)a.nobj * nseg, nseg, a.k <= 32 ? 256 : 1024, 1), dim3(kBlock), 0, s,
-                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
+                     a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.coeff, a.in_idx, a.out_idx,
                      a.mapping, nseg);
   return hipGetLastError();
 }
@@ -229,7 +229,7 @@ hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_wide_kernel<KC, kWideRows>), grid_for(ncols, (uint64_t)a.nobj * nseg, nseg),
-                     dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.k, a.coeff,
+                     dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.coeff,
                      a.in_idx, a.out_idx, a.mapping, nseg);
   return hipGetLastError();
 }

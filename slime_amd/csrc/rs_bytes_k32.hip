@@ -38,11 +38,11 @@ hipError_t enc_k32(const BytesLaunch& a, hipStream_t s) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, 1, 0>),
                        bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, kBlocks, 1), dim3(apply::kBlock), 0, s,
-                       a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
+                       a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags,
                        a.mapping, nseg);
   } else {
     hipLaunchKernelGGL((bytes::encode_bytes_pipe_kernel<K, 1, 1>), bytes_grid(ncols, 1, 1, kBlocks, 1),
-                       dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows,
+                       dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows,
                        a.coeff, a.out_idx, a.flags, a.mapping, 1u);
   }
   return hipGetLastError();
@@ -65,7 +65,7 @@ hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
         s,
         [&](uint32_t* set) {
           hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>),
-                             dim3((uint32_t)kBlocks), dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, a.col0,
+                             dim3((uint32_t)kBlocks), dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
                              ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, set, spread);
           return hipGetLastError();
         },
@@ -75,7 +75,7 @@ hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_pipe_kernel<K, 1>),
                      bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, kBlocks, 1), dim3(apply::kBlock), 0, s,
-                     a.slots, a.slot_stride, a.L, a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx,
+                     a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx,
                      a.mapping, nseg);
   return hipGetLastError();
 }

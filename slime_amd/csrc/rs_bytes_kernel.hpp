@@ -4,10 +4,13 @@
 // :215-242) on device, without materialising the symbol domain.
 //
 // Object slot layout (bytes): slot o starts at base + o*slot_stride; chunk c
-// of object o is the 4L bytes at slot + c*4L, L = ceil(ceil(S/4)/need)
-// (splitVector, multi_store.go:272).  The object's S bytes occupy the start
-// of its slot, so data chunk j IS bytes [4jL, 4(j+1)L) of the slot once the
-// encoder has written the tail past S with what MapFromGF produces there.
+// of object o is the 4L bytes at slot + c*chunk, L = ceil(ceil(S/4)/need)
+// (splitVector, multi_store.go:272), chunk >= 4L the chunk stride (every
+// kernel takes it).  With chunk = 4L (the wire layout) the object's S bytes
+// occupy the start of its slot, so data chunk j IS bytes [4jL, 4(j+1)L) of
+// the slot once the encoder has written the tail past S with what MapFromGF
+// produces there; with a larger stride (chunks on the 256 B line grid) object
+// byte i lives in chunk i / 4L at offset i % 4L.
 //
 // Encode (one object, mapping m chosen as gf.MapToGF does, map.go:15-67):
 //   word w < nw = ceil(S/4): packed = BE(bytes[4w..4w+3]) (a partial last
@@ -227,10 +230,9 @@ __device__ __forceinline__ Segment segment_of(uint64_t wi, uint32_t nseg, uint64
 // bytes apart; the host pipeline streams an object window by window.
 template <int K, int U, int MODE, bool FAST = true, bool FLAGS_ON = true>
 __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping, uint32_t nseg) {
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -320,13 +322,12 @@ __device__ __forceinline__ void load_chunk_symbols(const uint8_t* slot, const ui
 // Column window [col0, col0 + ncols) as in encode_bytes_kernel.
 template <int K, int U>
 __global__ __launch_bounds__(kBlock) void decode_bytes_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
-                                                              uint64_t L, uint64_t col0, uint64_t ncols,
+                                                              uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols,
                                                               uint32_t nobj, uint32_t rows,
                                                               const uint32_t* __restrict__ coeff,
                                                               const uint32_t* __restrict__ in_idx,
                                                               const uint32_t* __restrict__ out_idx,
                                                               const uint32_t* __restrict__ mapping, uint32_t nseg) {
-  const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -402,10 +403,9 @@ __device__ __forceinline__ void rows_tile(const uint4 (&x)[U][K], uint32_t rows,
 
 template <int K, int U>
 __global__ __launch_bounds__(kBlock) void decode_bytes_pipe_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
-  const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
@@ -484,10 +484,9 @@ __device__ __forceinline__ void encode_interior_tile(uint4 (&r)[U][K], uint8_t* 
 // tile), which take encode_bytes_kernel's edge step without the pipeline.
 template <int K, int U, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_pipe_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping, uint32_t nseg) {
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -574,11 +573,10 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_pipe_kernel(
 // object's tiles and the schedule spans the whole batch.
 template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t* __restrict__ ticket,
     uint32_t spread) {
-  const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nvec = (uint32_t)(ncols >> 2);
   const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
@@ -667,11 +665,10 @@ __host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L
 // delays the switch: the record always tells what the unit wrote.
 template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
     uint32_t units) {
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -828,11 +825,10 @@ __global__ __launch_bounds__(kBlock) void redo_list_kernel(const uint8_t* __rest
 // list.
 template <int K, int U, int C>
 __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     const uint32_t* __restrict__ status, const uint32_t* __restrict__ mapping, const uint32_t* __restrict__ list,
     const uint32_t* __restrict__ count, uint32_t units) {
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1007,12 +1003,11 @@ __device__ __forceinline__ void encode_wide_step(uint8_t* slot, uint8_t* par, ui
 
 template <int KC, int RB, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping,
     uint32_t nseg) {
   const uint32_t cs = apply::wide_coeff_stride(k);
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
   const uint32_t lane = threadIdx.x & 63;
@@ -1047,11 +1042,10 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_kernel(
 
 template <int KC, int RB>
 __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
   const uint32_t cs = apply::wide_coeff_stride(k);
-  const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -1116,14 +1110,13 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_wide_kernel(
 // tiles, tail columns) take encode_wide_step.  MODE as in encode_bytes_kernel.
 template <int RB, int MODE>
 __global__ __launch_bounds__(kBlock) void encode_bytes_wide_pipe_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags, const uint32_t* __restrict__ mapping,
     uint32_t nseg) {
   using apply::WideItem;
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint32_t nch = (k + 15) / 16, nrb = (rows + RB - 1) / RB;
-  const uint64_t chunk = 4 * L;
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
   const uint32_t lane = threadIdx.x & 63;
@@ -1234,13 +1227,12 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_pipe_kernel(
 // block stores BE(residue ^ m).
 template <int RB>
 __global__ __launch_bounds__(kBlock) void decode_bytes_wide_pipe_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t col0, uint64_t ncols, uint32_t nobj,
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
     const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
   using apply::WideItem;
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint32_t nch = (k + 15) / 16, nrb = (rows + RB - 1) / RB;
-  const uint64_t chunk = 4 * L;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;

@@ -50,7 +50,7 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
                      count);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(256), dim3(apply::kBlock), 0, s, a.slots,
-                     a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping,
+                     a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx, a.flags, a.mapping,
                      l.list(a.scratch), count, l.units);
   return hipGetLastError();
 }
@@ -68,7 +68,7 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       s,
       [&](uint32_t* set) {
         hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(256), dim3(apply::kBlock), 0, s,
-                           a.slots, a.slot_stride, a.L, a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
+                           a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
                            a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
       },

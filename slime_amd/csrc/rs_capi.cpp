@@ -980,24 +980,34 @@ int slime_rs_plan_destroy(slime_rs_plan_t plan) {
 
 static uint64_t slot_L(uint64_t S, uint32_t need) { return ((S + 3) / 4 + need - 1) / need; }
 
-static int check_slots(const slime_rs_plan* plan, const uint8_t* slots, uint64_t slot_stride, uint64_t L,
+// Chunk stride of a slot layout: 0 selects the wire layout (4L, the object's
+// bytes contiguous); otherwise >= 4L and a multiple of 4.
+static int resolve_cstride(uint64_t L, uint64_t* cstride, const char* what) {
+  if (*cstride == 0) *cstride = 4 * L;
+  if (*cstride < 4 * L || *cstride % 4)
+    return fail(Status::InvalidArg, std::string(what) + ": chunk_stride below 4L or not a multiple of 4");
+  return 0;
+}
+
+static int check_slots(const slime_rs_plan* plan, const uint8_t* slots, uint64_t slot_stride, uint64_t cstride,
                        uint32_t first_out, const char* what) {
   if (!plan || !slots) return fail(Status::InvalidArg, std::string(what) + ": null plan or slots");
   if (plan->k == 0) return fail(Status::InvalidArg, std::string(what) + ": empty plan");
-  const uint64_t chunk = 4 * L;
   uint64_t hi = first_out + plan->out_max;
   for (uint32_t j = 0; j < plan->k; ++j) hi = std::max<uint64_t>(hi, plan->in_idx_host[j]);
-  if ((hi + 1) * chunk > slot_stride)
+  if ((hi + 1) * cstride > slot_stride)
     return fail(Status::InvalidArg, std::string(what) + ": slot_stride smaller than the chunks it must hold");
   return 0;
 }
 
-static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
-                                uint64_t S, uint64_t nobj, int phase, uint32_t* flags, const uint32_t* mapping) {
+static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint64_t slot_stride, uint64_t cstride,
+                                uint64_t L, uint64_t S, uint64_t nobj, int phase, uint32_t* flags,
+                                const uint32_t* mapping) {
   const_cast<slime_rs_plan*>(plan)->executed.store(true, std::memory_order_relaxed);
   BytesLaunch a;
   a.slots = slots;
   a.slot_stride = slot_stride;
+  a.cstride = cstride;
   a.L = L;
   a.S = S;
   a.nobj = (uint32_t)nobj;
@@ -1096,15 +1106,16 @@ struct ScratchLease {
 }  // namespace
 extern "C" {
 
-extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
-                                       uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
-                                       void* stream) {
+extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                               uint64_t chunk_stride, uint64_t object_size, uint64_t nobj,
+                                               uint32_t* mapping, uint32_t* status, void* stream) {
   if (nobj == 0) return 0;
   if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "encode_objects: nobj exceeds 2^32-1");
   if (!mapping || !status) return fail(Status::InvalidArg, "encode_objects: null mapping/status");
   const uint64_t L = slot_L(object_size, plan ? plan->k : 1);
+  if (int rc = resolve_cstride(L, &chunk_stride, "encode_objects")) return rc;
   // parity row i goes to chunk need + out_idx[i]
-  if (int rc = check_slots(plan, slots, slot_stride, L, plan ? plan->k : 0, "encode_objects")) return rc;
+  if (int rc = check_slots(plan, slots, slot_stride, chunk_stride, plan ? plan->k : 0, "encode_objects")) return rc;
   hipStream_t s = (hipStream_t)stream;
   DeviceScope ds(plan->device);
   HIP_TRY(hipMemsetAsync(status, 0, nobj * sizeof(uint32_t), s));
@@ -1113,7 +1124,7 @@ extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uin
   // Phase 0 with the mid-object mapping switch where the dynamic schedule
   // runs (a scratch record of each unit's mapping), so phase 1 redoes only
   // the units encoded before an object's first word >= p was seen.
-  BytesLaunch a0 = bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 0, status, mapping);
+  BytesLaunch a0 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 0, status, mapping);
   ScratchLease sc;
   if (int rc = sc.take(plan->device, encode_switch_bytes(a0, s), s)) return rc;
   bool switched = false;
@@ -1121,21 +1132,28 @@ extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uin
   a0.switched = &switched;
   HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
-  BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, L, object_size, nobj, 1, status, mapping);
+  BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 1, status, mapping);
   if (switched) a1.scratch = sc.ptr();
   HIP_TRY(launch_encode_bytes(a1, s));
   sc.release(s);
   return 0;
 }
 
-extern "C" int slime_rs_resolve_fallbacks(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
-                                          uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
-                                          void* stream, int* resolved) {
+extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                       uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
+                                       void* stream) {
+  return slime_rs_encode_objects_chunked(plan, slots, slot_stride, 0, object_size, nobj, mapping, status, stream);
+}
+
+extern "C" int slime_rs_resolve_fallbacks_chunked(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                                  uint64_t chunk_stride, uint64_t object_size, uint64_t nobj,
+                                                  uint32_t* mapping, uint32_t* status, void* stream, int* resolved) {
   if (resolved) *resolved = 0;
   if (nobj == 0) return 0;
   if (!mapping || !status) return fail(Status::InvalidArg, "resolve_fallbacks: null mapping/status");
   const uint64_t L = slot_L(object_size, plan ? plan->k : 1);
-  if (int rc = check_slots(plan, slots, slot_stride, L, plan ? plan->k : 0, "resolve_fallbacks")) return rc;
+  if (int rc = resolve_cstride(L, &chunk_stride, "resolve_fallbacks")) return rc;
+  if (int rc = check_slots(plan, slots, slot_stride, chunk_stride, plan ? plan->k : 0, "resolve_fallbacks")) return rc;
   hipStream_t s = (hipStream_t)stream;
   DeviceScope ds(plan->device);
   std::vector<uint32_t> st(nobj);
@@ -1156,7 +1174,10 @@ extern "C" int slime_rs_resolve_fallbacks(slime_rs_plan_t plan, uint8_t* slots, 
     uint32_t* d_cand = (uint32_t*)(lease.ws->dbuf + round16(nw * 4));
     uint32_t* d_bad = d_cand + kCand;
     uint8_t* slot = slots + o * slot_stride;
-    HIP_TRY(launch_map_pack(slot, object_size, 0, d_words, nullptr, s));
+    // the object's words, chunk by chunk (object byte i is in chunk i / 4L)
+    for (uint64_t j = 0; j * 4 * L < object_size; ++j)
+      HIP_TRY(launch_map_pack(slot + j * chunk_stride, std::min<uint64_t>(4 * L, object_size - j * 4 * L), 0,
+                              d_words + j * L, nullptr, s));
     uint32_t m = 0;
     bool found = false;
     for (int round = 0; round < (1 << 16) && !found; ++round) {
@@ -1180,23 +1201,38 @@ extern "C" int slime_rs_resolve_fallbacks(slime_rs_plan_t plan, uint8_t* slots, 
     const uint32_t zero = 0;
     HIP_TRY(hipMemcpyAsync(mapping + o, &m, 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(status + o, &zero, 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, slot_stride, L, object_size, 1, 1, status + o, mapping + o), s));
+    HIP_TRY(launch_encode_bytes(
+        bytes_launch(plan, slot, slot_stride, chunk_stride, L, object_size, 1, 1, status + o, mapping + o), s));
     HIP_TRY(hipStreamSynchronize(s));  // m and zero live on this frame
     if (resolved) ++*resolved;
   }
   return 0;
 }
 
-extern "C" int slime_rs_decode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
-                                       uint64_t nobj, const uint32_t* mapping, void* stream) {
+extern "C" int slime_rs_resolve_fallbacks(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                          uint64_t object_size, uint64_t nobj, uint32_t* mapping, uint32_t* status,
+                                          void* stream, int* resolved) {
+  return slime_rs_resolve_fallbacks_chunked(plan, slots, slot_stride, 0, object_size, nobj, mapping, status, stream,
+                                            resolved);
+}
+
+extern "C" int slime_rs_decode_objects_chunked(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                               uint64_t chunk_stride, uint64_t L, uint64_t nobj,
+                                               const uint32_t* mapping, void* stream) {
   if (nobj == 0 || L == 0) return 0;
   if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "decode_objects: nobj exceeds 2^32-1");
   if (!mapping) return fail(Status::InvalidArg, "decode_objects: null mapping");
-  if (int rc = check_slots(plan, slots, slot_stride, L, 0, "decode_objects")) return rc;
+  if (int rc = resolve_cstride(L, &chunk_stride, "decode_objects")) return rc;
+  if (int rc = check_slots(plan, slots, slot_stride, chunk_stride, 0, "decode_objects")) return rc;
   DeviceScope ds(plan->device);
-  HIP_TRY(launch_decode_bytes(bytes_launch(plan, slots, slot_stride, L, 0, nobj, 0, nullptr, mapping),
+  HIP_TRY(launch_decode_bytes(bytes_launch(plan, slots, slot_stride, chunk_stride, L, 0, nobj, 0, nullptr, mapping),
                               (hipStream_t)stream));
   return 0;
+}
+
+extern "C" int slime_rs_decode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride, uint64_t L,
+                                       uint64_t nobj, const uint32_t* mapping, void* stream) {
+  return slime_rs_decode_objects_chunked(plan, slots, slot_stride, 0, L, nobj, mapping, stream);
 }
 
 // ---- device codec / fill ------------------------------------------------------------
@@ -1737,7 +1773,7 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
                 w.out.push_back({chunks[need + i] + 4 * c0, (uint64_t)(need + i) * chunk + 4 * c0, 4 * nc});
             },
             [&](uint64_t c, int, hipStream_t st) -> int {
-              BytesLaunch a = bytes_launch(plan, slot, stride, L, size, 1, 0, d_status, d_map);
+              BytesLaunch a = bytes_launch(plan, slot, stride, 0, L, size, 1, 0, d_status, d_map);
               a.col0 = c * cl;
               a.ncols = std::min(cl, L - a.col0);
               HIP_TRY(launch_encode_bytes(a, st));
@@ -1764,7 +1800,7 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
       HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
       HIP_TRY(hipStreamSynchronize(ws->stream));
     } else if (ms[0] != 0) {  // mapping 1<<31: re-encode the whole object (map.go:47-62)
-      HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, stride, L, size, 1, 1, d_status, d_map), ws->stream));
+      HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, stride, 0, L, size, 1, 1, d_status, d_map), ws->stream));
     }
     // The data-chunk tail (partial word, splitVector padding), and every
     // parity chunk again if the mapping was not 0.
@@ -1871,7 +1907,7 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
           }
         },
         [&](uint64_t c, int, hipStream_t st) -> int {
-          BytesLaunch a = bytes_launch(plan, slot, stride, L, 0, 1, 0, nullptr, d_map);
+          BytesLaunch a = bytes_launch(plan, slot, stride, 0, L, 0, 1, 0, nullptr, d_map);
           a.col0 = c * cl;
           a.ncols = std::min(cl, L - a.col0);
           HIP_TRY(launch_decode_bytes(a, st));

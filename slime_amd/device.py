@@ -234,10 +234,15 @@ def unpack_words(words: torch.Tensor, mapping: int, dst: torch.Tensor,
 
 # ---- fused byte-domain object pipeline (writeChunks / reconstruct on device) ----
 
-def slot_geometry(object_size: int, need: int, total: int) -> tuple[int, int, int]:
-    """(L symbols per chunk, chunk bytes, minimal slot bytes) for objects of object_size bytes."""
+def slot_geometry(object_size: int, need: int, total: int, chunk_align: int = 1) -> tuple[int, int, int]:
+    """(L symbols per chunk, chunk stride in bytes, minimal slot bytes) for objects of
+    object_size bytes.  chunk_align 1 is the wire layout (chunk stride 4L, the object's
+    bytes contiguous at the slot start); e.g. 256 puts every chunk on a line boundary."""
     L = -(-(-(-object_size // 4)) // need)
-    return L, 4 * L, 4 * L * total
+    if chunk_align < 1 or chunk_align % 4 and chunk_align != 1:
+        raise ValueError("chunk_align must be 1 or a positive multiple of 4")
+    cs = -(-4 * L // chunk_align) * chunk_align
+    return L, cs, cs * total
 
 
 def _check_slots(slots: torch.Tensor, slot_stride: int, nobj: int, slot_bytes: int) -> int:
@@ -248,39 +253,51 @@ def _check_slots(slots: torch.Tensor, slot_stride: int, nobj: int, slot_bytes: i
     return _dev_index(slots)
 
 
+def _chunk_stride(L: int, chunk_stride: int) -> int:
+    cs = chunk_stride or 4 * L
+    if cs < 4 * L or cs % 4:
+        raise ValueError("chunk_stride must be 0 or a multiple of 4 that is >= 4L")
+    return cs
+
+
 def encode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,
-                   mapping: torch.Tensor, status: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> None:
-    """Device writeChunks: chunks of every object slot, gf.MapToGF's mapping per object."""
-    _, _, need_bytes = slot_geometry(object_size, plan.k, plan.k + plan.rows)
-    dev = _check_slots(slots, slot_stride, nobj, need_bytes)
+                   mapping: torch.Tensor, status: torch.Tensor, stream: Optional[torch.cuda.Stream] = None,
+                   chunk_stride: int = 0) -> None:
+    """Device writeChunks: chunks of every object slot, gf.MapToGF's mapping per object.
+    Chunk c of a slot is at slot + c*chunk_stride (0: 4L, the object's bytes in place)."""
+    L, _, _ = slot_geometry(object_size, plan.k, plan.k + plan.rows)
+    dev = _check_slots(slots, slot_stride, nobj, _chunk_stride(L, chunk_stride) * (plan.k + plan.rows))
     for t in (mapping, status):
         if t.numel() < nobj or t.dtype not in (torch.int32, torch.uint32) or _dev_index(t) != dev:
             raise ValueError("mapping/status need nobj int32 words on the slots' device")
-    N.check(lib.slime_rs_encode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, object_size, nobj,
-                                        ctypes.c_void_p(mapping.data_ptr()), ctypes.c_void_p(status.data_ptr()),
-                                        _stream_handle(dev, stream)))
+    N.check(lib.slime_rs_encode_objects_chunked(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride,
+                                                chunk_stride, object_size, nobj,
+                                                ctypes.c_void_p(mapping.data_ptr()),
+                                                ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream)))
 
 
 def resolve_fallbacks(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,
                       mapping: torch.Tensor, status: torch.Tensor,
-                      stream: Optional[torch.cuda.Stream] = None) -> int:
+                      stream: Optional[torch.cuda.Stream] = None, chunk_stride: int = 0) -> int:
     """Finish objects that need MapToGF's random mapping; returns how many were fixed."""
-    _, _, need_bytes = slot_geometry(object_size, plan.k, plan.k + plan.rows)
-    dev = _check_slots(slots, slot_stride, nobj, need_bytes)
+    L, _, _ = slot_geometry(object_size, plan.k, plan.k + plan.rows)
+    dev = _check_slots(slots, slot_stride, nobj, _chunk_stride(L, chunk_stride) * (plan.k + plan.rows))
     n = ctypes.c_int(0)
-    N.check(lib.slime_rs_resolve_fallbacks(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, object_size,
-                                           nobj, ctypes.c_void_p(mapping.data_ptr()),
-                                           ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream),
-                                           ctypes.byref(n)))
+    N.check(lib.slime_rs_resolve_fallbacks_chunked(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride,
+                                                   chunk_stride, object_size, nobj,
+                                                   ctypes.c_void_p(mapping.data_ptr()),
+                                                   ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream),
+                                                   ctypes.byref(n)))
     return n.value
 
 
 def decode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, L: int, nobj: int, mapping: torch.Tensor,
-                   stream: Optional[torch.cuda.Stream] = None) -> None:
+                   stream: Optional[torch.cuda.Stream] = None, chunk_stride: int = 0) -> None:
     """Device reconstruct: rebuild the plan's output chunks from its input chunks in every slot."""
     hi = max(plan.in_max, plan.rows - 1 if plan.out_max is None else plan.out_max)
-    dev = _check_slots(slots, slot_stride, nobj, 4 * L * (hi + 1))
+    dev = _check_slots(slots, slot_stride, nobj, _chunk_stride(L, chunk_stride) * (hi + 1))
     if mapping.numel() < nobj or mapping.dtype not in (torch.int32, torch.uint32) or _dev_index(mapping) != dev:
         raise ValueError("mapping needs nobj int32 words on the slots' device")
-    N.check(lib.slime_rs_decode_objects(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride, L, nobj,
-                                        ctypes.c_void_p(mapping.data_ptr()), _stream_handle(dev, stream)))
+    N.check(lib.slime_rs_decode_objects_chunked(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride,
+                                                chunk_stride, L, nobj, ctypes.c_void_p(mapping.data_ptr()),
+                                                _stream_handle(dev, stream)))

@@ -686,6 +686,76 @@ def test_decode_objects_repairs_chunks(torch_dev, kernel_form, need, total, S):
         assert h[o * stride: o * stride + S].tobytes() == obj
 
 
+def _make_chunked_slots(torch, objs, need, total, align):
+    """Slots whose chunks sit `cs` = roundup(4L, align) bytes apart: object byte
+    i at chunk i // 4L, offset i % 4L; every other byte 0xA5."""
+    from slime_amd import device as D
+    S = len(objs[0])
+    L, cs, slot = D.slot_geometry(S, need, total, chunk_align=align)
+    stride = slot + 64
+    host = np.full(len(objs) * stride, 0xA5, dtype=np.uint8)
+    for o, b in enumerate(objs):
+        a = np.frombuffer(b, dtype=np.uint8)
+        for j in range(need):
+            part = a[j * 4 * L: (j + 1) * 4 * L]
+            host[o * stride + j * cs: o * stride + j * cs + part.size] = part
+    return torch.from_numpy(host).cuda(), L, cs, stride
+
+
+@pytest.mark.parametrize("need,total,S,nobj", [(8, 12, (2 << 20) + 5, 9), (4, 6, 4097, 5), (10, 14, 999999, 8),
+                                               (16, 20, (1 << 20) + 3, 4), (20, 24, 300001, 3), (2, 3, 7, 3)])
+@pytest.mark.parametrize("align", [256, 4096])
+def test_objects_chunk_stride_layout(torch_dev, kernel_form, need, total, S, nobj, align):
+    """encode/resolve/decode over a slot layout with padded chunk stride
+    (slime_rs_*_objects_chunked): every chunk equals the reference framing
+    (map.go:15-67, multi_store.go:526-554), the padding between chunks is
+    untouched, and erased chunks come back bit-exact."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(S + align + nobj)
+    objs = []
+    for o in range(nobj):
+        b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+        if S >= 8 and o % 3 == 1:
+            at = 4 * ((S // 4) * 2 // 3)
+            b[at: at + 4] = b"\xff\xff\xff\xfd"  # mid-object switch to 1<<31
+        if S >= 8 and o == nobj - 1:
+            b[0:8] = b"\xff\xff\xff\xff\x7f\xff\xff\xff"  # random fallback (map_test.go TestMapTricky)
+        objs.append(bytes(b))
+    slots, L, cs, stride = _make_chunked_slots(torch, objs, need, total, align)
+    assert cs % align == 0 and cs >= 4 * L
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, nobj, mapping, status, chunk_stride=cs)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().tolist()
+    if any(st):
+        assert D.resolve_fallbacks(plan, slots, stride, S, nobj, mapping, status, chunk_stride=cs) == sum(st)
+    torch.cuda.synchronize()
+    ms = mapping.cpu().numpy().view(np.uint32)
+    h = slots.cpu().numpy()
+    for o, obj in enumerate(objs):
+        m, chunks = _oracle_chunks(obj, need, total, [int(ms[o])] if st[o] else [])
+        assert ms[o] == m, o
+        base = o * stride
+        for c in range(total):
+            assert h[base + c * cs: base + c * cs + 4 * L].tobytes() == chunks[c], (o, c)
+            assert (h[base + c * cs + 4 * L: base + (c + 1) * cs] == 0xA5).all(), ("gap", o, c)
+        assert (h[base + total * cs: base + stride] == 0xA5).all(), ("tail", o)
+    truth = slots.clone()
+    r = total - need
+    for erase in (list(range(min(r, need))), [need - 1, total - 1][:r]):
+        have = [i for i in range(total) if i not in erase][:need]
+        rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+        v = slots.view(nobj, stride)
+        for e in erase:
+            v[:, e * cs: e * cs + 4 * L] = 0x5A
+        D.decode_objects(rec, slots, stride, L, nobj, mapping, chunk_stride=cs)
+        torch.cuda.synchronize()
+        assert torch.equal(slots, truth), erase
+
+
 # ------------------------------------------------- object entry points (host memory)
 
 def _obj_bytes(rng, S, kind):

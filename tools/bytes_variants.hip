@@ -13,7 +13,7 @@ template <int U, bool FAST, bool FLAGS>
 void enc(uint8_t* slots, uint64_t stride, uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows, const uint32_t* coeff,
          const uint32_t* oi, uint32_t* flags, const uint32_t* mapping, uint32_t gx, uint32_t gy, hipStream_t s) {
   hipLaunchKernelGGL((encode_bytes_kernel<8, U, 0, FAST, FLAGS>), dim3(gx, gy), dim3(kBlock), 0, s, slots, stride, L,
-                     (uint64_t)0, L, S, nobj, rows, coeff, oi, flags, mapping, 1u);
+                     4 * L, (uint64_t)0, L, S, nobj, rows, coeff, oi, flags, mapping, 1u);
 }
 }  // namespace
 

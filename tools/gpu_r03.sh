@@ -66,6 +66,12 @@ for step in "$@"; do
                run rehearse2_torchrun 400 env SLIME_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 ;;
     placeforce) run placeforce 300 env SLIME_RS_PLACEMENT_MIN_GBS=99999 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 &&
                 run placeforce2 300 env SLIME_RS_PLACEMENT_MIN_GBS=99999 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 ;;
+    tests_cstride) run pytest_cstride 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "chunk_stride or encode_objects or decode_objects" --timeout 120 --timeout-method thread ;;
+    cstride) run cstride_c3_1 400 python bench.py --chunk-align 1 $NOLEGS &&
+             run cstride_c3_256 400 python bench.py --chunk-align 256 $NOLEGS &&
+             run cstride_c5_1 400 python bench.py --preset c5 --global-objects 16 --chunk-align 1 $NOLEGS &&
+             run cstride_c5_256 400 python bench.py --preset c5 --global-objects 16 --chunk-align 256 $NOLEGS &&
+             run cstride_c2_256 400 python bench.py --preset c2 --chunk-align 256 $NOLEGS ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
