@@ -75,6 +75,12 @@ tools/libbytesvar.so: tools/bytes_variants.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: bytesvar
 
+# Byte encode first-pass unroll / unit variants (tools only): make bqvar
+bqvar: tools/libbqvar.so
+tools/libbqvar.so: tools/bytes_queue_variants.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: bqvar
+
 # Hash throughput probe for §8(f3) (tools only): make hashprobe
 hashprobe: tools/libhashprobe.so
 tools/libhashprobe.so: tools/hash_probe.hip

@@ -95,9 +95,9 @@ def parse(argv=None):
     ap.add_argument("--alloc-probe", type=int, default=1,
                     help="with --allocator vmm: also time 3 encodes and decodes of the same batch in a torch.empty "
                          "(hipMalloc) buffer, reported as allocator_probe (not value)")
-    ap.add_argument("--chunk-align", type=int, default=1,
-                    help="byte path: chunk stride alignment in bytes (1: the wire layout, chunks 4L apart; "
-                         "256: every chunk on a line boundary)")
+    ap.add_argument("--chunk-align", type=int, default=256,
+                    help="byte path: chunk stride alignment in bytes (256: every chunk on a line boundary, the "
+                         "device slot layout; 1: the wire layout, chunks 4L apart)")
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
@@ -353,7 +353,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
     kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
-    replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj}", need)
+    replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj} cs={cs}", need)
 
     def leg(what, alg, ms):
         ach = alg / (ms * 1e-3) / 1e9

@@ -72,6 +72,7 @@ for step in "$@"; do
              run cstride_c5_1 400 python bench.py --preset c5 --global-objects 16 --chunk-align 1 $NOLEGS &&
              run cstride_c5_256 400 python bench.py --preset c5 --global-objects 16 --chunk-align 256 $NOLEGS &&
              run cstride_c2_256 400 python bench.py --preset c2 --chunk-align 256 $NOLEGS ;;
+    bqv) run bqv 400 python tools/bytes_queue_variants.py --rounds 5 --blocks 256,512 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
