@@ -352,8 +352,11 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     # the same kernels' machine code when a committed summary has it.
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
-    kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
-    replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj} cs={cs}", need)
+    mode = D.N.lib.slime_rs_switch_bits(-1)
+    topbits = mode == 1 or (mode == 2 and S >= 384 << 20)  # rs_capi.cpp use_top_bits
+    enc_kernels = ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"] + (["encode_bytes_fix_kernel"] if topbits else [])
+    kernels = {"encode": enc_kernels, "decode": ["decode_bytes_queue_kernel"]}
+    replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj} cs={cs}", need, kernels)
 
     def leg(what, alg, ms):
         ach = alg / (ms * 1e-3) / 1e9
@@ -371,12 +374,13 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
             "fallback_redraws": redraws, "verified": ok, "placement": placement,
             "chunk_stride": cs, "chunk_bytes": 4 * L,
+            "switch_phase1": "top-bit parity correction" if topbits else "re-encode of the switched units",
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
                     "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
                     "erased chunks from chunk bytes"}
 
 
-def _bytes_traffic(args, config: str, need: int) -> dict:
+def _bytes_traffic(args, config: str, need: int, kernels: dict) -> dict:
     """PMC bytes per step of the byte path's kernels at `config`, replayed from
     profiles/r03/pmc_bytes.json only where every kernel's machine code matches
     this build (slime_amd/codeobj.py); {} otherwise."""
@@ -390,8 +394,7 @@ def _bytes_traffic(args, config: str, need: int) -> dict:
         return {}
     ks = e.get("kernels", {})
     out = {}
-    for what, names in (("encode", ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"]),
-                        ("decode", ["decode_bytes_queue_kernel"])):
+    for what, names in kernels.items():
         if not all(n in ks and ks[n].get("kernel_code") == kernel_code_id(D.N.LIB_PATH, (f"{n}ILi{need}E",))
                    for n in names):
             return {}

@@ -12,29 +12,33 @@ namespace {
 template <int K, int U, int C>
 int launch(uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows,
            const uint32_t* coeff, const uint32_t* out_idx, uint32_t* flags, uint32_t* ticket, uint32_t blocks,
-           hipStream_t s) {
+           uint8_t* record, hipStream_t s) {
   const uint32_t spread = queue_spread(nobj, L, U, C);
   if (!spread) return -2;
+  const uint32_t units = apply::walk_units<C>(bytes::encode_interior_tiles(S, L, 0, L, K, U), spread);
   hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(blocks), dim3(apply::kBlock),
                      0, s, slots, stride, L, cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket,
-                     spread, (uint8_t*)nullptr, 0u);
+                     spread, record, record ? units : 0u, (uint8_t*)nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace
 
+// record: the mid-object switch's per-unit record (>= nobj x units bytes) or
+// null (mapping 0 throughout, as the capture form runs).
 // variant: 0 <8,2,3> (product), 1 <8,3,2>, 2 <8,4,2>, 3 <10,1,6> (product), 4 <10,2,3>, 5 <10,3,2>, 6 <8,1,6>
 extern "C" int bqv_encode(int variant, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S,
                           uint32_t nobj, uint32_t rows, const uint32_t* coeff, const uint32_t* out_idx,
-                          uint32_t* flags, uint32_t* ticket, uint32_t blocks, void* stream) {
+                          uint32_t* flags, uint32_t* ticket, uint32_t blocks, uint8_t* record,
+                          void* stream) {
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
-    case 0: return launch<8, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 1: return launch<8, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 2: return launch<8, 4, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 3: return launch<10, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 4: return launch<10, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 5: return launch<10, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
-    case 6: return launch<8, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, s);
+    case 0: return launch<8, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 1: return launch<8, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 2: return launch<8, 4, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 3: return launch<10, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 4: return launch<10, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 5: return launch<10, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 6: return launch<8, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
     default: return -3;
   }
 }

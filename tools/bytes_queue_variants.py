@@ -35,12 +35,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--blocks", type=str, default="256")
     ap.add_argument("--shapes", type=str, default="c5,c3")
+    ap.add_argument("--switch", type=str, default="0,1", help="0: no switch record; 1: the product's switching pass")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libbqvar.so"))
     lib.bqv_encode.restype = ctypes.c_int
     lib.bqv_encode.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32] + [ctypes.c_void_p] * 4 + \
-        [ctypes.c_uint32, ctypes.c_void_p]
+        [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     s = torch.cuda.current_stream()
     ticket = torch.zeros(lib.bqv_ticket_words(), dtype=torch.int32, device="cuda")
     out = {}
@@ -56,15 +57,18 @@ def main():
         c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
         oi = torch.arange(rows, dtype=torch.int32, device="cuda")
         flags = torch.zeros(nobj, dtype=torch.int32, device="cuda")
-        par = slots.view(nobj, slot)[:, need * cs:]
+        par = slots.view(nobj, total, cs)[:, need:, : 4 * L]
         alg = nobj * 4 * L * total
 
-        def run(v, blocks):
+        record = torch.zeros(nobj * (1 << 20), dtype=torch.uint8, device="cuda")
+
+        def run(v, blocks, sw=0):
             flags.zero_()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
             rc = lib.bqv_encode(v, slots.data_ptr(), slot, cs, L, S, nobj, rows, c_t.data_ptr(), oi.data_ptr(),
-                                flags.data_ptr(), ticket.data_ptr(), blocks, ctypes.c_void_p(s.cuda_stream))
+                                flags.data_ptr(), ticket.data_ptr(), blocks,
+                                ctypes.c_void_p(record.data_ptr() if sw else 0), ctypes.c_void_p(s.cuda_stream))
             b.record(s)
             torch.cuda.synchronize()
             assert rc == 0, (v, rc)
@@ -76,11 +80,13 @@ def main():
         for r in range(args.rounds + 1):
             for v in variants:
                 for blocks in (int(x) for x in args.blocks.split(",")):
-                    par.fill_(0)
-                    ms = run(v, blocks)
-                    assert torch.equal(par, ref), (shape, v, blocks)
-                    if r:
-                        times.setdefault(f"{NAMES[v]} b{blocks}", []).append(ms)
+                    for sw in (int(x) for x in args.switch.split(",")):
+                        par.fill_(0)
+                        ms = run(v, blocks, sw)
+                        if not sw:  # the switching pass writes 1<<31 units of some objects
+                            assert torch.equal(par, ref), (shape, v, blocks)
+                        if r:
+                            times.setdefault(f"{NAMES[v]} b{blocks}{' switch' if sw else ''}", []).append(ms)
         res = {}
         for k, ts in times.items():
             med = statistics.median(ts)
