@@ -352,10 +352,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     # the same kernels' machine code when a committed summary has it.
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
-    mode = D.N.lib.slime_rs_switch_bits(-1)
-    topbits = mode == 1 or (mode == 2 and S >= 384 << 20)  # rs_capi.cpp use_top_bits
-    enc_kernels = ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"] + (["encode_bytes_fix_kernel"] if topbits else [])
-    kernels = {"encode": enc_kernels, "decode": ["decode_bytes_queue_kernel"]}
+    kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
     replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj} cs={cs}", need, kernels)
 
     def leg(what, alg, ms):
@@ -374,7 +371,6 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
             "fallback_redraws": redraws, "verified": ok, "placement": placement,
             "chunk_stride": cs, "chunk_bytes": 4 * L,
-            "switch_phase1": "top-bit parity correction" if topbits else "re-encode of the switched units",
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
                     "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
                     "erased chunks from chunk bytes"}

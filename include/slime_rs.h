@@ -104,14 +104,6 @@ int slime_rs_kernel_pipeline(int mode);
  * work from ticket counters (default); 0 = static shares per wave.  mode < 0
  * queries.  Results are identical; the parity tests run both. */
 int slime_rs_kernel_schedule(int mode);
-/* Parity correction of the fused encode's mid-object mapping switch
- * (process-wide; env SLIME_RS_SWITCH_BITS sets the initial value): 1 = the
- * first pass stores bit 31 of every data word it encodes with mapping 0 (k/32
- * of its read bytes), and the units an object encoded before switching to
- * 1<<31 get their parity corrected from those bits instead of re-encoded;
- * 0 = re-encode; 2 = auto (default): on for objects of 384 MiB or more.
- * mode < 0 queries.  Results are identical; the parity tests run both. */
-int slime_rs_switch_bits(int mode);
 
 /* ==== internal/rs/gf ===================================================== */
 

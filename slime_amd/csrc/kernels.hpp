@@ -135,10 +135,6 @@ struct BytesLaunch {
   // that used the wrong mapping.  Null: phase 1 re-encodes whole objects.
   uint8_t* scratch = nullptr;
   bool* switched = nullptr;
-  // With scratch: phase 0 also stores the top bits of the tiles it encodes
-  // with mapping 0, and phase 1 corrects the switched units' parity from them
-  // instead of re-encoding (set alike on both phases; switch_top_bits()).
-  bool topbits = false;
   uint64_t cstride = 0;  // bytes between a slot's chunks (0: 4L, the wire layout)
 };
 inline uint64_t chunk_stride(const BytesLaunch& a) { return a.cstride ? a.cstride : 4 * a.L; }

@@ -650,63 +650,6 @@ __host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L
   return (uint32_t)(end_max / (64 * (uint64_t)U));
 }
 
-// Top bits of a first-pass tile's data words, for the parity correction of
-// encode_bytes_fix_kernel: bit (u*K + j)*4 + c of a lane's bit string is bit
-// 31 of the packed word of chunk j, unit u, column c -- bit 7 of the raw
-// little-endian load.  A tile's strings are stored as planes of 32 bits per
-// lane (plane q at tile + 256 q, lane-contiguous), the last plane only as
-// wide as the bits left (1, 2 or 4 bytes per lane): K*U*4 bits rounded up to
-// a byte per lane, 256 B-or-less coalesced stores.
-template <int K, int U>
-struct TopBits {
-  static constexpr int kBits = K * U * 4;
-  static constexpr int kWords = (kBits + 31) / 32;
-  static constexpr int kLastBits = kBits - 32 * (kWords - 1);
-  static constexpr int kLastBytes = kLastBits <= 8 ? 1 : kLastBits <= 16 ? 2 : 4;
-  static constexpr uint64_t kTileBytes = 64ull * (4 * (kWords - 1) + kLastBytes);
-};
-
-template <int K, int U>
-__device__ __forceinline__ void store_top_bits(const uint4 (&r)[U][K], uint8_t* __restrict__ tile, uint32_t lane) {
-  using T = TopBits<K, U>;
-  uint32_t w[T::kWords];
-#pragma unroll
-  for (int q = 0; q < T::kWords; ++q) w[q] = 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const int b = (u * K + j) * 4;
-      const uint32_t q4 = ((r[u][j].x >> 7) & 1u) | ((r[u][j].y >> 6) & 2u) | ((r[u][j].z >> 5) & 4u) |
-                          ((r[u][j].w >> 4) & 8u);
-      w[b >> 5] |= q4 << (b & 31);
-    }
-#pragma unroll
-  for (int q = 0; q + 1 < T::kWords; ++q) reinterpret_cast<uint32_t*>(tile + 256 * q)[lane] = w[q];
-  uint8_t* const last = tile + 256 * (T::kWords - 1);
-  if constexpr (T::kLastBytes == 1)
-    last[lane] = (uint8_t)w[T::kWords - 1];
-  else if constexpr (T::kLastBytes == 2)
-    reinterpret_cast<uint16_t*>(last)[lane] = (uint16_t)w[T::kWords - 1];
-  else
-    reinterpret_cast<uint32_t*>(last)[lane] = w[T::kWords - 1];
-}
-
-template <int K, int U>
-__device__ __forceinline__ void load_top_bits(const uint8_t* __restrict__ tile, uint32_t lane,
-                                              uint32_t (&w)[TopBits<K, U>::kWords]) {
-  using T = TopBits<K, U>;
-#pragma unroll
-  for (int q = 0; q + 1 < T::kWords; ++q) w[q] = reinterpret_cast<const uint32_t*>(tile + 256 * q)[lane];
-  const uint8_t* const last = tile + 256 * (T::kWords - 1);
-  if constexpr (T::kLastBytes == 1)
-    w[T::kWords - 1] = last[lane];
-  else if constexpr (T::kLastBytes == 2)
-    w[T::kWords - 1] = reinterpret_cast<const uint16_t*>(last)[lane];
-  else
-    w[T::kWords - 1] = reinterpret_cast<const uint32_t*>(last)[lane];
-}
-
 // MODE 0 (speculative) encode on the ticket walk: the interior tiles are
 // dealt as units; the few edge tiles and column tails of every object follow,
 // spread over all waves (mapping 0).  MapToGF's flags (map.go:35-62) are OR-ed
@@ -719,16 +662,13 @@ __device__ __forceinline__ void load_top_bits(const uint8_t* __restrict__ tile, 
 // (encode_bytes_redo_kernel) then redoes only the units whose mapping differs
 // from the one the object ends with -- the units encoded before the first
 // word >= p was seen -- instead of the whole object.  A stale flag read only
-// delays the switch: the record always tells what the unit wrote.  With
-// `bits` (and a record) every interior tile encoded with mapping 0 also
-// stores its top bits (TopBits), so phase 1 can correct those units' parity
-// (encode_bytes_fix_kernel) instead of re-encoding them.
+// delays the switch: the record always tells what the unit wrote.
 template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
-    uint32_t units, uint8_t* __restrict__ bits) {
+    uint32_t units) {
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -769,7 +709,6 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
       sent = 0;
     }
     if (sw && first && lane == 0) record[(uint64_t)o * units + unit] = m ? 1 : 0;
-    if (bits && m == 0) store_top_bits<K, U>(r, bits + ((uint64_t)o * nint + t) * TopBits<K, U>::kTileBytes, lane);
     encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, m, rows, coeff, out_idx,
                                      t * (64 * U) + lane, nvec, fl);
     publish();
@@ -964,75 +903,6 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
     load_data_symbols<K, false, false>(slot, chunk, L, col0, b, 1, ow, m, x, nullptr);
     fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
     rows_out<K>(x, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, 4 * b, m, 1);
-  }
-}
-
-// Phase 1 of a switched first pass that stored its top bits: the listed
-// interior units (encoded with mapping 0; their object ends with 1<<31) are
-// corrected in place instead of re-encoded.  Symbol x' = x ^ 2^31 differs
-// from x by +2^31 (bit 31 clear) or -2^31 = 2^31 - 5 (set), mod p, so parity
-// row i gains 2^31 * sum_j c_ij - 5 * sum_j c_ij * bit31(x_j); the data
-// chunks of an interior unit are the object's own bytes under either mapping
-// (MapFromGF(m, x ^ m) = x).  Per column: k bits and the r parity words read,
-// the r words written back as BE(parity' ^ 1<<31) -- 4r + k/8 bytes read and
-// 4r written instead of the re-encode's 4k and 4r.
-template <int K, int U, int C>
-__global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
-    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t chunk, uint64_t col0, uint32_t rows,
-    const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping,
-    const uint8_t* __restrict__ bits, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-    uint32_t units, uint32_t nint) {
-  constexpr int KW = TopBits<K, U>::kWords;
-  constexpr uint32_t R = 4;  // parity rows whose loads are in flight together
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwaves = gridDim.x * kWaves;
-  for (apply::ListWalk<C> w(list, *count, wave, nwaves, units, nint); w.live; w.advance()) {
-    const uint32_t o = w.obj, t = w.tile();
-    const uint32_t m = mapping[o];
-    uint32_t tb[KW];
-    load_top_bits<K, U>(bits + ((uint64_t)o * nint + t) * TopBits<K, U>::kTileBytes, lane, tb);
-    uint8_t* const par = slots + (uint64_t)o * slot_stride + 4 * col0 + (uint64_t)K * chunk;
-    const uint32_t g0 = t * (64 * U) + lane;
-    for (uint32_t i0 = 0; i0 < rows; i0 += R) {
-      uint4 v[R][U];
-#pragma unroll
-      for (uint32_t ii = 0; ii < R; ++ii)
-        if (i0 + ii < rows) {
-          const uint4* const orow = reinterpret_cast<const uint4*>(par + (uint64_t)out_idx[i0 + ii] * chunk);
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[ii][u] = orow[g0 + 64 * u];
-        }
-#pragma unroll
-      for (uint32_t ii = 0; ii < R; ++ii) {
-        if (i0 + ii >= rows) break;
-        const apply::CoeffRow<K> c = apply::load_coeff_row<K>(coeff, i0 + ii);
-        uint64_t csum = 0;
-        uint32_t d[K];  // -5 c_ij mod p
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          csum += c[j];
-          const uint32_t f = fold96(5ull * c[j], 0);
-          d[j] = f ? kP - f : 0u;
-        }
-        const uint32_t a = fold96((uint64_t)fold96(csum, 0) << 31, 0);  // 2^31 * sum_j c_ij
-        uint4* const orow = reinterpret_cast<uint4*>(par + (uint64_t)out_idx[i0 + ii] * chunk);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          uint64_t l0 = (uint64_t)be(v[ii][u].x) + a, l1 = (uint64_t)be(v[ii][u].y) + a,
-                   l2 = (uint64_t)be(v[ii][u].z) + a, l3 = (uint64_t)be(v[ii][u].w) + a;
-          uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-#pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const int b = (u * K + j) * 4;
-            const uint32_t tw = tb[b >> 5] >> (b & 31);
-            mac4(l0, l1, l2, l3, h0, h1, h2, h3, tw & 1u, (tw >> 1) & 1u, (tw >> 2) & 1u, (tw >> 3) & 1u, d[j]);
-          }
-          orow[g0 + 64 * u] = make_uint4(be(fold96(l0, h0) ^ m), be(fold96(l1, h1) ^ m), be(fold96(l2, h2) ^ m),
-                                         be(fold96(l3, h3) ^ m));
-        }
-      }
-    }
   }
 }
 

@@ -1,6 +1,6 @@
 // Host launch templates of the fused byte encode's mid-object mapping switch
 // (kernels: rs_bytes_kernel.hpp encode_bytes_queue_kernel, redo_list_kernel,
-// encode_bytes_fix_kernel, encode_bytes_redo_kernel), shared by rs_bytes.hip (need <= 16) and
+// encode_bytes_redo_kernel), shared by rs_bytes.hip (need <= 16) and
 // rs_bytes_k32.hip (17 <= need <= 24).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -15,16 +15,12 @@ namespace slime {
 // list (nobj x units words) and the per-unit mapping record (nobj x units
 // bytes) of a phase 0 on the ticket walk with C-tile units of U vectors.
 namespace bytes {
-// With a.topbits, the first pass's top bits (TopBits words per interior
-// tile, nobj x nint tiles) follow on a 256 B boundary.
 struct SwitchLayout {
   uint32_t spread = 0, nint = 0, units = 0;
-  uint64_t bits_off = 0, bytes = 0;
+  uint64_t bytes = 0;
   uint32_t* count(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p); }
-  uint32_t* zero(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p) + 1; }  // an empty list's count
   uint32_t* list(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p + 256); }
   uint8_t* record(uint8_t* p, uint32_t nobj) const { return p + 256 + 4ull * nobj * units; }
-  uint8_t* bits(uint8_t* p) const { return bits_off ? p + bits_off : nullptr; }
 };
 template <int K, int U, int C>
 SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
@@ -35,10 +31,6 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
   l.nint = encode_interior_tiles(a.S, a.L, a.col0, ncols, K, U);
   l.units = apply::walk_units<C>(l.nint, l.spread);
   l.bytes = 256 + 5ull * a.nobj * l.units;
-  if (a.topbits && l.nint) {
-    l.bits_off = (l.bytes + 255) & ~255ull;
-    l.bytes = l.bits_off + TopBits<K, U>::kTileBytes * a.nobj * l.nint;
-  }
   return l;
 }
 
@@ -50,23 +42,16 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
   const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
   if (!l.spread) return hipErrorInvalidValue;  // phase 0 cannot have switched
   uint32_t* count = l.count(a.scratch);
-  if (hipError_t e = hipMemsetAsync(count, 0, 2 * sizeof(uint32_t), s)) return e;
+  if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
   const uint64_t entries = (uint64_t)a.nobj * l.units;
   const uint64_t lblocks = std::min<uint64_t>(1024, (entries + apply::kBlock - 1) / apply::kBlock);
   hipLaunchKernelGGL(redo_list_kernel<C>, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(apply::kBlock), 0, s,
                      l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
                      count);
   if (hipError_t e = hipGetLastError()) return e;
-  uint8_t* const bits = l.bits(a.scratch);
-  if (bits) {  // listed units: parity correction; the redo kernel then takes only edges and tails
-    hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C>), dim3(2048), dim3(apply::kBlock), 0, s, a.slots,
-                       a.slot_stride, chunk_stride(a), a.col0, a.rows, a.coeff, a.out_idx, a.mapping, bits,
-                       l.list(a.scratch), count, l.units, l.nint);
-    if (hipError_t e = hipGetLastError()) return e;
-  }
   hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(256), dim3(apply::kBlock), 0, s, a.slots,
                      a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
-                     a.flags, a.mapping, l.list(a.scratch), bits ? l.zero(a.scratch) : count, l.units);
+                     a.flags, a.mapping, l.list(a.scratch), count, l.units);
   return hipGetLastError();
 }
 
@@ -99,14 +84,13 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
   const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
   if (!l.spread) return hipSuccess;
   uint8_t* record = a.scratch ? l.record(a.scratch, a.nobj) : nullptr;
-  uint8_t* bits = a.scratch ? l.bits(a.scratch) : nullptr;
   const hipError_t e = with_tickets(
       s,
       [&](uint32_t* set) {
         hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(encode_queue_blocks<K, U, C>()),
                            dim3(apply::kBlock), 0, s,
                            a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
-                           a.flags, set, l.spread, record, l.units, bits);
+                           a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
       },
       launched);

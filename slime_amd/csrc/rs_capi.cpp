@@ -806,31 +806,6 @@ int slime_rs_kernel_schedule(int mode) {
   return 0;
 }
 
-// Top-bit parity correction of the mid-object switch (process-wide; env
-// SLIME_RS_SWITCH_BITS sets the initial value): 0 off, 1 on, 2 auto (default:
-// objects of kTopBitsAuto bytes or more).  The first pass then stores k bits
-// per column (k/32 of its read bytes) so that phase 1 corrects the parity of
-// the units encoded before an object's switch instead of re-encoding them.
-// For uniformly random bytes an object switches with probability
-// 1 - exp(-5 * ceil(S/4) / 2^32); the correction pays once
-// that exceeds about 10% (DESIGN "Top-bit correction"), i.e. from ~384 MiB.
-static constexpr uint64_t kTopBitsAuto = 384ull << 20;
-static std::atomic<int> g_switch_bits{[] {
-  const char* e = getenv("SLIME_RS_SWITCH_BITS");
-  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
-}()};
-static bool use_top_bits(uint64_t object_size) {
-  const int m = g_switch_bits.load(std::memory_order_relaxed);
-  return m == 1 || (m == 2 && object_size >= kTopBitsAuto);
-}
-
-int slime_rs_switch_bits(int mode) {
-  if (mode < 0) return g_switch_bits.load();
-  if (mode > 2) return fail(Status::InvalidArg, "switch_bits: mode must be 0 (off), 1 (on) or 2 (auto)");
-  g_switch_bits.store(mode);
-  return 0;
-}
-
 int slime_rs_ticket_sets(int device, uint64_t* sets, uint64_t* held) {
   if (!sets || !held) return fail(Status::InvalidArg, "ticket_sets: null output");
   if (int rc = check_device(device)) return rc;
@@ -1150,7 +1125,6 @@ extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* sl
   // runs (a scratch record of each unit's mapping), so phase 1 redoes only
   // the units encoded before an object's first word >= p was seen.
   BytesLaunch a0 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 0, status, mapping);
-  a0.topbits = use_top_bits(object_size);
   ScratchLease sc;
   if (int rc = sc.take(plan->device, encode_switch_bytes(a0, s), s)) return rc;
   bool switched = false;
@@ -1159,10 +1133,7 @@ extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* sl
   HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
   BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 1, status, mapping);
-  if (switched) {
-    a1.scratch = sc.ptr();
-    a1.topbits = a0.topbits;
-  }
+  if (switched) a1.scratch = sc.ptr();
   HIP_TRY(launch_encode_bytes(a1, s));
   sc.release(s);
   return 0;

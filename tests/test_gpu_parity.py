@@ -566,29 +566,17 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total
         assert ms[1] == 1 << 31
 
 
-@pytest.fixture(params=[0, 1], ids=["redo", "topbits"])
-def switch_bits(request):
-    """Phase 1 of a switched encode: re-encode the units an object encoded
-    before its switch (0) or correct their parity from the first pass's top
-    bits (1), selected process-wide by slime_rs_switch_bits."""
-    before = N.lib.slime_rs_switch_bits(-1)
-    assert N.lib.slime_rs_switch_bits(request.param) == 0
-    yield request.param
-    N.lib.slime_rs_switch_bits(before)
-
-
 @pytest.mark.parametrize("need,total,S,nobj", [(8, 12, 16 << 20, 12), (10, 14, (8 << 20) + 5, 12),
                                                (4, 6, (6 << 20) + 3, 18), (20, 24, (4 << 20) + 1, 6),
                                                (3, 5, 1 << 20, 36), (16, 20, (5 << 20) + 2, 6)])
-def test_encode_objects_mid_object_switch(torch_dev, switch_bits, need, total, S, nobj):
+def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
     """The dynamic-schedule encode switches an object to 1<<31 as soon as a
     word >= p has been seen and the second pass redoes only the units encoded
     before that (rs_bytes_kernel.hpp).  Objects with that word at the start,
     a quarter, half, 90 % and the last whole word, two such words, none, and
     one that needs the random fallback (a word >= p after a word 1<<31 cannot
     map); every chunk byte against the reference framing (map.go:15-67,
-    multi_store.go:526-554), the second pass re-encoding those units or
-    correcting their parity from the first pass's top bits."""
+    multi_store.go:526-554)."""
     torch = torch_dev
     from slime_amd import device as D
     assert N.lib.slime_rs_kernel_pipeline(-1) == 1 and N.lib.slime_rs_kernel_schedule(-1) == 1
@@ -717,7 +705,7 @@ def _make_chunked_slots(torch, objs, need, total, align):
 @pytest.mark.parametrize("need,total,S,nobj", [(8, 12, (2 << 20) + 5, 9), (4, 6, 4097, 5), (10, 14, 999999, 8),
                                                (16, 20, (1 << 20) + 3, 4), (20, 24, 300001, 3), (2, 3, 7, 3)])
 @pytest.mark.parametrize("align", [256, 4096])
-def test_objects_chunk_stride_layout(torch_dev, kernel_form, switch_bits, need, total, S, nobj, align):
+def test_objects_chunk_stride_layout(torch_dev, kernel_form, need, total, S, nobj, align):
     """encode/resolve/decode over a slot layout with padded chunk stride
     (slime_rs_*_objects_chunked): every chunk equals the reference framing
     (map.go:15-67, multi_store.go:526-554), the padding between chunks is

@@ -18,7 +18,7 @@ int launch(uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64
   const uint32_t units = apply::walk_units<C>(bytes::encode_interior_tiles(S, L, 0, L, K, U), spread);
   hipLaunchKernelGGL((bytes::encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(blocks), dim3(apply::kBlock),
                      0, s, slots, stride, L, cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket,
-                     spread, record, record ? units : 0u, (uint8_t*)nullptr);
+                     spread, record, record ? units : 0u);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace

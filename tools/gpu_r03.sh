@@ -73,18 +73,6 @@ for step in "$@"; do
              run cstride_c5_256 400 python bench.py --preset c5 --global-objects 16 --chunk-align 256 $NOLEGS &&
              run cstride_c2_256 400 python bench.py --preset c2 --chunk-align 256 $NOLEGS ;;
     bqv) run bqv 400 python tools/bytes_queue_variants.py --rounds 5 --blocks 256,512 ;;
-    tests_topbits) run pytest_topbits 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q -k "chunk_stride or encode_objects or decode_objects or bytes" --timeout 300 --timeout-method thread ;;
-    topbits) run tb_c5_auto 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
-             run tb_c5_off 400 env SLIME_RS_SWITCH_BITS=0 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
-             run tb_c3_on 400 env SLIME_RS_SWITCH_BITS=1 python bench.py $NOLEGS &&
-             run tb_c3_auto 400 python bench.py $NOLEGS &&
-             run tb_c5_auto2 400 python bench.py --preset c5 --global-objects 16 $NOLEGS ;;
-    tbprof) run tbprof_on 400 rocprofv3 --kernel-trace --stats -d "$OUT/tbprof_on" -o bench --output-format csv -- \
-            python3 bench.py --preset c5 --global-objects 16 --steps 5 --warmup 1 $NOLEGS &&
-            run tbprof_off 400 env SLIME_RS_SWITCH_BITS=0 rocprofv3 --kernel-trace --stats -d "$OUT/tbprof_off" -o bench --output-format csv -- \
-            python3 bench.py --preset c5 --global-objects 16 --steps 5 --warmup 1 $NOLEGS ;;
-    tbab) run tbab_c5 300 python tools/topbits_ab.py --preset c5 --rounds 8 &&
-          run tbab_c3 300 python tools/topbits_ab.py --preset c3 --rounds 6 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
