@@ -34,6 +34,33 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
   return l;
 }
 
+// Grid of the first pass and of the redo: two blocks per CU where the
+// kernel's registers allow two waves per SIMD (every need <= 16 form), else
+// one.  The second wave per SIMD covers the first's unit-start latency (flags
+// read, ticket draw, list entry): 512 blocks measured 1-4% faster than 256 for
+// the first pass at C3 and C5 and 3-4% for the redo (profiles/r03/s8_bqv/,
+// s14_redob/).
+template <typename Kernel>
+uint32_t two_per_cu(Kernel kernel) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), apply::kBlock, 0) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return n >= 2 ? 512u : 256u;
+}
+template <int K, int U, int C>
+uint32_t encode_queue_blocks() {
+  static const uint32_t blocks = two_per_cu(&encode_bytes_queue_kernel<K, U, C, kQueueCounters>);
+  return blocks;
+}
+template <int K, int U, int C>
+uint32_t redo_blocks() {
+  static const uint32_t blocks = two_per_cu(&encode_bytes_redo_kernel<K, U, C>);
+  return blocks;
+}
+
 // Phase 1 after a switched phase 0: build the redo list, then re-encode the
 // listed units plus the edge tiles and column tails of the objects mapped
 // with 1<<31.
@@ -49,30 +76,10 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
                      l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
                      count);
   if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(256), dim3(apply::kBlock), 0, s, a.slots,
-                     a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
-                     a.flags, a.mapping, l.list(a.scratch), count, l.units);
+  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(redo_blocks<K, U, C>()), dim3(apply::kBlock), 0, s,
+                     a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
+                     a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units);
   return hipGetLastError();
-}
-
-// Grid of the first pass: two blocks per CU where the kernel's registers
-// allow two waves per SIMD (every k <= 16 form), else one.  The second wave
-// per SIMD hides the unit-start latency (flags read, ticket draw) of the
-// first: 512 blocks measured 1-4% faster than 256 at C3 and C5
-// (profiles/r03/s8_bqv/).
-template <int K, int U, int C>
-uint32_t encode_queue_blocks() {
-  static const uint32_t blocks = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &n, reinterpret_cast<const void*>(&encode_bytes_queue_kernel<K, U, C, kQueueCounters>), apply::kBlock,
-            0) != hipSuccess) {
-      (void)hipGetLastError();
-      n = 1;
-    }
-    return n >= 2 ? 512u : 256u;
-  }();
-  return blocks;
 }
 
 // Phase 0 on the ticket walk (the mid-object switch when a.scratch is given).
@@ -88,8 +95,8 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       s,
       [&](uint32_t* set) {
         hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(encode_queue_blocks<K, U, C>()),
-                           dim3(apply::kBlock), 0, s,
-                           a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff, a.out_idx,
+                           dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols,
+                           a.S, a.nobj, a.rows, a.coeff, a.out_idx,
                            a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
       },

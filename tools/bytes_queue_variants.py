@@ -36,12 +36,18 @@ def main():
     ap.add_argument("--blocks", type=str, default="256")
     ap.add_argument("--shapes", type=str, default="c5,c3")
     ap.add_argument("--switch", type=str, default="0,1", help="0: no switch record; 1: the product's switching pass")
+    ap.add_argument("--redo-blocks", type=str, default="",
+                    help="instead: time the product's second pass (redo list + redo kernel) on these grids")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libbqvar.so"))
     lib.bqv_encode.restype = ctypes.c_int
     lib.bqv_encode.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32] + [ctypes.c_void_p] * 4 + \
         [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    lib.bqv_redo.restype = ctypes.c_int
+    lib.bqv_redo.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                             ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32] + [ctypes.c_void_p] * 7 + \
+        [ctypes.c_uint32, ctypes.c_void_p]
     s = torch.cuda.current_stream()
     ticket = torch.zeros(lib.bqv_ticket_words(), dtype=torch.int32, device="cuda")
     out = {}
@@ -74,6 +80,12 @@ def main():
             assert rc == 0, (v, rc)
             return a.elapsed_time(b)
 
+        if args.redo_blocks:
+            out[shape] = redo_ab(args, lib, s, ticket, shape, variants[0], slots, slot, cs, L, S, nobj, rows, c_t, oi,
+                                 flags, record, par, alg)
+            del slots, par
+            torch.cuda.empty_cache()
+            continue
         run(variants[0], 256)
         ref = par.clone()
         times = {}
@@ -96,6 +108,48 @@ def main():
         del slots, par, ref
         torch.cuda.empty_cache()
     print(json.dumps(out))
+
+
+def redo_ab(args, lib, s, ticket, shape, v, slots, slot, cs, L, S, nobj, rows, c_t, oi, flags, record, par, alg):
+    """First pass with the switch record (not timed), mapping selection as
+    select_mapping_kernel (rs_bytes.hip), then the second pass timed per grid;
+    the final chunks must not depend on the grid."""
+    status = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    mapping = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    lst = torch.zeros(nobj * (1 << 20) // 4, dtype=torch.int32, device="cuda")
+    count = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ref, times = None, {}
+    for r in range(args.rounds + 1):
+        for blocks in (int(x) for x in args.redo_blocks.split(",")):
+            flags.zero_()
+            rc = lib.bqv_encode(v, slots.data_ptr(), slot, cs, L, S, nobj, rows, c_t.data_ptr(), oi.data_ptr(),
+                                flags.data_ptr(), ticket.data_ptr(), 512, ctypes.c_void_p(record.data_ptr()),
+                                ctypes.c_void_p(s.cuda_stream))
+            assert rc == 0
+            f = flags
+            zero_ok, high_ok = (f & 1) == 0, (f & 2) == 0
+            mapping.copy_(torch.where(zero_ok, 0, torch.where(high_ok, -2**31, 0)).to(torch.int32))
+            status.copy_((~zero_ok & ~high_ok).to(torch.int32))
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            rc = lib.bqv_redo(v, slots.data_ptr(), slot, cs, L, S, nobj, rows, c_t.data_ptr(), oi.data_ptr(),
+                              mapping.data_ptr(), status.data_ptr(), record.data_ptr(), lst.data_ptr(), count.data_ptr(),
+                              blocks, ctypes.c_void_p(s.cuda_stream))
+            b.record(s)
+            torch.cuda.synchronize()
+            assert rc == 0
+            ok = (status == 0).nonzero().flatten()  # objects needing the random fallback are not final
+            if ref is None:
+                ref = par[ok].clone()
+            else:
+                assert torch.equal(par[ok], ref), (shape, blocks)
+            if r:
+                times.setdefault(f"redo b{blocks}", []).append(a.elapsed_time(b))
+    res = {"switched": int((mapping != 0).sum().item()), "listed_units": int(count.item())}
+    for k, ts in times.items():
+        res[k] = {"ms": round(statistics.median(ts), 4), "min_ms": round(min(ts), 4)}
+        print(f"{shape} {k}: {res[k]['ms']:.4f} ms", flush=True)
+    return res
 
 
 if __name__ == "__main__":
