@@ -756,6 +756,34 @@ def test_objects_chunk_stride_layout(torch_dev, kernel_form, need, total, S, nob
         assert torch.equal(slots, truth), erase
 
 
+def test_objects_chunk_stride_rejects_bad_layouts(torch_dev):
+    """The _chunked entry points refuse a chunk stride below 4L or not a
+    multiple of 4, and a slot stride that cannot hold total chunks at it
+    (SLIME_RS_ERR_INVALID_ARG, nothing launched); 0 is the wire layout."""
+    torch = torch_dev
+    import ctypes
+    from slime_amd import device as D
+    need, total, S, nobj = 4, 6, 4000, 2
+    L, _, _ = D.slot_geometry(S, need, total)
+    plan = D.Plan.encode(need, total)
+    cs = 4 * L + 256
+    slots = torch.zeros(nobj * total * cs, dtype=torch.uint8, device="cuda")
+    mapping = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    status = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    p, mp, sp = (ctypes.c_void_p(t.data_ptr()) for t in (slots, mapping, status))
+    enc = N.lib.slime_rs_encode_objects_chunked
+    for bad_cs, stride in ((4 * L - 4, total * cs), (4 * L + 2, total * cs), (cs, total * cs - 4)):
+        assert enc(plan._h, p, stride, bad_cs, S, nobj, mp, sp, None) == N.ERR_INVALID_ARG, (bad_cs, stride)
+        if bad_cs != cs:
+            assert N.lib.slime_rs_decode_objects_chunked(plan._h, p, stride, bad_cs, L, nobj, mp, None) == \
+                N.ERR_INVALID_ARG, bad_cs
+    assert enc(plan._h, p, total * cs, cs, S, nobj, mp, sp, None) == 0
+    assert enc(plan._h, p, total * cs, 0, S, nobj, mp, sp, None) == 0
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError):
+        D.encode_objects(plan, slots, total * cs, S, nobj, mapping, status, chunk_stride=4 * L - 4)
+
+
 # ------------------------------------------------- object entry points (host memory)
 
 def _obj_bytes(rng, S, kind):
