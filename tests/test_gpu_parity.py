@@ -260,6 +260,31 @@ def test_plan_encode_vs_oracle(torch_dev, need, total, L, nobj):
         assert np.array_equal(h[o], ref), o
 
 
+@pytest.mark.parametrize("need,total,L", [(8, 12, 1 << 20), (10, 14, 26843546 // 32), (4, 6, 99991)])
+def test_column_ranges_compose(torch_dev, need, total, L):
+    """one object split by column ranges [b0, b1) -- the
+    partition of a single huge object over GPUs, no exchange -- gives exactly
+    the whole-object launch: each range is the same layout at a column offset
+    with L = b1 - b0 (ranges of 1, odd and vector-multiple widths)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    nobj = 2
+    buf = _objects(torch, nobj, total, L, seed=L + need)
+    whole = buf.clone()
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    plan(whole, lay, whole, lay, L, nobj, dst_offset=need * L)
+    cuts = sorted({0, 1, 4 * 1000 + 3, L // 3, L // 2 + 1, L - 5, L})
+    for b0, b1 in zip(cuts, cuts[1:]):
+        plan(buf, lay, buf, lay, b1 - b0, nobj, src_offset=b0, dst_offset=need * L + b0)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, whole)
+    h = _host(buf, 1, total, L)[0]
+    ref = np.ascontiguousarray(h.copy())
+    OC.encode_object(ref, need, total)
+    assert np.array_equal(h, ref)
+
+
 @pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (20, 24)])
 @pytest.mark.parametrize("L", [4 * 262145, 4 * 262145 + 3])
 @pytest.mark.parametrize("align", [1, 64])
