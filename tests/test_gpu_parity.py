@@ -279,7 +279,7 @@ def test_column_ranges_compose(torch_dev, need, total, L):
         plan(buf, lay, buf, lay, b1 - b0, nobj, src_offset=b0, dst_offset=need * L + b0)
     torch.cuda.synchronize()
     assert torch.equal(buf, whole)
-    h = _host(buf, 1, total, L)[0]
+    h = _host(buf, nobj, total, L)[0]
     ref = np.ascontiguousarray(h.copy())
     OC.encode_object(ref, need, total)
     assert np.array_equal(h, ref)

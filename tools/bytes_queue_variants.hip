@@ -25,7 +25,8 @@ int launch(uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64
 
 // record: the mid-object switch's per-unit record (>= nobj x units bytes) or
 // null (mapping 0 throughout, as the capture form runs).
-// variant: 0 <8,2,3> (product), 1 <8,3,2>, 2 <8,4,2>, 3 <10,1,6> (product), 4 <10,2,3>, 5 <10,3,2>, 6 <8,1,6>
+// variant: 0 <8,2,3> (product), 1 <8,3,2>, 2 <8,4,2>, 3 <10,1,6> (product), 4 <10,2,3>, 5 <10,3,2>, 6 <8,1,6>,
+// 7 <4,2,3> (product), 8 <4,4,2>, 9 <4,3,2>
 extern "C" int bqv_encode(int variant, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S,
                           uint32_t nobj, uint32_t rows, const uint32_t* coeff, const uint32_t* out_idx,
                           uint32_t* flags, uint32_t* ticket, uint32_t blocks, uint8_t* record,
@@ -39,6 +40,9 @@ extern "C" int bqv_encode(int variant, uint8_t* slots, uint64_t stride, uint64_t
     case 4: return launch<10, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
     case 5: return launch<10, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
     case 6: return launch<8, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 7: return launch<4, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 8: return launch<4, 4, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
+    case 9: return launch<4, 3, 2>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, flags, ticket, blocks, record, s);
     default: return -3;
   }
 }

@@ -26,8 +26,10 @@ import torch  # noqa: E402
 from slime_amd import device as D  # noqa: E402
 
 NAMES = {0: "K8 U2 C3 (product)", 1: "K8 U3 C2", 2: "K8 U4 C2", 6: "K8 U1 C6",
-         3: "K10 U1 C6 (product)", 4: "K10 U2 C3", 5: "K10 U3 C2"}
-SHAPES = {"c3": (8, 12, 256, 128, 1, [0, 1, 2, 6]), "c5": (10, 14, 1024, 16, 256, [3, 4, 5])}
+         3: "K10 U1 C6 (product)", 4: "K10 U2 C3", 5: "K10 U3 C2", 7: "K4 U2 C3 (product)", 8: "K4 U4 C2",
+         9: "K4 U3 C2"}
+SHAPES = {"c3": (8, 12, 256, 128, 1, [0, 1, 2, 6]), "c5": (10, 14, 1024, 16, 256, [3, 4, 5]),
+          "c2": (4, 6, 64, 32, 1, [7, 8, 9])}
 
 
 def main():
