@@ -35,30 +35,36 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
 }
 
 // Grid of the first pass and of the redo: two blocks per CU where the
-// kernel's registers allow two waves per SIMD (every need <= 16 form), else
-// one.  The second wave per SIMD covers the first's unit-start latency (flags
-// read, ticket draw, list entry): 512 blocks measured 1-4% faster than 256 for
-// the first pass at C3 and C5 and 3-4% for the redo (profiles/r03/s8_bqv/,
-// s14_redob/).
+// kernel's registers allow two waves per SIMD (every need <= 16 form) and the
+// batch has at least 64 units per wave at that grid, else one.  The second
+// wave per SIMD covers the first's unit-start latency (flags read, ticket
+// draw, list entry): 512 blocks measured 1-4% faster than 256 for the first
+// pass at C3 and C5 (341 / 136 units per wave) and 3-4% for the redo, but 3.5%
+// slower at C2 (43 units per wave) (profiles/r03/s8_bqv/, s14_redob/,
+// s17_bqv_c2/).
 template <typename Kernel>
-uint32_t two_per_cu(Kernel kernel) {
+bool two_waves_per_simd(Kernel kernel) {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), apply::kBlock, 0) !=
       hipSuccess) {
     (void)hipGetLastError();
     n = 1;
   }
-  return n >= 2 ? 512u : 256u;
+  return n >= 2;
+}
+constexpr uint64_t kTwoBlockMinUnits = 64ull * 512 * apply::kWaves;
+inline uint32_t switch_grid(bool two_waves, uint64_t batch_units) {
+  return two_waves && batch_units >= kTwoBlockMinUnits ? 512u : 256u;
 }
 template <int K, int U, int C>
-uint32_t encode_queue_blocks() {
-  static const uint32_t blocks = two_per_cu(&encode_bytes_queue_kernel<K, U, C, kQueueCounters>);
-  return blocks;
+uint32_t encode_queue_blocks(uint64_t batch_units) {
+  static const bool two = two_waves_per_simd(&encode_bytes_queue_kernel<K, U, C, kQueueCounters>);
+  return switch_grid(two, batch_units);
 }
 template <int K, int U, int C>
-uint32_t redo_blocks() {
-  static const uint32_t blocks = two_per_cu(&encode_bytes_redo_kernel<K, U, C>);
-  return blocks;
+uint32_t redo_blocks(uint64_t batch_units) {
+  static const bool two = two_waves_per_simd(&encode_bytes_redo_kernel<K, U, C>);
+  return switch_grid(two, batch_units);
 }
 
 // Phase 1 after a switched phase 0: build the redo list, then re-encode the
@@ -70,14 +76,14 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
   if (!l.spread) return hipErrorInvalidValue;  // phase 0 cannot have switched
   uint32_t* count = l.count(a.scratch);
   if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
-  const uint64_t entries = (uint64_t)a.nobj * l.units;
-  const uint64_t lblocks = std::min<uint64_t>(1024, (entries + apply::kBlock - 1) / apply::kBlock);
+  const uint64_t batch_units = (uint64_t)a.nobj * l.units;
+  const uint64_t lblocks = std::min<uint64_t>(1024, (batch_units + apply::kBlock - 1) / apply::kBlock);
   hipLaunchKernelGGL(redo_list_kernel<C>, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(apply::kBlock), 0, s,
                      l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
                      count);
   if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(redo_blocks<K, U, C>()), dim3(apply::kBlock), 0, s,
-                     a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
+  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(redo_blocks<K, U, C>(batch_units)), dim3(apply::kBlock),
+                     0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                      a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units);
   return hipGetLastError();
 }
@@ -94,10 +100,10 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
   const hipError_t e = with_tickets(
       s,
       [&](uint32_t* set) {
-        hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), dim3(encode_queue_blocks<K, U, C>()),
-                           dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols,
-                           a.S, a.nobj, a.rows, a.coeff, a.out_idx,
-                           a.flags, set, l.spread, record, l.units);
+        hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>),
+                           dim3(encode_queue_blocks<K, U, C>((uint64_t)a.nobj * l.units)), dim3(apply::kBlock), 0, s,
+                           a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
+                           a.out_idx, a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
       },
       launched);
