@@ -276,16 +276,27 @@ NumaInfo numa_info(int device, const void* page) {
   return ni;
 }
 
+// Host pipeline depth: stages in flight per call (env SLIME_RS_HOST_STAGES,
+// 2..Workspace::kMaxStages, read once; default 3).
+int host_stages() {
+  static const int s = [] {
+    const char* e = getenv("SLIME_RS_HOST_STAGES");
+    const int v = e ? atoi(e) : 3;
+    return v < 2 ? 2 : v > 6 ? 6 : v;
+  }();
+  return s;
+}
+
 struct Workspace {
-  static constexpr int kStages = 3;  // host pipeline depth (host_apply)
+  static constexpr int kMaxStages = 6;
   int device = -1;
   hipStream_t stream = nullptr;
   uint8_t* dbuf = nullptr;
   size_t dcap = 0;
-  hipStream_t sst[kStages] = {};  // one stream per pipeline stage
-  hipEvent_t sev[kStages] = {};   // stage's D2H done
-  hipEvent_t cev = nullptr;       // compute stream reached a point (staged_d2h)
-  uint8_t* pin = nullptr;         // pinned staging, kStages x (in rows | out rows)
+  hipStream_t sst[kMaxStages] = {};  // one stream per pipeline stage
+  hipEvent_t sev[kMaxStages] = {};   // stage's D2H done
+  hipEvent_t cev = nullptr;          // compute stream reached a point (staged_d2h)
+  uint8_t* pin = nullptr;            // pinned staging, host_stages() x (in rows | out rows)
   size_t pcap = 0;
   int reserve(size_t bytes) {
     if (bytes <= dcap) return 0;
@@ -326,7 +337,7 @@ struct Workspace {
   int ensure_stages() {
     if (sst[0]) return 0;
     DeviceScope ds(device);
-    for (int i = 0; i < kStages; ++i) {
+    for (int i = 0; i < kMaxStages; ++i) {
       HIP_TRY(hipStreamCreateWithFlags(&sst[i], hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming));
     }
@@ -363,14 +374,23 @@ size_t round16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 // ---- host <-> device pipeline for the Go-API entry points ----------------------
 //
-// Column-chunked and kStages deep: chunk c's H2D / kernel / D2H run on stage
+// Column-chunked and host_stages() deep: chunk c's H2D / kernel / D2H run on stage
 // stream c % S while the host thread copies chunk c-S's results out of pinned
 // memory and chunk c's inputs into it (host_copy.cpp spreads those memcpys
 // over a small pool).  The caller's buffers stay pageable; only the staging
 // ring is pinned, so nothing is registered per call.
 
 constexpr size_t kStageBytes = 8u << 20;      // in + out bytes one stage moves (Go-API rows)
-constexpr size_t kObjStageBytes = 16u << 20;  // per window of the object entry points
+// Bytes one window of the object entry points moves (env
+// SLIME_RS_OBJ_WINDOW_MIB, 1..256, read once; default 16).
+size_t obj_window_bytes() {
+  static const size_t b = [] {
+    const char* e = getenv("SLIME_RS_OBJ_WINDOW_MIB");
+    const long v = e ? atol(e) : 16;
+    return (size_t)(v < 1 ? 1 : v > 256 ? 256 : v) << 20;
+  }();
+  return b;
+}
 
 enum class HostPipe : int { Staged = 0, Register = 1, Direct = 2 };
 
@@ -419,7 +439,7 @@ std::vector<Span> pieces_of(const Span* sp, size_t n) {
 }
 
 int stage_ring(Workspace* ws) {
-  if (int rc = ws->reserve_pinned(kStageBytes * Workspace::kStages)) return rc;
+  if (int rc = ws->reserve_pinned(kStageBytes * host_stages())) return rc;
   return ws->ensure_stages();
 }
 
@@ -428,7 +448,7 @@ int stage_ring(Workspace* ws) {
 int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
   if (int rc = stage_ring(ws)) return rc;
   const std::vector<Span> pcs = pieces_of(sp, n);
-  const int S = Workspace::kStages;
+  const int S = host_stages();
   HIP_TRY(hipEventRecord(ws->cev, ws->stream));
   for (int s = 0; s < S; ++s) HIP_TRY(hipStreamWaitEvent(ws->sst[s], ws->cev, 0));
   auto land = [&](size_t p) -> int {
@@ -550,7 +570,7 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t_start = clk::now();
   double t_in = 0, t_wait = 0, t_out = 0, t_enq = 0, t_h2d = 0, t_launch = 0;
-  const int S = (int)std::min<uint64_t>(Workspace::kStages, n);
+  const int S = (int)std::min<uint64_t>(host_stages(), n);
   if (int rc = ws->reserve_pinned(stage_bytes * S)) return rc;
   if (int rc = ws->ensure_stages()) return rc;
   std::vector<Window> win(S);
@@ -654,7 +674,7 @@ int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
   const uint64_t n = (L + cl - 1) / cl;
   const uint64_t rs = (cl + 63) & ~63ull;  // device row stride: 256 B aligned rows (line-aligned streams)
   const size_t stage_dev = (size_t)(nin + nout) * rs * 4;
-  if (int rc = ws->reserve(stage_dev * std::min<uint64_t>(Workspace::kStages, n))) return rc;
+  if (int rc = ws->reserve(stage_dev * std::min<uint64_t>(host_stages(), n))) return rc;
   uint8_t* const dev = ws->dbuf;
   return run_windows(
       "rows", ws, dev, n, (size_t)(nin + nout) * round64(rs * 4),
@@ -698,7 +718,7 @@ int host_apply_registered(Workspace* ws, const slime_rs_plan* plan, const uint32
   uint64_t cl = std::max<uint64_t>(4 * kStageBytes / ((nin + nout) * 4), 4096) & ~4095ull;
   if (cl >= L) cl = (L + 63) & ~63ull;  // row stride: 256 B aligned
   const uint64_t nch = (L + cl - 1) / cl;
-  const int S = (int)std::min<uint64_t>(Workspace::kStages, nch);
+  const int S = (int)std::min<uint64_t>(host_stages(), nch);
   const size_t stage_words = (size_t)(nin + nout) * cl;
   int rc = ws->reserve(stage_words * 4 * S);
   if (!rc) rc = ws->ensure_stages();
@@ -1754,7 +1774,7 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
   // MapToGF(x)) = x, map.go:15-33,103-113) and are placed on the host with
   // each window's inputs.  The device computes every byte that depends on m.
   const int r = total - need;
-  const uint64_t cl = window_cols(L, (uint64_t)total, kObjStageBytes);
+  const uint64_t cl = window_cols(L, (uint64_t)total, obj_window_bytes());
   const uint64_t nwin = (L + cl - 1) / cl;
   auto body = [&]() -> int {
     HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
@@ -1890,7 +1910,7 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   uint32_t* const d_map = (uint32_t*)(ws->dbuf + round16(stride));
   // Window by window: survivors' columns in, all need data rows decoded,
   // the object's bytes of those columns out.
-  const uint64_t cl = window_cols(L, 2 * (uint64_t)need, kObjStageBytes);
+  const uint64_t cl = window_cols(L, 2 * (uint64_t)need, obj_window_bytes());
   const uint64_t nwin = (L + cl - 1) / cl;
   auto body = [&]() -> int {
     HIP_TRY(hipMemcpyAsync(d_map, &mapping, 4, hipMemcpyHostToDevice, ws->stream));

@@ -80,6 +80,9 @@ for step in "$@"; do
     c2trace) run c2trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/c2trace" -o bench --output-format csv -- \
             python3 bench.py --preset c2 --steps 20 --warmup 2 $NOLEGS --bytes-path 0 ;;
     bqv_c2) run bqv_c2 300 python tools/bytes_queue_variants.py --shapes c2 --rounds 8 --blocks 256,512 ;;
+    hostsweep) for W in 16 8 4 32; do for S in 3 4 6; do
+                 run hs_w${W}_s${S} 120 env SLIME_RS_OBJ_WINDOW_MIB=$W SLIME_RS_HOST_STAGES=$S python tools/host_trace.py --reps 10 || exit $?
+               done; done ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
