@@ -148,13 +148,17 @@ def _oracle_chunks_threaded(obj: bytes, need: int, total: int, cands=()):
     return m, [OC.map_from_gf(m, p) for p in parts + parity]
 
 
-def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None):
+def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None, align=1):
     """Objects at[0] (uniform random) and at[1] (forced to mapping 1<<31) of an
     nobj-object batch, every chunk byte against the oracle's framing; the
-    other objects are random bytes drawn on the device."""
+    other objects are random bytes drawn on the device.  align > 1: chunks
+    `cs` = roundup(4L, align) apart (the _chunked entry points), object byte i
+    at chunk i // 4L, offset i % 4L."""
     from slime_amd import device as D
     S = mib << 20
-    L, chunk, slot = D.slot_geometry(S, need, total)
+    L, cs, slot = D.slot_geometry(S, need, total, chunk_align=align)
+    chunk = 4 * L
+    cstride = cs if align > 1 else 0
     rng = np.random.default_rng(mib * 131 + need)
     objs = [rng.integers(0, 256, size=S, dtype=np.uint8) for _ in range(2)]
     # at[1]: a word >= p and no word that 1<<31 would map to >= p, so MapToGF
@@ -170,22 +174,25 @@ def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None):
         gen = torch.Generator(device="cuda").manual_seed(mib + nobj)
         slots = torch.randint(0, 256, (nobj * slot,), dtype=torch.uint8, device="cuda", generator=gen)
     for i, o in enumerate(at):
-        if slots is None:
-            host[o * slot: o * slot + S] = objs[i]
-        else:
-            slots[o * slot: o * slot + S].copy_(torch.from_numpy(objs[i]))
+        for j in range(need):  # data chunk j: object bytes [4jL, 4(j+1)L) at slot + j*cs
+            part = objs[i][j * chunk: (j + 1) * chunk]
+            at_ = o * slot + j * cs
+            if slots is None:
+                host[at_: at_ + part.size] = part
+            else:
+                slots[at_: at_ + part.size].copy_(torch.from_numpy(part))
     if slots is None:
         slots = torch.from_numpy(host).cuda()
         del host
     enc = D.Plan.encode(need, total)
     mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
     status = torch.empty(nobj, dtype=torch.int32, device="cuda")
-    D.encode_objects(enc, slots, slot, S, nobj, mapping, status)
+    D.encode_objects(enc, slots, slot, S, nobj, mapping, status, chunk_stride=cstride)
     torch.cuda.synchronize()
     st = status.cpu().numpy().tolist()
     assert st[at[1]] == 0
     if any(st):  # MapToGF's random fallback (map.go:64-66): resolved on the device
-        assert D.resolve_fallbacks(enc, slots, slot, S, nobj, mapping, status) == sum(st)
+        assert D.resolve_fallbacks(enc, slots, slot, S, nobj, mapping, status, chunk_stride=cstride) == sum(st)
     ms = mapping.cpu().numpy().view(np.uint32).tolist()
     truth = {}
     for i, o in enumerate(at):
@@ -194,7 +201,7 @@ def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None):
         assert ms[o] == m, o
         got = slots[o * slot: (o + 1) * slot].cpu().numpy()
         for c in range(total):
-            assert got[c * chunk:(c + 1) * chunk].tobytes() == want[c], (o, c)
+            assert got[c * cs: c * cs + chunk].tobytes() == want[c], (o, c)
         if i == 1:
             assert m == 1 << 31
         truth[o] = want
@@ -202,14 +209,14 @@ def _bytes_case(torch, need, total, mib, nobj=2, at=(0, 1), erasures=None):
     for erase in erasures or ([0, 1, 2, 3], [0, 3, need, total - 1]):
         have = [i for i in range(total) if i not in erase][:need]
         rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
-        v = slots.view(nobj, slot)[:, : total * chunk].view(nobj, total, chunk)
-        v[:, erase, :] = 0x5A
-        D.decode_objects(rec, slots, slot, L, nobj, mapping)
+        v = slots.view(nobj, slot)[:, : total * cs].view(nobj, total, cs)
+        v[:, erase, :chunk] = 0x5A
+        D.decode_objects(rec, slots, slot, L, nobj, mapping, chunk_stride=cstride)
         torch.cuda.synchronize()
         for o in at:
             got = slots[o * slot: (o + 1) * slot].cpu().numpy()
             for c in erase:
-                assert got[c * chunk:(c + 1) * chunk].tobytes() == truth[o][c], (o, erase, c)
+                assert got[c * cs: c * cs + chunk].tobytes() == truth[o][c], (o, erase, c)
     del slots
     torch.cuda.empty_cache()
 
@@ -220,6 +227,13 @@ def test_c3_bytes_every_byte_vs_oracle(torch_dev):
 
 def test_c5_bytes_every_byte_vs_oracle(torch_dev):
     _bytes_case(torch_dev, 10, 14, 1024)
+
+
+def test_c5_bytes_aligned_chunks_every_byte_vs_oracle(torch_dev):
+    """The bench's byte-path layout at C5: 16 x 1 GiB objects on 256 B-aligned
+    chunk strides (4L = 107,374,184 B -> 107,374,336), objects 3 (random) and
+    11 (1<<31) of the batch, every byte of encode and both repairs."""
+    _bytes_case(torch_dev, 10, 14, 1024, nobj=16, at=(3, 11), align=256)
 
 
 def test_c2_bytes_every_byte_vs_oracle(torch_dev):
