@@ -346,6 +346,8 @@ extern "C" int av_launch_queue(int C, int k, const uint32_t* in, uint32_t* out, 
   QU(4, 5, 1, 8, 1) QU(4, 6, 1, 8, 1) QU(4, 6, 2, 8, 1) QU(4, 8, 1, 8, 1) QU(4, 4, 1, 8, 1)
   // k = 8: U = 4, 2
   QU(8, 4, 2, 8, 1) QU(8, 4, 1, 8, 1) QU(8, 2, 3, 8, 1) QU(8, 2, 2, 8, 1) Q(8, 3, 8, 1)
+  // k = 10 (C5): U = 2, 1 (no AGPRs: the U = 3 form holds 256 VGPRs + 14 AGPRs)
+  QU(10, 2, 3, 8, 1) QU(10, 2, 2, 8, 1) QU(10, 1, 6, 8, 1)
   // k = 16: U = 1, 2
   QU(16, 1, 6, 8, 1) QU(16, 1, 12, 8, 1) QU(16, 2, 3, 8, 1)
 #undef Q

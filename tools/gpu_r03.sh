@@ -83,6 +83,8 @@ for step in "$@"; do
     hostsweep) for W in 16 8 4 32; do for S in 3 4 6; do
                  run hs_w${W}_s${S} 120 env SLIME_RS_OBJ_WINDOW_MIB=$W SLIME_RS_HOST_STAGES=$S python tools/host_trace.py --reps 10 || exit $?
                done; done ;;
+    c5u) run c5u_enc 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --pad 38 --variants 13 --blocks 256,512 --nseg 4 --rounds 5 --queue 802,200803,200802,100806 &&
+         run c5u_dec 300 python tools/apply_variants.py --need 10 --total 14 --mib 1024 --nobj 16 --pad 38 --decode 1 --separate 0 --variants 13 --blocks 256,512 --nseg 4 --rounds 5 --queue 802,200803,200802,100806 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
