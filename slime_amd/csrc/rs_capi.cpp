@@ -26,6 +26,7 @@
 #include <tuple>
 #include <vector>
 
+#include "capi_common.hpp"
 #include "device_pool.hpp"
 #include "digest.hpp"
 #include "gfp_host.hpp"
@@ -51,7 +52,6 @@ struct slime_rs_plan {
 
 namespace slime {
 namespace {
-
 thread_local std::string t_error;
 // Device of the calling thread's host entry points after
 // slime_rs_select_device (-1: not selected, the device pool picks).
@@ -60,7 +60,9 @@ thread_local int t_device = -1;
 // buffer), active for the duration of that one call on this thread.
 thread_local const slime_rs_call_t* t_call = nullptr;
 std::atomic<int64_t> g_tables_live{0};  // device plan tables allocated and not yet freed
+}  // namespace
 
+// capi_common.hpp
 int fail(Status st, std::string detail) {
   t_error = std::move(detail);
   return (int)st;
@@ -68,11 +70,6 @@ int fail(Status st, std::string detail) {
 int fail_hip(hipError_t e, const char* what) {
   return fail(Status::Hip, std::string(what) + ": " + hipGetErrorString(e));
 }
-#define HIP_TRY(expr)                                   \
-  do {                                                  \
-    const hipError_t e_ = (expr);                       \
-    if (e_ != hipSuccess) return fail_hip(e_, #expr);   \
-  } while (0)
 
 int visible_devices() {
   static const int n = [] {
@@ -91,19 +88,7 @@ int check_device(int dev) {
   return 0;
 }
 
-// Switch the calling thread to `dev` for the scope, restoring its previous device.
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceScope() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
+namespace {
 // ---- device pool (host entry points) -------------------------------------------
 // Routing policy and its CPU test: device_pool.hpp.  Each device has its own
 // workspaces and plans (plan keys and workspaces carry the device).
@@ -1283,244 +1268,6 @@ int slime_rs_fill_symbols(int device, uint32_t* dst, uint64_t count, uint64_t se
   if (int rc = check_device(device)) return rc;
   DeviceScope ds(device);
   HIP_TRY(launch_fill_symbols(dst, count, seed, (hipStream_t)stream));
-  return 0;
-}
-
-// ---- device batch buffers (HIP virtual memory) ------------------------------------
-// A buffer is `n` physical chunks (hipMemCreate) mapped in order into one
-// reserved virtual range, or (a probed alternative) one hipMalloc.
-// Registry: base -> buffer, for slime_rs_device_free and _info.
-}  // extern "C"
-namespace {
-struct DevBuffer {
-  int device = 0;
-  uint64_t bytes = 0, chunk = 0;  // chunk 0: hipMalloc
-  std::vector<hipMemGenericAllocationHandle_t> handles;
-  slime_rs_alloc_info_t info = {};
-};
-std::mutex g_vmm_mu;
-std::map<void*, DevBuffer>& dev_buffers() {
-  static auto* m = new std::map<void*, DevBuffer>();
-  return *m;
-}
-uint64_t vmm_chunk_bytes() {
-  static const uint64_t c = [] {
-    const char* e = getenv("SLIME_RS_VMM_CHUNK_MIB");
-    const long long v = e ? atoll(e) : 0;
-    return (uint64_t)(v > 0 ? v : 2) << 20;
-  }();
-  return c;
-}
-double env_double(const char* name, double dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atof(e) : dflt;
-}
-// Unmaps and releases the first `mapped` / `created` chunks, frees the range.
-void vmm_unwind(void* va, uint64_t bytes, uint64_t chunk, const std::vector<hipMemGenericAllocationHandle_t>& h,
-                size_t created, size_t mapped) {
-  for (size_t i = 0; i < mapped; ++i) (void)hipMemUnmap((char*)va + i * chunk, chunk);
-  for (size_t i = 0; i < created; ++i) (void)hipMemRelease(h[i]);
-  (void)hipMemAddressFree(va, bytes);
-}
-void release_buffer(void* va, const DevBuffer& b) {
-  if (b.chunk == 0)
-    (void)hipFree(va);
-  else
-    vmm_unwind(va, b.bytes, b.chunk, b.handles, b.handles.size(), b.handles.size());
-}
-
-// `bytes` as physical chunks of `chunk` bytes mapped in order (chunk 0:
-// hipMalloc).  The current device is `device`.
-int map_buffer(int device, uint64_t bytes, uint64_t chunk, void** va_out, DevBuffer* out) {
-  out->device = device;
-  if (chunk == 0) {
-    void* p = nullptr;
-    HIP_TRY(hipMalloc(&p, bytes));
-    out->bytes = bytes;
-    out->chunk = 0;
-    *va_out = p;
-    return 0;
-  }
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = device;
-  size_t gran = 0;
-  HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
-  if (gran && chunk % gran) chunk = (chunk + gran - 1) / gran * gran;
-  const uint64_t total = (bytes + chunk - 1) / chunk * chunk;
-  const size_t n = (size_t)(total / chunk);
-  void* va = nullptr;
-  HIP_TRY(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
-  std::vector<hipMemGenericAllocationHandle_t> h(n);
-  for (size_t i = 0; i < n; ++i) {
-    if (hipError_t e = hipMemCreate(&h[i], chunk, &prop, 0)) {
-      vmm_unwind(va, total, chunk, h, i, i);
-      return fail(Status::Hip, std::string("device_alloc: hipMemCreate: ") + hipGetErrorString(e));
-    }
-    if (hipError_t e = hipMemMap((char*)va + i * chunk, chunk, 0, h[i], 0)) {
-      vmm_unwind(va, total, chunk, h, i + 1, i);
-      return fail(Status::Hip, std::string("device_alloc: hipMemMap: ") + hipGetErrorString(e));
-    }
-  }
-  hipMemAccessDesc acc = {};
-  acc.location = prop.location;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  if (hipError_t e = hipMemSetAccess(va, total, &acc, 1)) {
-    vmm_unwind(va, total, chunk, h, n, n);
-    return fail(Status::Hip, std::string("device_alloc: hipMemSetAccess: ") + hipGetErrorString(e));
-  }
-  out->bytes = total;
-  out->chunk = chunk;
-  out->handles = std::move(h);
-  *va_out = va;
-  return 0;
-}
-
-// The placement probe: the product apply kernel's C3-shaped walk (8 data
-// shards in, 4 parity shards out, 128 objects) over the whole fresh buffer,
-// one warm launch and two timed ones on a private stream; GB/s of
-// algorithmic traffic of the faster timed launch (0: not measurable).  The
-// slow placement mode follows a buffer's physical memory for its whole life
-// and shows up in exactly this many-stream read/write mix (DESIGN.md
-// "Placement modes"); the buffer's contents are garbage either way.
-double placement_probe(int device, uint8_t* va, uint64_t bytes) {
-  constexpr uint32_t kNeed = 8, kTotal = 12, kRows = kTotal - kNeed, kObj = 128;
-  const uint64_t L = (bytes / 4 / kTotal / kObj) & ~(uint64_t)63;
-  if (L < 65536) return 0;
-  std::vector<uint32_t> table(kRows * 16 + 16, 0);
-  for (uint32_t i = 0; i < kRows; ++i)
-    for (uint32_t j = 0; j < kNeed; ++j) table[i * 16 + j] = 0x9E3779B9u * (i * kNeed + j + 1) % kP;
-  for (uint32_t j = 0; j < kNeed; ++j) table[kRows * 16 + j] = j;
-  for (uint32_t i = 0; i < kRows; ++i) table[kRows * 16 + 8 + i] = kNeed + i;
-  uint32_t* d = nullptr;
-  if (hipMalloc((void**)&d, table.size() * 4) != hipSuccess) return 0;
-  hipStream_t s = nullptr;
-  hipEvent_t ev[3] = {};
-  double best = 0;
-  bool ok = hipMemcpy(d, table.data(), table.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-            hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
-  for (auto& e : ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-  if (ok) {
-    ApplyLaunch a;
-    a.in = (const uint32_t*)va;
-    a.out = (uint32_t*)va;
-    a.in_obj_stride = a.out_obj_stride = kTotal * L;
-    a.in_shard_stride = a.out_shard_stride = L;
-    a.coeff = d;
-    a.in_idx = d + kRows * 16;
-    a.out_idx = d + kRows * 16 + 8;
-    a.ncols = L;
-    a.nobj = kObj;
-    a.rows = kRows;
-    a.k = kNeed;
-    a.vec_ok = true;
-    ok = launch_apply(a, s) == hipSuccess && hipEventRecord(ev[0], s) == hipSuccess &&
-         launch_apply(a, s) == hipSuccess && hipEventRecord(ev[1], s) == hipSuccess &&
-         launch_apply(a, s) == hipSuccess && hipEventRecord(ev[2], s) == hipSuccess &&
-         hipStreamSynchronize(s) == hipSuccess;
-    float ms[2] = {0, 0};
-    if (ok && hipEventElapsedTime(&ms[0], ev[0], ev[1]) == hipSuccess &&
-        hipEventElapsedTime(&ms[1], ev[1], ev[2]) == hipSuccess) {
-      const double t = std::min(ms[0], ms[1]) * 1e-3;
-      if (t > 0) best = (double)kObj * 4.0 * L * kTotal / t / 1e9;
-    }
-  }
-  if (!ok) (void)hipGetLastError();
-  for (auto& e : ev)
-    if (e) (void)hipEventDestroy(e);
-  if (s) (void)hipStreamDestroy(s);
-  (void)hipFree(d);
-  return best;
-}
-}  // namespace
-extern "C" {
-
-// Placement: a buffer of at least SLIME_RS_PLACEMENT_PROBE_GIB (default 16)
-// is probed once created (placement_probe).  Below SLIME_RS_PLACEMENT_MIN_GBS
-// (default 6100: the C3 apply kernel at <= 8.45 ms) the library tries the
-// other placements -- 1 GiB chunks, then one hipMalloc -- while still holding
-// the first, while the device has room for both, and keeps the fastest.
-int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
-  if (!ptr || bytes == 0) return fail(Status::InvalidArg, "device_alloc: null ptr or zero bytes");
-  *ptr = nullptr;
-  if (int rc = check_device(device)) return rc;
-  DeviceScope ds(device);
-  void* va = nullptr;
-  DevBuffer best;
-  if (int rc = map_buffer(device, bytes, vmm_chunk_bytes(), &va, &best)) return rc;
-  const double probe_gib = env_double("SLIME_RS_PLACEMENT_PROBE_GIB", 16.0);
-  slime_rs_alloc_info_t& info = best.info;
-  info.kind = 0;
-  info.chunk_bytes = best.chunk;
-  if (probe_gib > 0 && (double)bytes >= probe_gib * (1ull << 30)) {
-    const double want = env_double("SLIME_RS_PLACEMENT_MIN_GBS", 6100.0);
-    double best_gbs = placement_probe(device, (uint8_t*)va, bytes);
-    info.probe_gbs[0] = best_gbs;
-    info.probe_chunk[0] = best.chunk;
-    info.probes = 1;
-    const uint64_t alts[2] = {1ull << 30, 0};  // 1 GiB chunks, then hipMalloc
-    for (uint64_t alt : alts) {
-      if (best_gbs <= 0 || best_gbs >= want || alt == best.chunk) continue;
-      size_t free_b = 0, total_b = 0;
-      if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (2ull << 30)) break;
-      void* va2 = nullptr;
-      DevBuffer cand;
-      if (map_buffer(device, bytes, alt, &va2, &cand) != 0) {
-        (void)hipGetLastError();
-        break;
-      }
-      const double gbs = placement_probe(device, (uint8_t*)va2, bytes);
-      const int idx = info.probes++;
-      info.probe_gbs[idx] = gbs;
-      info.probe_chunk[idx] = alt;
-      if (gbs > best_gbs) {  // keep the new placement, release the old one
-        release_buffer(va, best);
-        const slime_rs_alloc_info_t keep = info;
-        best = std::move(cand);
-        best.info = keep;
-        best.info.chosen = idx;
-        best.info.kind = alt ? 0 : 1;
-        best.info.chunk_bytes = alt;
-        va = va2;
-        best_gbs = gbs;
-      } else {
-        release_buffer(va2, cand);
-      }
-    }
-  }
-  {
-    std::lock_guard<std::mutex> lock(g_vmm_mu);
-    dev_buffers()[va] = std::move(best);
-  }
-  *ptr = va;
-  return 0;
-}
-
-int slime_rs_device_alloc_info(const void* ptr, slime_rs_alloc_info_t* info) {
-  if (!info) return fail(Status::InvalidArg, "device_alloc_info: null info");
-  std::lock_guard<std::mutex> lock(g_vmm_mu);
-  auto it = dev_buffers().find(const_cast<void*>(ptr));
-  if (it == dev_buffers().end()) return fail(Status::InvalidArg, "device_alloc_info: not a slime_rs_device_alloc base");
-  *info = it->second.info;
-  return 0;
-}
-
-int slime_rs_device_free(void* ptr) {
-  DevBuffer b;
-  {
-    std::lock_guard<std::mutex> lock(g_vmm_mu);
-    auto it = dev_buffers().find(ptr);
-    if (it == dev_buffers().end()) return fail(Status::InvalidArg, "device_free: not a slime_rs_device_alloc base");
-    b = std::move(it->second);
-    dev_buffers().erase(it);
-  }
-  DeviceScope ds(b.device);
-  // Work still queued on any stream may touch the range (a tensor dropped right
-  // after an asynchronous launch): wait for the device before unmapping.
-  const hipError_t e = hipDeviceSynchronize();
-  release_buffer(ptr, b);
-  if (e != hipSuccess) return fail(Status::Hip, std::string("device_free: hipDeviceSynchronize: ") + hipGetErrorString(e));
   return 0;
 }
 
