@@ -34,37 +34,20 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
   return l;
 }
 
-// Grid of the first pass and of the redo: two blocks per CU where the
-// kernel's registers allow two waves per SIMD (every need <= 16 form) and the
-// batch has at least 64 units per wave at that grid, else one.  The second
-// wave per SIMD covers the first's unit-start latency (flags read, ticket
-// draw, list entry): 512 blocks measured 1-4% faster than 256 for the first
-// pass at C3 and C5 (341 / 136 units per wave) and 3-4% for the redo, but 3.5%
-// slower at C2 (43 units per wave) (profiles/r03/s8_bqv/, s14_redob/,
-// s17_bqv_c2/).
-template <typename Kernel>
-bool two_waves_per_simd(Kernel kernel) {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), apply::kBlock, 0) !=
-      hipSuccess) {
-    (void)hipGetLastError();
-    n = 1;
-  }
-  return n >= 2;
-}
+// Grid of the first pass and of the redo: two blocks per CU for the need <=
+// 16 forms, whose registers allow two waves per SIMD (at most 250 VGPRs, no
+// AGPRs: -Rpass-analysis=kernel-resource-usage), when the batch has at least
+// 64 units per wave at that grid; else one.  The second wave per SIMD covers
+// the first's unit-start latency (flags read, ticket draw, list entry): 512
+// blocks measured 1-4% faster than 256 for the first pass at C3 and C5 (341 /
+// 136 units per wave) and 3-4% for the redo, but 3.5% slower at C2 (43 units
+// per wave) (profiles/r03/s8_bqv/, s14_redob/, s17_bqv_c2/).  A compile-time
+// rule rather than an occupancy query: the first launch may be inside a graph
+// capture.
 constexpr uint64_t kTwoBlockMinUnits = 64ull * 512 * apply::kWaves;
-inline uint32_t switch_grid(bool two_waves, uint64_t batch_units) {
-  return two_waves && batch_units >= kTwoBlockMinUnits ? 512u : 256u;
-}
-template <int K, int U, int C>
-uint32_t encode_queue_blocks(uint64_t batch_units) {
-  static const bool two = two_waves_per_simd(&encode_bytes_queue_kernel<K, U, C, kQueueCounters>);
-  return switch_grid(two, batch_units);
-}
-template <int K, int U, int C>
-uint32_t redo_blocks(uint64_t batch_units) {
-  static const bool two = two_waves_per_simd(&encode_bytes_redo_kernel<K, U, C>);
-  return switch_grid(two, batch_units);
+template <int K>
+uint32_t switch_grid(uint64_t batch_units) {
+  return K <= 16 && batch_units >= kTwoBlockMinUnits ? 512u : 256u;
 }
 
 // Phase 1 after a switched phase 0: build the redo list, then re-encode the
@@ -82,7 +65,7 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
                      l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
                      count);
   if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(redo_blocks<K, U, C>(batch_units)), dim3(apply::kBlock),
+  hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock),
                      0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                      a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units);
   return hipGetLastError();
@@ -101,7 +84,7 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       s,
       [&](uint32_t* set) {
         hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>),
-                           dim3(encode_queue_blocks<K, U, C>((uint64_t)a.nobj * l.units)), dim3(apply::kBlock), 0, s,
+                           dim3(switch_grid<K>((uint64_t)a.nobj * l.units)), dim3(apply::kBlock), 0, s,
                            a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                            a.out_idx, a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
