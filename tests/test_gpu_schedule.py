@@ -205,6 +205,62 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
             assert np.array_equal(r[:, i], (ref[:, t].astype(np.uint64) % P).astype(np.uint32)), t
 
 
+def test_graph_captured_byte_path_replays_exactly(torch_dev):
+    """The fused byte path captured into a graph: encode_objects (no scratch
+    inside a capture, so no mid-object switch: objects mapped with 1<<31 are
+    re-encoded whole) and decode_objects on 256 B chunk strides, replayed three
+    times over fresh objects, each time equal to the uncaptured calls."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, nobj, S = 10, 14, 6, (24 << 20) + 5
+    L, cs, slot = D.slot_geometry(S, need, total, chunk_align=256)
+    erase = [0, 3, 10, 13]
+    have = [i for i in range(total) if i not in erase][:need]
+    enc = D.Plan.encode(need, total)
+    rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+    slots = torch.zeros(nobj * slot, dtype=torch.uint8, device="cuda")
+    mapping = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    status = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    chunks = slots.view(nobj, total, cs)[:, :, : 4 * L]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+
+    def fill(seed):
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        slots.copy_(torch.randint(0, 256, slots.shape, dtype=torch.uint8, device="cuda", generator=g))
+        words = chunks[:, :need].view(torch.int32)
+        words[1:3] &= 0x7F7F7F7F  # objects 1 and 2: every word below 2^31 (mapping 0)
+        slots.view(nobj, slot)[2, :4] = torch.tensor([255, 255, 255, 253], dtype=torch.uint8)  # 2: now 1<<31
+
+    def calls():
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, s, cs)
+        chunks[:, erase] = 0x5A
+        D.decode_objects(rec, slots, slot, L, nobj, mapping, s, cs)
+
+    with torch.cuda.stream(s):
+        fill(1)
+        calls()  # warm the launch paths outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        calls()
+    for seed in (2, 3, 4):
+        with torch.cuda.stream(s):
+            fill(seed)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        got, gm, gs = chunks.clone(), mapping.clone(), status.clone()
+        with torch.cuda.stream(s):
+            fill(seed)
+            calls()
+        torch.cuda.synchronize()
+        ok = (status == 0).nonzero().flatten()
+        assert torch.equal(gs, status) and torch.equal(gm, mapping), seed
+        assert int(mapping[2]) == -2**31
+        assert torch.equal(got[ok], chunks[ok]), seed
+
+
 HIP_STREAM_PER_THREAD = 2  # (hipStream_t)2, hip_runtime_api.h
 
 
