@@ -234,7 +234,8 @@ def test_graph_captured_byte_path_replays_exactly(torch_dev):
 
     def calls():
         D.encode_objects(enc, slots, slot, S, nobj, mapping, status, s, cs)
-        chunks[:, erase] = 0x5A
+        for e in erase:  # basic slices: a fill kernel, capturable (a list index would upload it)
+            chunks[:, e].fill_(0x5A)
         D.decode_objects(rec, slots, slot, L, nobj, mapping, s, cs)
 
     with torch.cuda.stream(s):
