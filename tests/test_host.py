@@ -340,3 +340,25 @@ def test_bench_rejects_impossible_erasures():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--need", "17", "--total", "20",
                         "--erase", "0,1,2,3"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 2
+
+
+def test_slot_geometry_chunk_strides():
+    """Slot layouts of the fused byte path (device.slot_geometry): the wire
+    layout (chunks 4L apart, L = ceil(ceil(S/4)/need), multi_store.go:272)
+    and padded chunk strides; bad alignments and strides are refused before
+    any C call."""
+    from slime_amd import device as D
+    for S, need, total in [(1, 2, 3), (4097, 4, 6), (1 << 30, 10, 14), (3 * (1 << 20) + 7, 8, 12)]:
+        L = -(-(-(-S // 4)) // need)
+        assert D.slot_geometry(S, need, total) == (L, 4 * L, 4 * L * total)
+        for align in (4, 16, 256, 4096):
+            Lg, cs, slot = D.slot_geometry(S, need, total, chunk_align=align)
+            assert Lg == L and cs % align == 0 and 4 * L <= cs < 4 * L + align and slot == cs * total
+    assert D.slot_geometry(1 << 30, 10, 14, chunk_align=256)[1] == 107374336  # C5: 4L = 107,374,184
+    for bad in (0, 2, 6, -4):
+        with pytest.raises(ValueError):
+            D.slot_geometry(4097, 4, 6, chunk_align=bad)
+    assert D._chunk_stride(1025, 0) == 4100 and D._chunk_stride(1025, 4352) == 4352
+    for bad in (4096, 4102):  # below 4L, not a multiple of 4
+        with pytest.raises(ValueError):
+            D._chunk_stride(1025, bad)
