@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--blocks", type=str, default="256")
     ap.add_argument("--shapes", type=str, default="c5,c3")
     ap.add_argument("--switch", type=str, default="0,1", help="0: no switch record; 1: the product's switching pass")
+    ap.add_argument("--variants-c5", type=str, default="", help="override the shape's variant list")
+    ap.add_argument("--variants-c3", type=str, default="")
+    ap.add_argument("--variants-c2", type=str, default="")
     ap.add_argument("--redo-blocks", type=str, default="",
                     help="instead: time the product's second pass (redo list + redo kernel) on these grids")
     args = ap.parse_args()
@@ -55,6 +58,9 @@ def main():
     out = {}
     for shape in args.shapes.split(","):
         need, total, mib, nobj, align, variants = SHAPES[shape]
+        over = getattr(args, f"variants_{shape}")
+        if over:
+            variants = [int(x) for x in over.split(",")]
         S = mib << 20
         L, cs, slot = D.slot_geometry(S, need, total, chunk_align=align)
         rows = total - need
