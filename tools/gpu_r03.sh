@@ -88,6 +88,8 @@ for step in "$@"; do
     proffull) run proffull 600 rocprofv3 --kernel-trace --stats -d "$OUT/proffull" -o bench --output-format csv -- python3 bench.py ;;
     rehearse4) run rehearse4 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 4 --objects 16 --steps 5 --warmup 1 &&
                run rehearse4_c5 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 4 --preset c5 --global-objects 8 --steps 3 --warmup 1 ;;
+    c2blk) run c2blk_enc 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --variants 13 --blocks 128,192,256,320 --nseg 2 --rounds 6 --queue 400802 &&
+           run c2blk_dec 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --decode 1 --separate 0 --variants 13 --blocks 128,192,256,320 --nseg 2 --rounds 6 --queue 400802 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
