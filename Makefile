@@ -8,15 +8,20 @@ SRC      := slime_amd/csrc
 OBJ      := build/obj
 LIB      := slime_amd/lib/libslime_rs.so
 
-OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/rs_capi.o
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_apply_mfma.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 CXXTEST  := tests/cpp/rs_host_test
 CACHETEST := tests/cpp/plan_cache_test
 COPYTEST := tests/cpp/copy_pool_test
 POOLTEST := tests/cpp/device_pool_test
+MFMATEST := tests/cpp/mfma_table_test
 
-all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
+
+# The matrix-core kernel's int8-limb arithmetic emulated on its table (mfma_table.hpp), CPU only.
+$(MFMATEST): tests/cpp/mfma_table_test.cpp $(SRC)/mfma_table.hpp $(SRC)/gfp.hpp $(SRC)/gfp_host.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -I$(SRC) -o $@ tests/cpp/mfma_table_test.cpp
 
 # Device routing of host calls (device_pool.hpp) with a fixed device count, CPU only.
 $(POOLTEST): tests/cpp/device_pool_test.cpp $(SRC)/device_pool.hpp $(SRC)/plan_cache.hpp
@@ -52,7 +57,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST)
+	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

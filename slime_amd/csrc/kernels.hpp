@@ -30,7 +30,21 @@ struct ApplyLaunch {
   uint32_t rows;
   uint32_t k;
   bool vec_ok;              // 16-byte units per lane (needs 4-byte aligned bases; see rs_capi.cpp)
+  // Matrix-core form (rs_apply_mfma.hip): the plan's digit table
+  // (mfma_table.hpp, device) or null, and the highest input / output shard
+  // index (the kernel's 32-bit offsets need every object under 4 GiB).
+  const uint8_t* mfma = nullptr;
+  uint32_t in_max = 0, out_max = 0;
 };
+
+// Matrix-core apply kernel: whether this launch can take it (table present,
+// mode on, k at or above the tuning threshold, shape and spans supported),
+// and the launch.  Process-wide mode: env SLIME_RS_MFMA=0 sets it off;
+// slime_rs_kernel_matrix_cores() switches it.
+bool mfma_eligible(const ApplyLaunch& a);
+hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream);
+int matrix_core_mode();
+void set_matrix_core_mode(int m);
 
 // Row stride (words) of a device coefficient table: k rounded up to 16 words,
 // so every 16-coefficient chunk of a row is one aligned s_load_dwordx16.

@@ -454,6 +454,7 @@ hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t s) {
   (void)hipGetLastError();  // report only this launch's error, not one left on the thread
   if (a.nobj == 0 || a.ncols == 0 || a.rows == 0) return hipSuccess;
+  if (mfma_eligible(a)) return launch_apply_mfma(a, s);  // wide codes on the matrix cores
   switch (a.k) {
     case 1: return dispatch_vec<1>(a, s);
     case 2: return dispatch_vec<2>(a, s);

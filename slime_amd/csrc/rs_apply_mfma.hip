@@ -1,0 +1,102 @@
+// Launcher of the matrix-core apply kernel (rs_apply_mfma_kernel.hpp) for wide
+// codes: applyMatrix (internal/rs/vector.go:90-102) as an exact int8-limb
+// product on v_mfma_i32_16x16x64_i8, for plans whose table carries the digit
+// fragments (mfma_table.hpp: rows <= 32, k <= 112).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <atomic>
+
+#include "kernels.hpp"
+#include "rs_apply_mfma_kernel.hpp"
+
+namespace slime {
+
+// Process-wide switch (env SLIME_RS_MFMA=0 sets the initial value;
+// slime_rs_kernel_matrix_cores() switches it) and the smallest k that takes
+// the matrix-core kernel (env SLIME_RS_MFMA_MINK, tuning; default 33: up to
+// k = 32 the VALU kernels are HBM-bound already).
+static std::atomic<int> g_mfma{[] {
+  const char* e = getenv("SLIME_RS_MFMA");
+  return e && e[0] == '0' ? 0 : 1;
+}()};
+int matrix_core_mode() { return g_mfma.load(std::memory_order_relaxed); }
+void set_matrix_core_mode(int m) { g_mfma.store(m, std::memory_order_relaxed); }
+static uint32_t mfma_min_k() {
+  static const uint32_t v = [] {
+    const char* e = getenv("SLIME_RS_MFMA_MINK");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (uint32_t)x : 33u;
+  }();
+  return v;
+}
+
+bool mfma_eligible(const ApplyLaunch& a) {
+  if (!a.mfma || !a.vec_ok || !matrix_core_mode() || a.k < mfma_min_k()) return false;
+  if (!mfma::supported(a.rows, a.k)) return false;
+  // 32-bit per-lane byte offsets from each object's base (see the kernel).
+  const uint64_t lim = 1ull << 32;
+  if (((uint64_t)a.in_max * a.in_shard_stride + a.ncols) * 4 >= lim) return false;
+  if (((uint64_t)a.out_max * a.out_shard_stride + a.ncols) * 4 >= lim) return false;
+  return true;
+}
+
+namespace {
+
+constexpr bool kNtLoads = true;
+constexpr bool kNtStores = true;
+
+// Software-pipelined form (next tile's loads in flight during the math) or
+// not; env SLIME_RS_MFMA_PIPE=0 selects the latter (tuning A/B).
+bool mfma_pipe() {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_MFMA_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int KS>
+hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
+  const uint32_t mt = mfma::mtiles(a.rows);
+  const uint32_t lds = apply::mfma_lds_bytes(mt, KS);
+  const uint64_t per_block = 4ull * 16 * 4;  // 4 waves x 16 vectors
+  const uint32_t nseg = object_segments(a.nobj, a.ncols);
+  const uint64_t nwork = (uint64_t)a.nobj * nseg;
+  const ApplyGeometry& geo = apply_geometry();
+  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
+  if (gy > 65535) gy = 65535;
+  const uint64_t target = geo.target ? geo.target : 512;
+  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  if (mfma_pipe())
+    hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, true>), dim3((uint32_t)gx, (uint32_t)gy),
+                       dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
+                       a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
+                       a.rows, a.k, nseg);
+  else
+    hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, false>), dim3((uint32_t)gx, (uint32_t)gy),
+                       dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
+                       a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
+                       a.rows, a.k, nseg);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream) {
+  switch (mfma::ksteps(a.k)) {
+    case 1: return launch_ks<1>(a, stream);
+    case 2: return launch_ks<2>(a, stream);
+    case 3: return launch_ks<3>(a, stream);
+    case 4: return launch_ks<4>(a, stream);
+    case 5: return launch_ks<5>(a, stream);
+    case 6: return launch_ks<6>(a, stream);
+    case 7: return launch_ks<7>(a, stream);
+    default: return hipErrorInvalidValue;  // mfma_eligible() rules this out
+  }
+}
+
+}  // namespace slime

@@ -32,6 +32,7 @@
 #include "gfp_host.hpp"
 #include "host_copy.hpp"
 #include "kernels.hpp"
+#include "mfma_table.hpp"
 #include "plan_cache.hpp"
 #include "rs_matrix.hpp"
 
@@ -48,6 +49,8 @@ struct slime_rs_plan {
   const uint32_t* d_coeff = nullptr;
   const uint32_t* d_in_idx = nullptr;
   const uint32_t* d_out_idx = nullptr;
+  const uint8_t* d_mfma = nullptr;  // device: matrix-core digit table (mfma_table.hpp), or null
+  uint32_t in_max = 0;              // highest input shard index
 };
 
 namespace slime {
@@ -131,11 +134,18 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   const uint32_t cs = coeff_stride(k);
   const size_t ncoef = (size_t)rows * cs;
   const size_t n_in = (k + 3) & ~3u, n_out = (rows + 3) & ~3u;
-  std::vector<uint32_t> host(ncoef + n_in + n_out, 0u);
+  // Wide codes also get the matrix-core kernel's digit table (rs_apply_mfma.hip),
+  // 16-byte aligned after the index arrays.
+  const size_t n_head = (ncoef + n_in + n_out + 3) & ~(size_t)3;
+  std::vector<uint8_t> mt;
+  if (k >= 17 && mfma::supported(rows, k)) mt = mfma::build_table(coeff, rows, k, false);
+  std::vector<uint32_t> host(n_head + mt.size() / 4, 0u);
   for (uint32_t i = 0; i < rows; ++i)
     for (uint32_t j = 0; j < k; ++j) host[(size_t)i * cs + j] = coeff[(size_t)i * k + j] % kP;
   std::copy(in_idx.begin(), in_idx.end(), host.begin() + ncoef);
   std::copy(out_idx.begin(), out_idx.end(), host.begin() + ncoef + n_in);
+  if (!mt.empty()) memcpy(host.data() + n_head, mt.data(), mt.size());
+  plan->in_max = in_idx.empty() ? 0 : *std::max_element(in_idx.begin(), in_idx.end());
   DeviceScope ds(device);
   void* p = nullptr;
   HIP_TRY(hipMalloc(&p, host.size() * sizeof(uint32_t)));
@@ -155,6 +165,7 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   plan->d_coeff = plan->table;
   plan->d_in_idx = plan->table + ncoef;
   plan->d_out_idx = plan->table + ncoef + n_in;
+  if (!mt.empty()) plan->d_mfma = reinterpret_cast<const uint8_t*>(plan->table + n_head);
   *out = plan.release();
   return 0;
 }
@@ -195,6 +206,9 @@ int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, ui
   // vectorised.  16-byte aligned layouts are faster; pad strides where the
   // layout is yours to choose.
   a.vec_ok = aligned4(src) && aligned4(dst);
+  a.mfma = plan->d_mfma;
+  a.in_max = plan->in_max;
+  a.out_max = plan->out_max;
   const_cast<slime_rs_plan*>(plan)->executed.store(true, std::memory_order_relaxed);
   DeviceScope ds(plan->device);
   HIP_TRY(launch_apply(a, stream));
@@ -808,6 +822,13 @@ int slime_rs_kernel_schedule(int mode) {
   if (mode < 0) return queue_mode();
   if (mode > 1) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0 (static) or 1 (dynamic)");
   set_queue_mode(mode);
+  return 0;
+}
+
+int slime_rs_kernel_matrix_cores(int mode) {
+  if (mode < 0) return matrix_core_mode();
+  if (mode > 1) return fail(Status::InvalidArg, "kernel_matrix_cores: mode must be 0 (VALU) or 1 (matrix cores)");
+  set_matrix_core_mode(mode);
   return 0;
 }
 

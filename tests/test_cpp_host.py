@@ -84,3 +84,19 @@ def test_device_pool_routing_with_a_fixed_device_count():
     assert r.returncode == 0, r.stdout + r.stderr
     for name in ("TestAllowedDevices", "TestPoolSpreadsConcurrentCallers", "TestPinnedDevices", "TestLeastLoaded"):
         assert f"ok   {name}" in r.stdout
+
+
+MFMA_BIN = os.path.join(ROOT, "tests", "cpp", "mfma_table_test")
+
+
+def test_mfma_table_arithmetic_emulated():
+    """The matrix-core kernel's exact int8-limb identity (mfma_table.hpp),
+    emulated on the CPU from the very A-fragment table a plan uploads and the
+    B fragments the kernel assembles: every (rows, k) shape the kernel takes
+    (k up to 112, rows up to 32, symbol and big-endian byte order) is
+    bit-exact against sum_j c_ij x_j mod p, including non-canonical symbols
+    and coefficients at the digit window's edges."""
+    subprocess.run(["make", "-C", ROOT, "tests/cpp/mfma_table_test"], check=True, capture_output=True)
+    r = subprocess.run([MFMA_BIN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bit-exact" in r.stdout

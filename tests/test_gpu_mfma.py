@@ -1,0 +1,163 @@
+"""GPU parity of the matrix-core apply kernel (rs_apply_mfma.hip): wide codes
+(k >= 33, up to 32 output rows) as an exact int8-limb product on
+v_mfma_i32_16x16x64_i8, against the C oracle (applyMatrix,
+internal/rs/vector.go:90-102) and against the VALU kernels in the same process
+(slime_rs_kernel_matrix_cores 0/1).  Bit-exact: integer field arithmetic.
+
+Cases: every K-step count 3..7 (k = 33..112), 1..32 output rows (M-tile
+padding), column tails past the last 16-byte vector and partial wave tiles,
+non-canonical inputs (x >= p, 0xFFFFFFFF), arbitrary coefficient matrices
+including non-canonical coefficients, shuffled survivor indices, padded shard
+strides, a separate destination, and rows > 32 (the VALU kernels take over).
+"""
+import numpy as np
+import pytest
+
+from slime_amd import _native as N
+from slime_amd import gf
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+P = gf.MaxVal
+EDGES = np.array([0, 1, 2, P - 1, P, P + 1, P + 4, 0xFFFFFFFF, 0x7FFFFFFF, 0x80000000, 0x80808080],
+                 dtype=np.uint32)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(params=[1, 0], ids=["mfma", "valu"])
+def matrix_cores(request):
+    prev = N.lib.slime_rs_kernel_matrix_cores(-1)
+    N.check(N.lib.slime_rs_kernel_matrix_cores(request.param))
+    yield request.param
+    N.check(N.lib.slime_rs_kernel_matrix_cores(prev))
+
+
+def _rand(rng, shape):
+    x = rng.integers(0, 2**32, size=shape, dtype=np.uint64).astype(np.uint32)
+    flat = x.reshape(-1)
+    n = min(flat.size, 64)
+    flat[rng.choice(flat.size, size=n, replace=False)] = rng.choice(EDGES, size=n)
+    return x
+
+
+def _apply_ref(coeff, x):
+    """out[i] = sum_j coeff[i][j] * x[j] mod p over columns (exact, numpy uint64 in pieces)."""
+    c = coeff.astype(np.uint64) % P
+    xs = x.astype(np.uint64) % P
+    out = np.zeros((c.shape[0], x.shape[1]), dtype=np.uint64)
+    for j in range(c.shape[1]):
+        out = (out + (c[:, j:j + 1] * xs[j:j + 1]) % P) % P
+    return out.astype(np.uint32)
+
+
+@pytest.mark.parametrize("need,total", [(33, 34), (33, 50), (40, 56), (47, 48), (48, 64), (64, 80), (80, 100),
+                                        (64, 96), (99, 100)])
+@pytest.mark.parametrize("L", [1, 5, 64, 67, 1001, 4096 + 3])
+def test_encode_vs_oracle(torch_dev, matrix_cores, need, total, L):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(need * 131 + L)
+    nobj = 2
+    h = _rand(rng, (nobj, total, L))
+    buf = torch.from_numpy(h.reshape(-1).view(np.int32).copy()).cuda()
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+    for o in range(nobj):
+        ref = np.ascontiguousarray(h[o].copy())
+        OC.encode_object(ref, need, total)
+        assert np.array_equal(got[o], ref), (o, need, total, L)
+
+
+@pytest.mark.parametrize("need,total,nerase", [(64, 80, 16), (40, 56, 5), (50, 82, 32), (96, 100, 4), (33, 50, 17)])
+def test_reconstruct_shuffled_survivors_separate_dst(torch_dev, matrix_cores, need, total, nerase):
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(total * 7 + nerase)
+    L, nobj, ss = 3 * 1024 + 7, 3, 3 * 1024 + 64  # padded shard stride
+    data = _rand(rng, (nobj, need, L)) % P
+    code = np.zeros((nobj, total, ss), dtype=np.uint32)
+    for o in range(nobj):
+        ref = np.zeros((total, L), dtype=np.uint32)
+        ref[:need] = data[o]
+        OC.encode_object(ref, need, total)
+        code[o, :, :L] = ref
+    buf = torch.from_numpy(code.reshape(-1).view(np.int32).copy()).cuda()
+    erase = sorted(rng.choice(total, size=nerase, replace=False).tolist())
+    have = [i for i in range(total) if i not in erase]
+    rng.shuffle(have)
+    have = have[:need]
+    out = torch.zeros(nobj * nerase * L, dtype=torch.int32, device="cuda")
+    D.Plan.reconstruct(need, total, have, erase)(buf, D.layout_of(total, L, ss), out, D.layout_of(nerase, L), L, nobj)
+    torch.cuda.synchronize()
+    rec = out.cpu().numpy().view(np.uint32).reshape(nobj, nerase, L)
+    for o in range(nobj):
+        for i, t in enumerate(erase):
+            assert np.array_equal(rec[o, i], code[o, t, :L]), (o, t)
+
+
+@pytest.mark.parametrize("rows,k", [(1, 33), (3, 47), (5, 64), (17, 70), (31, 99), (32, 112), (33, 64), (40, 100)])
+def test_arbitrary_matrix_noncanonical_coefficients(torch_dev, matrix_cores, rows, k):
+    """Plan.matrix with random coefficients, a quarter of them >= p or at the
+    digit window's edges; rows 33 and 40 exceed the matrix-core table (VALU)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(rows * 1000 + k)
+    coeff = rng.integers(0, 2**32, size=(rows, k), dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0, 1, P - 1, P, 0xFFFFFFFF, 2139062143, 2139062144, 2155905147, 256], dtype=np.uint32)
+    mask = rng.random((rows, k)) < 0.25
+    coeff[mask] = rng.choice(edge, size=int(mask.sum()))
+    L, nobj = 2 * 1024 + 3, 2
+    shards = [int(s) for s in rng.permutation(k + 5)[:k]]  # k input shards out of k + 5, any order
+    src = _rand(rng, (nobj, k + 5, L))
+    sbuf = torch.from_numpy(src.reshape(-1).view(np.int32).copy()).cuda()
+    dbuf = torch.zeros(nobj * rows * L, dtype=torch.int32, device="cuda")
+    D.Plan.matrix(coeff, shards)(sbuf, D.layout_of(k + 5, L), dbuf, D.layout_of(rows, L), L, nobj)
+    torch.cuda.synchronize()
+    got = dbuf.cpu().numpy().view(np.uint32).reshape(nobj, rows, L)
+    for o in range(nobj):
+        want = _apply_ref(coeff, src[o][shards])
+        assert np.array_equal(got[o], want), o
+
+
+def test_matrix_cores_match_valu_large(torch_dev):
+    """64/80 on 3 objects of 4 Mi symbols per shard: the two kernel families
+    agree on every symbol; one object's first 64 Ki columns vs the oracle."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, L, nobj = 64, 80, 1 << 22, 3
+    lay = D.layout_of(total, L)
+    buf = D.device_empty(nobj * total * L, torch.int32, 0)
+    D.fill_symbols(buf, 4242)
+    prev = N.lib.slime_rs_kernel_matrix_cores(-1)
+    try:
+        outs = []
+        for mode in (1, 0):
+            N.check(N.lib.slime_rs_kernel_matrix_cores(mode))
+            out = torch.zeros(nobj * (total - need) * L, dtype=torch.int32, device="cuda")
+            D.Plan.encode(need, total)(buf, lay, out, D.layout_of(total - need, L), L, nobj)
+            torch.cuda.synchronize()
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        N.check(N.lib.slime_rs_kernel_matrix_cores(prev))
+    cols = 1 << 16
+    h = buf.view(nobj, total, L)[1, :need, :cols].cpu().numpy().view(np.uint32)
+    ref = np.zeros((total, cols), dtype=np.uint32)
+    ref[:need] = h
+    OC.encode_object(ref, need, total)
+    got = outs[0].view(nobj, total - need, L)[1, :, :cols].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, ref[need:])
+
+
+def test_matrix_cores_switch():
+    assert N.lib.slime_rs_kernel_matrix_cores(-1) in (0, 1)
+    assert N.lib.slime_rs_kernel_matrix_cores(2) != 0
