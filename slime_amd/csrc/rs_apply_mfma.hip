@@ -46,14 +46,23 @@ namespace {
 constexpr bool kNtLoads = true;
 constexpr bool kNtStores = true;
 
-// Software-pipelined form (next tile's loads in flight during the math) or
-// not; env SLIME_RS_MFMA_PIPE=0 selects the latter (tuning A/B).
-bool mfma_pipe() {
-  static const bool on = [] {
-    const char* e = getenv("SLIME_RS_MFMA_PIPE");
-    return !(e && e[0] == '0');
+// Kernel form (tuning A/B; env SLIME_RS_MFMA_MODE): 2 = one tile of data
+// registers refilled K step by K step behind the math (default), 1 = two
+// tile buffers, 0 = no prefetch.
+int mfma_mode() {
+  static const int m = [] {
+    const char* e = getenv("SLIME_RS_MFMA_MODE");
+    const int v = e ? atoi(e) : 2;
+    return v >= 0 && v <= 2 ? v : 2;
   }();
-  return on;
+  return m;
+}
+
+template <int KS, int MODE>
+void launch_mode(const ApplyLaunch& a, hipStream_t stream, dim3 grid, uint32_t lds, uint32_t nseg) {
+  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, MODE>), grid, dim3(apply::kBlock), lds,
+                     stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride, a.out_shard_stride,
+                     a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
 }
 
 template <int KS>
@@ -66,21 +75,18 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const ApplyGeometry& geo = apply_geometry();
   uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
   if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : 512;
+  const int mode = mfma_mode();
+  const uint64_t target = geo.target ? geo.target : 256ull * apply::mfma_waves(KS, mode);  // resident blocks
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  if (mfma_pipe())
-    hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, true>), dim3((uint32_t)gx, (uint32_t)gy),
-                       dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
-                       a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
-                       a.rows, a.k, nseg);
-  else
-    hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, false>), dim3((uint32_t)gx, (uint32_t)gy),
-                       dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
-                       a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
-                       a.rows, a.k, nseg);
+  const dim3 grid((uint32_t)gx, (uint32_t)gy);
+  switch (mode) {
+    case 0: launch_mode<KS, 0>(a, stream, grid, lds, nseg); break;
+    case 1: launch_mode<KS, 1>(a, stream, grid, lds, nseg); break;
+    default: launch_mode<KS, 2>(a, stream, grid, lds, nseg); break;
+  }
   return hipGetLastError();
 }
 

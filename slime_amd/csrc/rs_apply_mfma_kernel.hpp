@@ -39,6 +39,27 @@ __host__ __device__ constexpr uint32_t mfma_lds_bytes(uint32_t mt, uint32_t ks) 
   return mt * ks * mfma::kFragBytes + mt * 4 * (8 + 4);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// R + d0 + 2^8 d1 + 2^16 d2 + 2^24 d3 as a 64-bit integer (R carries the
+// offset that keeps it positive): four v_mad_i64_i32, the constants in SGPRs
+// (gfx9 VOP3 takes no literals).
+__device__ __forceinline__ uint64_t mfma_recombine(const i32x4& d, uint64_t R) {
+  uint64_t v = R, cc;
+  asm("v_mad_i64_i32 %0, %1, %2, 1, %0" : "+v"(v), "=s"(cc) : "v"(d[0]));
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cc) : "v"(d[1]), "s"(256));
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cc) : "v"(d[2]), "s"(65536));
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cc) : "v"(d[3]), "s"(16777216));
+  return v;
+}
+#else
+__device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
+#endif
+
+// Waves per SIMD the kernel is compiled for (registers permitting): two up
+// to four K steps (k <= 64; the refill form then fits 256 VGPRs with the
+// accumulators in VGPRs), one above (k <= 112 holds up to 112 data VGPRs).
+__host__ __device__ constexpr int mfma_waves(int ks, int mode) { return ks <= (mode == 1 ? 2 : 4) ? 2 : 1; }
+
 template <int KS, bool NTL>
 __device__ __forceinline__ void mfma_load_tile(uint4 (&x)[KS][4], const char* __restrict__ ib,
                                                const uint32_t (&soff)[KS][4], uint32_t colb, uint32_t lim) {
@@ -46,69 +67,88 @@ __device__ __forceinline__ void mfma_load_tile(uint4 (&x)[KS][4], const char* __
   for (int q = 0; q < KS; ++q)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj)
-      x[q][jj] = soff[q][jj] != 0xFFFFFFFFu
-                     ? ld16<NTL>(reinterpret_cast<const uint32_t*>(ib + (uint32_t)(soff[q][jj] + colb)))
-                     : make_uint4(0, 0, 0, 0);
+      x[q][jj] = ld16<NTL>(reinterpret_cast<const uint32_t*>(ib + (uint32_t)(soff[q][jj] + colb)));
   (void)lim;
 }
 
-// One tile's math and stores: x holds the raw words, lane's output column
-// vector at byte offset colb (store only if `store`).
-template <int KS, bool NTS>
-__device__ __forceinline__ void mfma_tile(const uint4 (&x)[KS][4], const i32x4* __restrict__ lfrag,
-                                          const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
-                                          uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, char* __restrict__ ob,
-                                          uint32_t colb, bool store) {
-  for (uint32_t mb = 0; mb < MT; mb += 4) {
-    i32x4 acc[4][4];
+// One row block (M tiles mb..mb+3) of a tile: the MFMAs over every K step,
+// then the recombination, fold and store of the lane's output vector (byte
+// offset colb; only if `store`).  REFILL: after K step q's B fragments are
+// built, x[q] is reloaded with the next tile's vectors (byte offset colbn), so
+// the next tile streams in one K step at a time behind the math and the wave
+// holds one tile of data registers instead of two.
+template <int KS, bool NTL, bool NTS, bool REFILL>
+__device__ __forceinline__ void mfma_rows(uint4 (&x)[KS][4], const char* __restrict__ ib,
+                                          const uint32_t (&soff)[KS][4], uint32_t colbn,
+                                          const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
+                                          const uint32_t* __restrict__ loff, uint32_t mb, uint32_t MT, uint32_t rows,
+                                          uint32_t lane, uint32_t g, char* __restrict__ ob, uint32_t colb, bool store) {
+  i32x4 acc[4][4];
 #pragma unroll
-    for (int mm = 0; mm < 4; ++mm)
+  for (int q = 0; q < KS; ++q) {
+    // B fragments of K step q: b[c] = the lane's four shards at column
+    // 4n+c, each byte XOR 0x80 (u - 128 as int8).
+    i32x4 b[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[mm][c] = i32x4{0, 0, 0, 0};
+    for (int jj = 0; jj < 4; ++jj) {
+      b[0][jj] = (int)(x[q][jj].x ^ 0x80808080u);
+      b[1][jj] = (int)(x[q][jj].y ^ 0x80808080u);
+      b[2][jj] = (int)(x[q][jj].z ^ 0x80808080u);
+      b[3][jj] = (int)(x[q][jj].w ^ 0x80808080u);
+    }
+    if constexpr (REFILL) {
 #pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      // B fragments of K step q: b[c] = the lane's four shards at column
-      // 4n+c, each byte XOR 0x80 (u - 128 as int8).
-      i32x4 b[4];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        b[0][jj] = (int)(x[q][jj].x ^ 0x80808080u);
-        b[1][jj] = (int)(x[q][jj].y ^ 0x80808080u);
-        b[2][jj] = (int)(x[q][jj].z ^ 0x80808080u);
-        b[3][jj] = (int)(x[q][jj].w ^ 0x80808080u);
-      }
-#pragma unroll
-      for (int mm = 0; mm < 4; ++mm) {
-        if (mb + mm < MT) {
-          const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) acc[mm][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], acc[mm][c], 0, 0, 0);
-        }
-      }
+      for (int jj = 0; jj < 4; ++jj)
+        x[q][jj] = ld16<NTL>(reinterpret_cast<const uint32_t*>(ib + (uint32_t)(soff[q][jj] + colbn)));
     }
 #pragma unroll
     for (int mm = 0; mm < 4; ++mm) {
-      const uint32_t i = 4 * (mb + mm) + g;
-      if (mb + mm < MT && i < rows && store) {
-        const uint64_t R = lrowc[i];
-        uint32_t r[4];
+      if (mb + mm < MT) {
+        const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const i32x4 d = acc[mm][c];
-          const int64_t v = (int64_t)d[0] + ((int64_t)d[1] << 8) + ((int64_t)d[2] << 16) + ((int64_t)d[3] << 24);
-          r[c] = fold96(R + (uint64_t)v, 0);
-        }
-        st16<NTS>(reinterpret_cast<uint32_t*>(ob + (uint32_t)(loff[i] + colb)), make_uint4(r[0], r[1], r[2], r[3]));
+        for (int c = 0; c < 4; ++c)
+          acc[mm][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], q == 0 ? i32x4{0, 0, 0, 0} : acc[mm][c], 0, 0, 0);
       }
+    }
+    // Keep step q's refill loads in step q: scheduled all at the top they
+    // would double the live data registers (and halve the occupancy).
+    if constexpr (REFILL) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    const uint32_t i = 4 * (mb + mm) + g;
+    if (mb + mm < MT && i < rows && store) {
+      const uint64_t R = lrowc[i];
+      uint32_t r[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        r[c] = fold96(mfma_recombine(acc[mm][c], R), 0);
+      }
+      st16<NTS>(reinterpret_cast<uint32_t*>(ob + (uint32_t)(loff[i] + colb)), make_uint4(r[0], r[1], r[2], r[3]));
     }
   }
 }
 
+// One tile: every row block; with REFILL the last one reloads x with the
+// next tile.
+template <int KS, bool NTL, bool NTS, bool REFILL>
+__device__ __forceinline__ void mfma_tile(uint4 (&x)[KS][4], const char* __restrict__ ib,
+                                          const uint32_t (&soff)[KS][4], uint32_t colbn,
+                                          const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
+                                          const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows, uint32_t lane,
+                                          uint32_t g, char* __restrict__ ob, uint32_t colb, bool store) {
+  uint32_t mb = 0;
+  for (; mb + 4 < MT; mb += 4)
+    mfma_rows<KS, NTL, NTS, false>(x, ib, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb, store);
+  mfma_rows<KS, NTL, NTS, REFILL>(x, ib, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb, store);
+}
+
 // table: the plan's mfma table (mfma_table.hpp layout); coeff: the plan's
-// coefficient rows (column tails); PIPE: the next tile's loads are issued
-// before the current tile's math.
-template <int KS, bool NTL, bool NTS, bool PIPE>
-__global__ __launch_bounds__(kBlock) void rs_apply_mfma_kernel(
+// coefficient rows (column tails).  MODE 0: load a tile, compute it; 1: two
+// tile buffers, the next tile's loads issued before the current tile's math;
+// 2: one tile buffer refilled K step by K step behind the math (mfma_rows).
+template <int KS, bool NTL, bool NTS, int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, MODE)))) void rs_apply_mfma_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
@@ -137,7 +177,9 @@ __global__ __launch_bounds__(kBlock) void rs_apply_mfma_kernel(
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const uint32_t j = 16 * q + 4 * g + jj;
-      soff[q][jj] = j < k ? (uint32_t)(in_idx[j] * in_shard * 4) : 0xFFFFFFFFu;
+      // Shards past k: their digits are zero, so any real shard will do --
+      // in_idx[k-1], whose lines the lanes of shard k-1 fetch anyway.
+      soff[q][jj] = (uint32_t)(in_idx[j < k ? j : k - 1] * in_shard * 4);
     }
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
@@ -154,32 +196,47 @@ __global__ __launch_bounds__(kBlock) void rs_apply_mfma_kernel(
     const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
     const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
     const uint32_t ntiles = (v1 - v0 + 15) / 16;
-    if constexpr (PIPE) {
+    auto colb_of = [&](uint32_t tile) {
+      const uint32_t v = v0 + tile * 16 + n;
+      return (v < v1 ? v : v1 - 1) << 4;
+    };
+    if constexpr (MODE == 1) {
       uint4 xa[KS][4], xb[KS][4];
       uint32_t t = wave;
-      auto colb_of = [&](uint32_t tile) {
-        const uint32_t v = v0 + tile * 16 + n;
-        return (v < v1 ? v : v1 - 1) << 4;
-      };
       if (t < ntiles) mfma_load_tile<KS, NTL>(xa, ib, soff, colb_of(t), 0);
       while (t < ntiles) {
         const uint32_t t1 = t + nwaves;
         mfma_load_tile<KS, NTL>(xb, ib, soff, colb_of(t1 < ntiles ? t1 : t), 0);
-        mfma_tile<KS, NTS>(xa, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t), v0 + t * 16 + n < v1);
+        mfma_tile<KS, NTL, NTS, false>(xa, ib, soff, 0, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+                                       v0 + t * 16 + n < v1);
         t = t1;
         if (t >= ntiles) break;
         const uint32_t t2 = t + nwaves;
         mfma_load_tile<KS, NTL>(xa, ib, soff, colb_of(t2 < ntiles ? t2 : t), 0);
-        mfma_tile<KS, NTS>(xb, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t), v0 + t * 16 + n < v1);
+        mfma_tile<KS, NTL, NTS, false>(xb, ib, soff, 0, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+                                       v0 + t * 16 + n < v1);
         t = t2;
+      }
+    } else if constexpr (MODE == 2) {
+      uint4 x[KS][4];
+      uint32_t t = wave;
+      if (t < ntiles) mfma_load_tile<KS, NTL>(x, ib, soff, colb_of(t), 0);
+      while (t < ntiles) {
+        const uint32_t tn = t + nwaves;
+        if (tn < ntiles)
+          mfma_tile<KS, NTL, NTS, true>(x, ib, soff, colb_of(tn), lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+                                        v0 + t * 16 + n < v1);
+        else
+          mfma_tile<KS, NTL, NTS, false>(x, ib, soff, 0, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+                                         v0 + t * 16 + n < v1);
+        t = tn;
       }
     } else {
       for (uint32_t t = wave; t < ntiles; t += nwaves) {
-        const uint32_t v = v0 + t * 16 + n;
-        const uint32_t colb = (v < v1 ? v : v1 - 1) << 4;
         uint4 x[KS][4];
-        mfma_load_tile<KS, NTL>(x, ib, soff, colb, 0);
-        mfma_tile<KS, NTS>(x, lds, lrowc, loff, MT, rows, lane, g, ob, colb, v < v1);
+        mfma_load_tile<KS, NTL>(x, ib, soff, colb_of(t), 0);
+        mfma_tile<KS, NTL, NTS, false>(x, ib, soff, 0, lds, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+                                       v0 + t * 16 + n < v1);
       }
     }
     if (seg == nseg - 1)

@@ -53,19 +53,17 @@ for step in "$@"; do
             --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
     mfma_tests) run pytest_mfma 600 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 300 --timeout-method thread ;;
     # wide codes: matrix-core kernel (default), its non-pipelined form, the VALU kernels
+    # wide codes: matrix-core kernel forms (SLIME_RS_MFMA_MODE 2 = K-step refill, default; 1 two tile
+    # buffers; 0 no prefetch) against the VALU kernels (SLIME_RS_MFMA=0), same box
     wide) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          E20=$E16,16,17,18,19
           WIDE="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
-          run wide_6480_mfma 300 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $WIDE &&
-          run wide_6480_mfma_nopipe 300 env SLIME_RS_MFMA_PIPE=0 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $WIDE &&
-          run wide_6480_valu 300 env SLIME_RS_MFMA=0 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $WIDE &&
-          run wide_4864_mfma 300 python bench.py --need 48 --total 64 --objects 32 --erase $E16 $WIDE &&
-          run wide_4864_mfma_nopipe 300 env SLIME_RS_MFMA_PIPE=0 python bench.py --need 48 --total 64 --objects 32 --erase $E16 $WIDE &&
-          run wide_4864_valu 300 env SLIME_RS_MFMA=0 python bench.py --need 48 --total 64 --objects 32 --erase $E16 $WIDE &&
-          run wide_80100_mfma 300 python bench.py --need 80 --total 100 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19 $WIDE &&
-          run wide_80100_valu 300 env SLIME_RS_MFMA=0 python bench.py --need 80 --total 100 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19 $WIDE &&
-          run wide_3240_mfma 300 env SLIME_RS_MFMA_MINK=17 python bench.py --need 32 --total 40 --objects 32 --erase 0,1,2,3,4,5,6,7 $WIDE &&
-          run wide_3240_mfma_nopipe 300 env SLIME_RS_MFMA_MINK=17 SLIME_RS_MFMA_PIPE=0 python bench.py --need 32 --total 40 --objects 32 --erase 0,1,2,3,4,5,6,7 $WIDE &&
-          run wide_3240_valu 300 python bench.py --need 32 --total 40 --objects 32 --erase 0,1,2,3,4,5,6,7 $WIDE ;;
+          for shp in "64 80 $E16" "48 64 $E16" "80 100 $E20" "96 100 0,1,2,3" "40 48 0,1,2,3,4,5,6,7"; do
+            set -- $shp
+            for v in "m2:SLIME_RS_MFMA_MODE=2" "m1:SLIME_RS_MFMA_MODE=1" "m0:SLIME_RS_MFMA_MODE=0" "valu:SLIME_RS_MFMA=0"; do
+              run wide_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WIDE || exit 1
+            done
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
