@@ -45,6 +45,11 @@ bool mfma_eligible(const ApplyLaunch& a);
 hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream);
 int matrix_core_mode();
 void set_matrix_core_mode(int m);
+// Smallest k that takes the matrix cores (env SLIME_RS_MFMA_MINK, tuning;
+// default 33) and the kernel form (env SLIME_RS_MFMA_MODE: 2 K-step refill,
+// the product; 1 two tile buffers; 0 no prefetch).
+uint32_t mfma_min_k();
+int mfma_kernel_form();
 
 // Row stride (words) of a device coefficient table: k rounded up to 16 words,
 // so every 16-coefficient chunk of a row is one aligned s_load_dwordx16.
@@ -150,6 +155,10 @@ struct BytesLaunch {
   uint8_t* scratch = nullptr;
   bool* switched = nullptr;
   uint64_t cstride = 0;  // bytes between a slot's chunks (0: 4L, the wire layout)
+  // Matrix-core form (rs_bytes_mfma.hip): the plan's byte-order digit table
+  // or null, and the highest input / output chunk index.
+  const uint8_t* mfma = nullptr;
+  uint32_t in_max = 0, out_max = 0;
 };
 inline uint64_t chunk_stride(const BytesLaunch& a) { return a.cstride ? a.cstride : 4 * a.L; }
 hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
@@ -173,6 +182,11 @@ inline dim3 bytes_grid(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t ta
   return dim3((uint32_t)gx, (uint32_t)gy);
 }
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t stream);
+// Wide codes on the matrix cores (rs_bytes_mfma.hip): eligibility (table,
+// mode, k >= mfma_min_k(), shape, chunk offsets under 4 GiB) and the launches.
+bool bytes_mfma_eligible(const BytesLaunch& a);
+hipError_t launch_encode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
+hipError_t launch_decode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t stream);
 
 // --- byte <-> symbol codec (internal/rs/gf/map.go) -------------------------

@@ -22,7 +22,7 @@ static std::atomic<int> g_mfma{[] {
 }()};
 int matrix_core_mode() { return g_mfma.load(std::memory_order_relaxed); }
 void set_matrix_core_mode(int m) { g_mfma.store(m, std::memory_order_relaxed); }
-static uint32_t mfma_min_k() {
+uint32_t mfma_min_k() {
   static const uint32_t v = [] {
     const char* e = getenv("SLIME_RS_MFMA_MINK");
     const long long x = e ? atoll(e) : 0;
@@ -49,7 +49,8 @@ constexpr bool kNtStores = true;
 // Kernel form (tuning A/B; env SLIME_RS_MFMA_MODE): 2 = one tile of data
 // registers refilled K step by K step behind the math (default), 1 = two
 // tile buffers, 0 = no prefetch.
-int mfma_mode() {
+}  // namespace
+int mfma_kernel_form() {
   static const int m = [] {
     const char* e = getenv("SLIME_RS_MFMA_MODE");
     const int v = e ? atoi(e) : 2;
@@ -57,6 +58,7 @@ int mfma_mode() {
   }();
   return m;
 }
+namespace {
 
 template <int KS, int MODE>
 void launch_mode(const ApplyLaunch& a, hipStream_t stream, dim3 grid, uint32_t lds, uint32_t nseg) {
@@ -75,7 +77,7 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const ApplyGeometry& geo = apply_geometry();
   uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
   if (gy > 65535) gy = 65535;
-  const int mode = mfma_mode();
+  const int mode = mfma_kernel_form();
   const uint64_t target = geo.target ? geo.target : 256ull * apply::mfma_waves(KS, mode);  // resident blocks
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;

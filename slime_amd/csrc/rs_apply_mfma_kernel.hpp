@@ -90,6 +90,14 @@ __device__ __forceinline__ void mfma_load_tile(vec_t<W> (&x)[KS][4], const char*
     for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ib + (uint32_t)(soff[q][jj] + colb));
 }
 
+// Hook run on every loaded vector of a tile before its B fragments are
+// built (the byte encode folds MapToGF's flags there); the symbol path's is
+// empty.
+struct NoPre {
+  template <class V>
+  __device__ __forceinline__ void operator()(const V&) {}
+};
+
 // Per-launch word transforms: B fragments are (word ^ xin) as int8 bytes
 // (xin = 0x80808080 for symbols: u - 128), outputs are stored as r ^ xout,
 // byte-swapped when BSWAP (the byte path's big-endian chunk words).
@@ -103,22 +111,24 @@ struct MfmaIO {
 // built, x[q] is reloaded with the next tile's vectors (byte offset colbn), so
 // the next tile streams in one K step at a time behind the math and the wave
 // holds one tile of data registers instead of two.
-template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP>
+template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre>
 __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __restrict__ ib,
                                           const uint32_t (&soff)[KS][4], uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
                                           const uint32_t* __restrict__ loff, uint32_t mb, uint32_t MT, uint32_t rows,
                                           uint32_t lane, uint32_t g, char* __restrict__ ob, uint32_t colb, bool store,
-                                          MfmaIO io) {
+                                          MfmaIO io, Pre& pre) {
   i32x4 acc[4][W];
 #pragma unroll
   for (int q = 0; q < KS; ++q) {
     // B fragments of K step q: b[c] = the lane's four shards at column nW+c.
     i32x4 b[W];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
+    for (int jj = 0; jj < 4; ++jj) {
+      pre(x[q][jj]);
 #pragma unroll
       for (int c = 0; c < W; ++c) b[c][jj] = (int)(x[q][jj][c] ^ io.xin);
+    }
     if constexpr (REFILL) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ib + (uint32_t)(soff[q][jj] + colbn));
@@ -154,18 +164,19 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
 
 // One tile: every row block; with REFILL the last one reloads x with the
 // next tile.
-template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP>
+template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre>
 __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ib,
                                           const uint32_t (&soff)[KS][4], uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
                                           const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows, uint32_t lane,
-                                          uint32_t g, char* __restrict__ ob, uint32_t colb, bool store, MfmaIO io) {
+                                          uint32_t g, char* __restrict__ ob, uint32_t colb, bool store, MfmaIO io,
+                                          Pre& pre) {
   uint32_t mb = 0;
   for (; mb + 4 < MT; mb += 4)
     mfma_rows<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb,
-                                             store, io);
+                                             store, io, pre);
   mfma_rows<KS, W, NTL, NTS, REFILL, BSWAP>(x, ib, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb,
-                                            store, io);
+                                            store, io, pre);
 }
 
 // The tile walk of one wave over columns [c0, c1) of one object (c0, c1
@@ -173,12 +184,13 @@ __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __re
 // compute it; 1: two tile buffers, the next tile's loads issued before the
 // current tile's math; 2: one tile buffer refilled K step by K step behind
 // the math (mfma_rows).
-template <int KS, int W, bool NTL, bool NTS, int MODE, bool BSWAP>
+template <int KS, int W, bool NTL, bool NTS, int MODE, bool BSWAP, class Pre>
 __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob,
                                           const uint32_t (&soff)[KS][4], const i32x4* __restrict__ lfrag,
                                           const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
                                           uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
-                                          uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves, MfmaIO io) {
+                                          uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves, MfmaIO io,
+                                          Pre& pre) {
   constexpr uint32_t TC = 16 * W;
   const uint32_t ntiles = (c1 - c0 + TC - 1) / TC;
   auto col_of = [&](uint32_t tile) { return c0 + tile * TC + n * W; };
@@ -194,13 +206,13 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
       const uint32_t t1 = t + nwaves;
       mfma_load_tile<KS, W, NTL>(xb, ib, soff, colb_of(t1 < ntiles ? t1 : t));
       mfma_tile<KS, W, NTL, NTS, false, BSWAP>(xa, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io);
+                                               col_of(t) < c1, io, pre);
       t = t1;
       if (t >= ntiles) break;
       const uint32_t t2 = t + nwaves;
       mfma_load_tile<KS, W, NTL>(xa, ib, soff, colb_of(t2 < ntiles ? t2 : t));
       mfma_tile<KS, W, NTL, NTS, false, BSWAP>(xb, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io);
+                                               col_of(t) < c1, io, pre);
       t = t2;
     }
   } else if constexpr (MODE == 2) {
@@ -211,10 +223,10 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
       const uint32_t tn = t + nwaves;
       if (tn < ntiles)
         mfma_tile<KS, W, NTL, NTS, true, BSWAP>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
-                                                colb_of(t), col_of(t) < c1, io);
+                                                colb_of(t), col_of(t) < c1, io, pre);
       else
         mfma_tile<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                                 col_of(t) < c1, io);
+                                                 col_of(t) < c1, io, pre);
       t = tn;
     }
   } else {
@@ -222,14 +234,14 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
       vec_t<W> x[KS][4];
       mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));
       mfma_tile<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io);
+                                               col_of(t) < c1, io, pre);
     }
   }
 }
 
 // Block prologue: the plan's A fragments and row constants into LDS, the
 // output rows' byte offsets (out_idx[i] * out_unit), and each lane's input
-// byte offsets (in_idx[j] * in_unit; shards past k read shard in_idx[k-1],
+// byte offsets (in_idx[j] * in_unit, in_idx null: j; shards past k read shard in_idx[k-1],
 // whose digits are zero -- lines the lanes of shard k-1 fetch anyway).
 template <int KS>
 __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restrict__ table,
@@ -252,7 +264,8 @@ __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restr
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const uint32_t j = 16 * q + 4 * g + jj;
-      soff[q][jj] = (uint32_t)(in_idx[j < k ? j : k - 1] * in_unit);
+      const uint32_t jc = j < k ? j : k - 1;
+      soff[q][jj] = (uint32_t)((in_idx ? in_idx[jc] : jc) * in_unit);
     }
   __syncthreads();
 }
@@ -280,6 +293,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_wav
   const uint64_t nwork = (uint64_t)nobj * nseg;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
+  NoPre nopre;
   for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
     const uint64_t obj = wi / nseg;
     const uint32_t seg = (uint32_t)(wi % nseg);
@@ -289,7 +303,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_wav
     const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
     if (v1 > v0)
       mfma_walk<KS, W, NTL, NTS, MODE, false>(ib, ob, soff, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1,
-                                              wave, nwaves, MfmaIO{0x80808080u, 0u});
+                                              wave, nwaves, MfmaIO{0x80808080u, 0u}, nopre);
     if (seg == nseg - 1)
       for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)
         apply_column<0>(reinterpret_cast<const uint32_t*>(ib), reinterpret_cast<uint32_t*>(ob), coeff, in_idx,

@@ -1,0 +1,253 @@
+// Matrix-core form of the fused byte-domain encode and decode for wide codes
+// (need >= 33): writeChunks' MapToGF -> splitVector -> CreateParity ->
+// MapFromGF (internal/store/multi/multi_store.go:526-557) and reconstruct's
+// MapToGFWith -> RecoverData -> MapFromGF (multi_store.go:185-242), on the
+// int8-limb product of rs_apply_mfma_kernel.hpp.
+//
+// Chunk bytes hold big-endian symbols: a chunk word loaded little-endian is
+// w = bswap(x ^ m), so the plan's byte-order digit table (mfma_table.hpp,
+// big_endian: register byte b weighs 2^(8(3-b))) takes (w ^ bswap(m)) directly
+// -- with the signed-byte shift, B fragments are w ^ (0x80808080 ^ bswap(m))
+// -- and results are stored as bswap(r ^ m).  No per-word byte swap on the
+// data path; the encode's MapToGF flags take bswap(w) of every data word.
+// Tiles whose every data word is a whole object word (the bulk) run on the
+// matrix cores; edge tiles (splitVector padding, the partial last word, the
+// data-chunk tails MapFromGF writes) and column tails take the VALU step of
+// the wide byte kernels (encode_wide_step, rs_bytes_kernel.hpp).
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+#include "rs_apply_mfma_kernel.hpp"
+#include "rs_bytes_kernel.hpp"
+
+namespace slime {
+namespace bytes {
+
+using apply::i32x4;
+using apply::MfmaIO;
+
+// MapToGF's flags over every loaded data word (encode, speculative pass).
+struct FlagPre {
+  Flags* fl;
+  template <class V>
+  __device__ __forceinline__ void operator()(const V& v) {
+    constexpr int W = sizeof(V) / sizeof(uint32_t);
+#pragma unroll
+    for (int c = 0; c < W; ++c) fl->add(c & 3, be(v[c]));
+  }
+};
+
+// MODE 0: speculative pass (mapping 0, MapToGF flags into flags[obj]);
+// MODE 1: re-encode of the objects select_mapping gave mapping != 0 (status 0).
+// FORM: the apply kernel's walk form (rs_apply_mfma_kernel.hpp mfma_walk).
+template <int KS, int MODE, int FORM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, FORM)))) void
+encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
+                         uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
+                         const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
+                         const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
+                         const uint32_t* __restrict__ mapping, uint32_t nseg) {
+  constexpr int W = apply::mfma_width(KS);
+  constexpr uint32_t TCV = 4 * W;  // tile width in 16-byte vectors
+  constexpr bool F = MODE == 0;
+  extern __shared__ i32x4 lds[];
+  const uint32_t MT = (rows + 3) / 4;
+  const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
+  uint64_t* lrowc;
+  uint32_t* loff;
+  uint32_t soff[KS][4];
+  apply::mfma_prologue<KS>(lds, table, nullptr, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t obj = sg.obj;
+    const uint32_t v0 = (uint32_t)sg.v0, v1 = (uint32_t)sg.v1;
+    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
+    uint32_t m = 0;
+    if constexpr (MODE == 1) {
+      m = mapping[obj];
+      if (m == 0 || flags[obj] != 0) continue;  // uniform per block
+    }
+    uint8_t* const slot = slots + (uint64_t)obj * slot_stride + 4 * col0;  // window base
+    uint8_t* const par = slot + (uint64_t)k * chunk;
+    // Interior tiles: whole tiles of the segment whose columns are below the
+    // object's last word in the last data chunk (k-1), hence in every chunk.
+    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
+    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    if (end_max > v1) end_max = v1;
+    const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / TCV) : 0u;
+    Flags fl;
+    const MfmaIO io{0x80808080u ^ be(m), m};
+    if (nint) {
+      if constexpr (F) {
+        FlagPre pre{&fl};
+        apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
+                                                        reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT, rows,
+                                                        lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io,
+                                                        pre);
+      } else {
+        apply::NoPre pre;
+        apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
+                                                        reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT, rows,
+                                                        lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io,
+                                                        pre);
+      }
+    }
+    // Edge tiles and tail columns (VALU step, with the data-chunk tail fix).
+    for (uint64_t gv = (uint64_t)v0 + (uint64_t)nint * TCV + (uint64_t)wave * 64 + lane; gv - lane < u1;
+         gv += (uint64_t)nwaves * 64)
+      encode_wide_step<16, 8, F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, gv,
+                                 nvec, u1, sg.v1, lane, fl);
+    if constexpr (F) {
+      const uint32_t f = fl.bits();
+      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
+      if (wf && lane == 0) atomicOr(&flags[obj], wf);
+    }
+  }
+}
+
+// Decode: survivors in_idx -> rebuilt chunks out_idx of the same slot.
+template <int KS, int FORM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, FORM)))) void
+decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
+                         uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, const uint8_t* __restrict__ table,
+                         const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
+                         const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
+  constexpr int W = apply::mfma_width(KS);
+  extern __shared__ i32x4 lds[];
+  const uint32_t MT = (rows + 3) / 4;
+  const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
+  uint64_t* lrowc;
+  uint32_t* loff;
+  uint32_t soff[KS][4];
+  apply::mfma_prologue<KS>(lds, table, in_idx, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  (void)L;
+  apply::NoPre pre;
+  for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t m = mapping[sg.obj];
+    uint8_t* const slot = slots + (uint64_t)sg.obj * slot_stride + 4 * col0;  // window base
+    if (sg.v1 > sg.v0)
+      apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot),
+                                                      soff, lds, lrowc, loff, MT, rows, lane, lg, ln,
+                                                      4 * (uint32_t)sg.v0, 4 * (uint32_t)sg.v1, wave, nwaves,
+                                                      MfmaIO{0x80808080u ^ be(m), m}, pre);
+    // Columns past the last whole vector of the window, one per lane.
+    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
+      for (uint32_t i = 0; i < rows; ++i) {
+        const uint32_t* crow = coeff + (uint64_t)i * cs;
+        uint64_t lo = 0;
+        uint32_t hi = 0;
+        for (uint32_t j = 0; j < k; ++j)
+          mac(lo, hi, be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m, crow[j]);
+        *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
+      }
+    }
+  }
+}
+
+}  // namespace bytes
+
+namespace {
+
+using apply::kBlock;
+
+template <int KS, int FORM>
+hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
+  const uint64_t blocks = 256ull * apply::mfma_waves(KS, FORM);
+  if (a.phase == 0) {
+    const uint32_t nseg = object_segments(a.nobj, ncols);
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0, FORM>),
+                       bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
+                       a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma, a.coeff,
+                       a.out_idx, a.flags, a.mapping, nseg);
+  } else {
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1, FORM>), bytes_grid(ncols, 1, 1, blocks, 1),
+                       dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj,
+                       a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, 1u);
+  }
+  return hipGetLastError();
+}
+
+template <int KS, int FORM>
+hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
+  const uint64_t blocks = 256ull * apply::mfma_waves(KS, FORM);
+  const uint32_t nseg = object_segments(a.nobj, ncols);
+  hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS, FORM>),
+                     bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
+                     a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.mfma, a.coeff,
+                     a.in_idx, a.out_idx, a.mapping, nseg);
+  return hipGetLastError();
+}
+
+// The refill form (2) is the product; env SLIME_RS_MFMA_MODE picks 0/1 for A/B.
+template <int KS>
+hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
+  switch (mfma_kernel_form()) {
+    case 0: return enc_form<KS, 0>(a, s);
+    case 1: return enc_form<KS, 1>(a, s);
+    default: return enc_form<KS, 2>(a, s);
+  }
+}
+template <int KS>
+hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
+  switch (mfma_kernel_form()) {
+    case 0: return dec_form<KS, 0>(a, s);
+    case 1: return dec_form<KS, 1>(a, s);
+    default: return dec_form<KS, 2>(a, s);
+  }
+}
+
+}  // namespace
+
+bool bytes_mfma_eligible(const BytesLaunch& a) {
+  if (!a.mfma || !matrix_core_mode() || a.k < 17 || a.k < mfma_min_k() || !mfma::supported(a.rows, a.k)) return false;
+  if (!pipelined_kernels()) return false;  // SLIME_RS_PIPE=0 / kernel_pipeline(0): the non-pipelined VALU forms
+  const uint64_t ncols = a.ncols ? a.ncols : a.L;
+  // 32-bit byte offsets from the window base: every chunk the launch reads
+  // or writes, plus the window's columns.
+  // (Encode writes parity chunk k + out_idx[i]; decode reads in_idx and
+  // writes out_idx: k + out_max bounds both.)
+  const uint64_t hi_chunk = (uint64_t)a.k + a.out_max > a.in_max ? (uint64_t)a.k + a.out_max : a.in_max;
+  return (hi_chunk + 1) * chunk_stride(a) + 4 * ncols < (1ull << 32);
+}
+
+hipError_t launch_encode_bytes_mfma(const BytesLaunch& a, hipStream_t s) {
+  switch (mfma::ksteps(a.k)) {
+    case 2: return enc_ks<2>(a, s);
+    case 3: return enc_ks<3>(a, s);
+    case 4: return enc_ks<4>(a, s);
+    case 5: return enc_ks<5>(a, s);
+    case 6: return enc_ks<6>(a, s);
+    case 7: return enc_ks<7>(a, s);
+    default: return hipErrorInvalidValue;  // 17 <= k <= 112 (bytes_mfma_eligible)
+  }
+}
+
+hipError_t launch_decode_bytes_mfma(const BytesLaunch& a, hipStream_t s) {
+  switch (mfma::ksteps(a.k)) {
+    case 2: return dec_ks<2>(a, s);
+    case 3: return dec_ks<3>(a, s);
+    case 4: return dec_ks<4>(a, s);
+    case 5: return dec_ks<5>(a, s);
+    case 6: return dec_ks<6>(a, s);
+    case 7: return dec_ks<7>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace slime

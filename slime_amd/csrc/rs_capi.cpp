@@ -49,7 +49,8 @@ struct slime_rs_plan {
   const uint32_t* d_coeff = nullptr;
   const uint32_t* d_in_idx = nullptr;
   const uint32_t* d_out_idx = nullptr;
-  const uint8_t* d_mfma = nullptr;  // device: matrix-core digit table (mfma_table.hpp), or null
+  const uint8_t* d_mfma = nullptr;     // device: matrix-core digit table (mfma_table.hpp), or null
+  const uint8_t* d_mfma_be = nullptr;  // the same for big-endian chunk words (the byte path)
   uint32_t in_max = 0;              // highest input shard index
 };
 
@@ -137,14 +138,20 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   // Wide codes also get the matrix-core kernel's digit table (rs_apply_mfma.hip),
   // 16-byte aligned after the index arrays.
   const size_t n_head = (ncoef + n_in + n_out + 3) & ~(size_t)3;
-  std::vector<uint8_t> mt;
-  if (k >= 17 && mfma::supported(rows, k)) mt = mfma::build_table(coeff, rows, k, false);
-  std::vector<uint32_t> host(n_head + mt.size() / 4, 0u);
+  std::vector<uint8_t> mt, mtb;
+  if (k >= 17 && mfma::supported(rows, k)) {
+    mt = mfma::build_table(coeff, rows, k, false);
+    mtb = mfma::build_table(coeff, rows, k, true);
+  }
+  std::vector<uint32_t> host(n_head + (mt.size() + mtb.size()) / 4, 0u);
   for (uint32_t i = 0; i < rows; ++i)
     for (uint32_t j = 0; j < k; ++j) host[(size_t)i * cs + j] = coeff[(size_t)i * k + j] % kP;
   std::copy(in_idx.begin(), in_idx.end(), host.begin() + ncoef);
   std::copy(out_idx.begin(), out_idx.end(), host.begin() + ncoef + n_in);
-  if (!mt.empty()) memcpy(host.data() + n_head, mt.data(), mt.size());
+  if (!mt.empty()) {
+    memcpy(host.data() + n_head, mt.data(), mt.size());
+    memcpy(host.data() + n_head + mt.size() / 4, mtb.data(), mtb.size());
+  }
   plan->in_max = in_idx.empty() ? 0 : *std::max_element(in_idx.begin(), in_idx.end());
   DeviceScope ds(device);
   void* p = nullptr;
@@ -165,7 +172,10 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
   plan->d_coeff = plan->table;
   plan->d_in_idx = plan->table + ncoef;
   plan->d_out_idx = plan->table + ncoef + n_in;
-  if (!mt.empty()) plan->d_mfma = reinterpret_cast<const uint8_t*>(plan->table + n_head);
+  if (!mt.empty()) {
+    plan->d_mfma = reinterpret_cast<const uint8_t*>(plan->table + n_head);
+    plan->d_mfma_be = reinterpret_cast<const uint8_t*>(plan->table + n_head + mt.size() / 4);
+  }
   *out = plan.release();
   return 0;
 }
@@ -1045,6 +1055,9 @@ static BytesLaunch bytes_launch(const slime_rs_plan* plan, uint8_t* slots, uint6
   a.out_idx = plan->d_out_idx;
   a.flags = flags;
   a.mapping = mapping;
+  a.mfma = plan->d_mfma_be;
+  a.in_max = plan->in_max;
+  a.out_max = plan->out_max;
   return a;
 }
 

@@ -161,3 +161,82 @@ def test_matrix_cores_match_valu_large(torch_dev):
 def test_matrix_cores_switch():
     assert N.lib.slime_rs_kernel_matrix_cores(-1) in (0, 1)
     assert N.lib.slime_rs_kernel_matrix_cores(2) != 0
+
+
+# ---------------------------------------------------------------- byte path
+# writeChunks / reconstruct on chunk bytes (rs_bytes_mfma.hip): the encode's
+# matrix-core interior tiles with MapToGF flags and the VALU edge step, the
+# re-encode of 1<<31 objects, the decode; every chunk byte vs the oracle's
+# framing (map.go:15-113, multi_store.go:185-242, 526-557).
+
+def _byte_objects(rng, S, n):
+    objs = [rng.integers(0, 256, size=S, dtype=np.uint8).tobytes() for _ in range(n)]
+    nfull = S // 4
+    if nfull >= 8:
+        b = bytearray(objs[1]); a = int(0.6 * (nfull - 1)); b[4 * a: 4 * a + 4] = b"\xff\xff\xff\xfd"
+        objs[1] = bytes(b)  # a word >= p mid-object: mapping 1<<31
+        b = bytearray(objs[2]); b[4 * (nfull - 1): 4 * nfull] = b"\xff\xff\xff\xfe"
+        objs[2] = bytes(b)  # on the last whole word (an edge step)
+    return objs
+
+
+@pytest.mark.parametrize("need,total,S", [(33, 50, (1 << 20) + 7), (40, 56, 3 * (1 << 20) + 3), (64, 80, (4 << 20) + 1),
+                                          (80, 100, 2 << 20), (99, 100, 99999), (47, 48, 65537), (64, 96, 5 << 20),
+                                          (48, 64, 777)])
+def test_bytes_encode_objects_vs_oracle(torch_dev, matrix_cores, need, total, S):
+    torch = torch_dev
+    from slime_amd import device as D
+    from test_gpu_parity import _make_slots, _oracle_chunks
+    rng = np.random.default_rng(S + need)
+    objs = _byte_objects(rng, S, 4)
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total, extra=64)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(4, dtype=torch.int32, device="cuda")
+    status = torch.empty(4, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 4, mapping, status)
+    torch.cuda.synchronize()
+    assert status.cpu().numpy().tolist() == [0, 0, 0, 0]
+    ms = mapping.cpu().numpy().view(np.uint32)
+    h = slots.cpu().numpy()
+    for o, obj in enumerate(objs):
+        m, chunks = _oracle_chunks(obj, need, total)
+        assert ms[o] == m, o
+        for c in range(total):
+            assert h[o * stride + c * chunk: o * stride + (c + 1) * chunk].tobytes() == chunks[c], (o, c)
+        assert (h[o * stride + total * chunk: (o + 1) * stride] == 0xA5).all(), "wrote past the chunks"
+    if S // 4 >= 8:
+        assert ms[1] == 1 << 31 and ms[2] == 1 << 31
+
+
+@pytest.mark.parametrize("need,total,S,align", [(64, 80, (2 << 20) + 5, 256), (40, 56, 300001, 4096),
+                                                (80, 100, 1 << 20, 0), (33, 49, 123457, 0)])
+def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, total, S, align):
+    torch = torch_dev
+    from slime_amd import device as D
+    from test_gpu_parity import _make_chunked_slots, _make_slots
+    rng = np.random.default_rng(S + total)
+    objs = _byte_objects(rng, S, 3)
+    if align:
+        slots, L, chunk, stride = _make_chunked_slots(torch, objs, need, total, align)
+        cs = dict(chunk_stride=chunk)
+    else:
+        slots, L, chunk, stride = _make_slots(torch, objs, need, total)
+        cs = {}
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(3, dtype=torch.int32, device="cuda")
+    status = torch.empty(3, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, 3, mapping, status, **cs)
+    torch.cuda.synchronize()
+    truth = slots.clone()
+    r = total - need
+    for erase in (list(range(min(r, 16))), sorted(rng.choice(total, size=min(r, 20), replace=False).tolist()),
+                  [need - 1, total - 1][: r]):
+        have = [i for i in range(total) if i not in erase]
+        rng.shuffle(have)
+        have = have[:need]
+        rec = D.Plan.reconstruct(need, total, have, erase).set_outputs(erase)
+        v = slots.view(3, stride)[:, : total * chunk].view(3, total, chunk)
+        v[:, erase, : 4 * L] = 0x5A
+        D.decode_objects(rec, slots, stride, L, 3, mapping, **cs)
+        torch.cuda.synchronize()
+        assert torch.equal(slots, truth), erase

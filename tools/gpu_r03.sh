@@ -64,6 +64,15 @@ for step in "$@"; do
               run wide_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WIDE || exit 1
             done
           done ;;
+    # wide codes on the fused byte path (object_bytes_path leg), matrix cores vs VALU
+    widebytes) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          WB="--steps 3 --warmup 1 $NOLEGS"
+          for shp in "64 80 $E16" "80 100 $E16,16,17,18,19" "40 56 $E16"; do
+            set -- $shp
+            for v in "mfma:SLIME_RS_MFMA=1" "valu:SLIME_RS_MFMA=0"; do
+              run wbytes_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
+            done
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
