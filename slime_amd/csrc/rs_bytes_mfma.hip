@@ -15,6 +15,7 @@
 // data-chunk tails MapFromGF writes) and column tails take the VALU step of
 // the wide byte kernels (encode_wide_step, rs_bytes_kernel.hpp).
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 #include "kernels.hpp"
 #include "rs_apply_mfma_kernel.hpp"
@@ -26,16 +27,43 @@ namespace bytes {
 using apply::i32x4;
 using apply::MfmaIO;
 
-// MapToGF's flags over every loaded data word (encode, speculative pass).
+// MapToGF's flags over every loaded data word (encode, speculative pass) in
+// two registers: the unsigned maximum of the words (bit0: >= p) and their
+// signed maximum (the unsigned maximum of word ^ 1<<31; bit1: >= p) --
+// a byte swap and two max per word.
 struct FlagPre {
-  Flags* fl;
+  uint32_t umax = 0;
+  int32_t smax = INT32_MIN;
   template <class V>
   __device__ __forceinline__ void operator()(const V& v) {
     constexpr int W = sizeof(V) / sizeof(uint32_t);
 #pragma unroll
-    for (int c = 0; c < W; ++c) fl->add(c & 3, be(v[c]));
+    for (int c = 0; c < W; ++c) {
+      const uint32_t w = be(v[c]);
+      umax = umax > w ? umax : w;
+      smax = smax > (int32_t)w ? smax : (int32_t)w;
+    }
+  }
+  __device__ __forceinline__ uint32_t bits() const {
+    return (umax >= kP ? 1u : 0u) | (((uint32_t)smax ^ 0x80000000u) >= kP ? 2u : 0u);
   }
 };
+
+// The edge steps of one segment (vectors [e0, u1)), out of line: inlined,
+// their registers would crowd the matrix-core walk's (two waves per SIMD).
+template <bool F>
+__device__ __forceinline__ uint32_t encode_edges(uint8_t* slot, uint8_t* par, uint64_t chunk, uint64_t L, uint64_t col0,
+                                              ObjWords ow, uint64_t first_tail_word, uint32_t m, uint32_t rows,
+                                              uint32_t k, uint32_t cs, const uint32_t* __restrict__ coeff,
+                                              const uint32_t* __restrict__ out_idx, uint64_t e0, uint64_t nvec,
+                                              uint64_t u1, uint64_t seg_v1, uint32_t lane, uint32_t wave,
+                                              uint32_t nwaves) {
+  Flags fl;
+  for (uint64_t gv = e0 + (uint64_t)wave * 64 + lane; gv - lane < u1; gv += (uint64_t)nwaves * 64)
+    encode_wide_step<16, 8, F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, gv, nvec,
+                               u1, seg_v1, lane, fl);
+  return F ? fl.bits() : 0u;
+}
 
 // MODE 0: speculative pass (mapping 0, MapToGF flags into flags[obj]);
 // MODE 1: re-encode of the objects select_mapping gave mapping != 0 (status 0).
@@ -81,15 +109,16 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
     if (end_max > v1) end_max = v1;
     const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / TCV) : 0u;
-    Flags fl;
     const MfmaIO io{0x80808080u ^ be(m), m};
+    uint32_t fbits = 0;
     if (nint) {
       if constexpr (F) {
-        FlagPre pre{&fl};
+        FlagPre pre;
         apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
                                                         reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT, rows,
                                                         lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io,
                                                         pre);
+        fbits = pre.bits();
       } else {
         apply::NoPre pre;
         apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
@@ -99,13 +128,12 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
       }
     }
     // Edge tiles and tail columns (VALU step, with the data-chunk tail fix).
-    for (uint64_t gv = (uint64_t)v0 + (uint64_t)nint * TCV + (uint64_t)wave * 64 + lane; gv - lane < u1;
-         gv += (uint64_t)nwaves * 64)
-      encode_wide_step<16, 8, F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, gv,
-                                 nvec, u1, sg.v1, lane, fl);
+    const uint64_t e0 = (uint64_t)v0 + (uint64_t)nint * TCV;
+    if (e0 < u1)
+      fbits |= encode_edges<F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, e0, nvec,
+                               u1, sg.v1, lane, wave, nwaves);
     if constexpr (F) {
-      const uint32_t f = fl.bits();
-      const uint64_t a1 = __ballot(f & 1u), a2 = __ballot(f & 2u);
+      const uint64_t a1 = __ballot(fbits & 1u), a2 = __ballot(fbits & 2u);
       const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
       if (wf && lane == 0) atomicOr(&flags[obj], wf);
     }
@@ -194,10 +222,14 @@ hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The refill form (2) is the product; env SLIME_RS_MFMA_MODE picks 0/1 for A/B.
+// The refill form (2) is the product for the decode and the re-encode; the
+// speculative encode takes the no-prefetch form (0): with the MapToGF flags
+// the refill form needs more than 256 VGPRs at four K steps and spills.  Env
+// SLIME_RS_MFMA_MODE=0/1 forces a form for A/B.
 template <int KS>
 hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
-  switch (mfma_kernel_form()) {
+  const int form = mfma_kernel_form();
+  switch (form == 2 && a.phase == 0 ? 0 : form) {
     case 0: return enc_form<KS, 0>(a, s);
     case 1: return enc_form<KS, 1>(a, s);
     default: return enc_form<KS, 2>(a, s);

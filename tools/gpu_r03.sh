@@ -58,9 +58,9 @@ for step in "$@"; do
     wide) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
           E20=$E16,16,17,18,19
           WIDE="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
-          for shp in "64 80 $E16" "48 64 $E16" "80 100 $E20" "96 100 0,1,2,3" "40 48 0,1,2,3,4,5,6,7"; do
+          for shp in "64 80 $E16" "48 64 $E16" "80 100 $E20" "40 48 0,1,2,3,4,5,6,7"; do
             set -- $shp
-            for v in "m2:SLIME_RS_MFMA_MODE=2" "m1:SLIME_RS_MFMA_MODE=1" "m0:SLIME_RS_MFMA_MODE=0" "valu:SLIME_RS_MFMA=0"; do
+            for v in "queue:SLIME_RS_MFMA_MODE=2" "static:SLIME_RS_MFMA_QUEUE=0" "m0:SLIME_RS_MFMA_MODE=0" "valu:SLIME_RS_MFMA=0"; do
               run wide_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WIDE || exit 1
             done
           done ;;
