@@ -67,62 +67,13 @@ void launch_mode(const ApplyLaunch& a, hipStream_t stream, dim3 grid, uint32_t l
                      a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
 }
 
-// Dynamic schedule (rs_apply_mfma_queue_kernel) for the refill form, unless
-// the schedule is static (slime_rs_kernel_schedule(0)) or env
-// SLIME_RS_MFMA_QUEUE=0 (A/B).  A unit is C tiles: 4 KiB of every shard.
-bool mfma_queue() {
-  static const bool on = [] {
-    const char* e = getenv("SLIME_RS_MFMA_QUEUE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-template <int KS>
-constexpr int queue_tiles() {
-  return 64 / apply::mfma_width(KS);  // 16 tiles of 256 B, or 32 of 128 B, per shard
-}
-// Segments per object (TicketWalk spread, as queue_spread in kernels.hpp for
-// this kernel's tiles): ceil(64 / nobj) capped at the object's groups; 0 when
-// the launch has too many units for 32-bit tickets.
-uint32_t mfma_spread(uint32_t nobj, uint64_t ncols, uint32_t tc, int C) {
-  const uint64_t ntiles = ((ncols >> 2) * 4 + tc - 1) / tc;
-  const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
-  uint64_t S = (64 + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
-  if (S > groups) S = groups ? groups : 1;
-  const uint64_t B = (groups + S - 1) / S;
-  if ((uint64_t)nobj * S * B * 4 >= (1ull << 32)) return 0;
-  return (uint32_t)S;
-}
-
-template <int KS>
-hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, uint32_t lds, bool* launched) {
-  constexpr int C = queue_tiles<KS>();
-  *launched = false;
-  const uint32_t spread = mfma_spread(a.nobj, a.ncols, 16 * apply::mfma_width(KS), C);
-  if (!spread) return hipSuccess;
-  const ApplyGeometry& geo = apply_geometry();
-  const uint64_t blocks = geo.target ? geo.target : 256ull * apply::mfma_waves(KS, 2);
-  return with_tickets(
-      stream,
-      [&](uint32_t* set) {
-        hipLaunchKernelGGL((apply::rs_apply_mfma_queue_kernel<KS, kNtLoads, kNtStores, C, kQueueCounters>),
-                           dim3((uint32_t)blocks), dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride,
-                           a.in_shard_stride, a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx,
-                           a.out_idx, a.ncols, a.nobj, a.rows, a.k, set, spread);
-        return hipGetLastError();
-      },
-      launched);
-}
-
+// Static tile walk only: a dynamic-schedule form (TicketWalk units of 4 KiB
+// per shard, the refill streaming across objects) measured 0-6% slower than
+// this walk at 40/48, 48/64, 64/80 and 80/100 (profiles/r03/s33_mfma_queue_bytes/).
 template <int KS>
 hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint32_t mt = mfma::mtiles(a.rows);
   const uint32_t lds = apply::mfma_lds_bytes(mt, KS);
-  if (mfma_kernel_form() == 2 && mfma_queue() && queue_allowed(stream)) {
-    bool launched = false;
-    const hipError_t e = launch_queue<KS>(a, stream, lds, &launched);
-    if (launched || e != hipSuccess) return e;
-  }
   const uint64_t per_block = 4ull * 16 * 4;  // 4 waves x 16 vectors
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;

@@ -312,68 +312,5 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_wav
   }
 }
 
-// Dynamic schedule (as rs_apply_queue_kernel): waves take units of C tiles
-// from the ticket counters of TicketWalk, so the XCDs that stream faster take
-// more of the batch; the refill form streams the next tile -- possibly of
-// another object -- behind the current one's math.  Tiles of 16W columns per
-// object; columns past the last whole vector go one per lane at the end.
-template <int KS, bool NTL, bool NTS, int C, int NC>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, 2)))) void
-rs_apply_mfma_queue_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride,
-                           uint64_t in_shard, uint64_t out_obj_stride, uint64_t out_shard,
-                           const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
-                           const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols,
-                           uint32_t nobj, uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint32_t spread) {
-  constexpr int W = mfma_width(KS);
-  constexpr uint32_t TC = 16 * W;
-  extern __shared__ i32x4 lds[];
-  const uint32_t MT = (rows + 3) / 4;
-  const uint32_t lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
-  uint64_t* lrowc;
-  uint32_t* loff;
-  uint32_t soff[KS][4];
-  mfma_prologue<KS>(lds, table, in_idx, out_idx, in_shard * 4, out_shard * 4, MT, rows, k, g, &lrowc, &loff, soff);
-  const uint32_t nvec = (uint32_t)(ncols >> 2);
-  const uint32_t c1 = nvec << 2;  // whole-vector columns
-  const uint32_t ntiles = (c1 + TC - 1) / TC;
-  const MfmaIO io{0x80808080u, 0u};
-  NoPre pre;
-  auto ibase = [&](uint32_t o) { return reinterpret_cast<const char*>(in + (uint64_t)o * in_obj_stride); };
-  auto colb_of = [&](uint32_t t) {
-    const uint32_t c = t * TC + n * W;
-    return (c < c1 ? c : c1 - W) << 2;
-  };
-  TicketWalk<C, NC> w(ticket, nobj, ntiles, lane, spread);
-  if (w.live) {
-    vec_t<W> x[KS][4];
-    mfma_load_tile<KS, W, NTL>(x, ibase(w.obj), soff, colb_of(w.tile()));
-    for (;;) {
-      const uint32_t co = w.obj, ct = w.tile();
-      char* const ob = reinterpret_cast<char*>(out + (uint64_t)co * out_obj_stride);
-      const bool st = ct * TC + n * W < c1;
-      w.advance();
-      if (w.live) {
-        mfma_tile<KS, W, NTL, NTS, true, false>(x, ibase(w.obj), soff, colb_of(w.tile()), lds, lrowc, loff, MT, rows,
-                                                lane, g, ob, colb_of(ct), st, io, pre);
-      } else {
-        mfma_tile<KS, W, NTL, NTS, false, false>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, g, ob,
-                                                 colb_of(ct), st, io, pre);
-        break;
-      }
-    }
-  }
-  w.finish();
-  const uint32_t tailc = (uint32_t)(ncols - c1);
-  if (tailc) {
-    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t t = tid; t < (uint64_t)nobj * tailc; t += nthr) {
-      const uint64_t o = t / tailc;
-      apply_column<0>(in + o * in_obj_stride, out + o * out_obj_stride, coeff, in_idx, in_shard, out_idx, out_shard,
-                      rows, k, (uint64_t)c1 + t % tailc);
-    }
-  }
-}
-
 }  // namespace apply
 }  // namespace slime

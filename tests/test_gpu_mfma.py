@@ -31,17 +31,13 @@ def torch_dev():
     return torch
 
 
-@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["mfma-queue", "mfma-static", "valu"])
+@pytest.fixture(params=[1, 0], ids=["mfma", "valu"])
 def matrix_cores(request):
-    """Matrix cores with the dynamic schedule (product), with static shares
-    (slime_rs_kernel_schedule(0)), and the VALU kernels."""
-    mode, sched = request.param
-    prev = N.lib.slime_rs_kernel_matrix_cores(-1), N.lib.slime_rs_kernel_schedule(-1)
-    N.check(N.lib.slime_rs_kernel_matrix_cores(mode))
-    N.check(N.lib.slime_rs_kernel_schedule(sched))
-    yield mode
-    N.check(N.lib.slime_rs_kernel_matrix_cores(prev[0]))
-    N.check(N.lib.slime_rs_kernel_schedule(prev[1]))
+    """Matrix cores (product for k >= 33) and the VALU kernels."""
+    prev = N.lib.slime_rs_kernel_matrix_cores(-1)
+    N.check(N.lib.slime_rs_kernel_matrix_cores(request.param))
+    yield request.param
+    N.check(N.lib.slime_rs_kernel_matrix_cores(prev))
 
 
 def _rand(rng, shape):

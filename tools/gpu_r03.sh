@@ -73,6 +73,13 @@ for step in "$@"; do
               run wbytes_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
             done
           done ;;
+    # the matrix-core kernel on the BASELINE shapes (SLIME_RS_MFMA_MINK=1), symbol path only
+    mink1) run mink1_c3 300 env SLIME_RS_MFMA_MINK=1 python bench.py --bytes-path 0 --steps 5 $NOLEGS &&
+           run mink1_c5 300 env SLIME_RS_MFMA_MINK=1 python bench.py --preset c5 --global-objects 16 --bytes-path 0 --steps 5 $NOLEGS &&
+           run mink1_c2 300 env SLIME_RS_MFMA_MINK=1 python bench.py --preset c2 --bytes-path 0 --steps 5 $NOLEGS ;;
+    # kernel times of the wide byte path (64/80, 32 x 256 MiB): rocprofv3 stats
+    wprof) run wprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof" -o bench --output-format csv -- \
+             python3 bench.py --need 64 --total 80 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --warmup 1 $NOLEGS ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
