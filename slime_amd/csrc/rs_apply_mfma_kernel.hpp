@@ -59,9 +59,12 @@ __device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
 // Waves per SIMD the kernel is compiled for (registers permitting): two for
 // the no-prefetch and refill forms (W = 4 up to k = 64, W = 2 above: at most
 // 64 data VGPRs, the accumulators in VGPRs), two for the two-buffer form up
-// to two K steps, else one.
+// to two K steps, else one; form 3 is the refill form at one wave per SIMD
+// (for kernels whose extra state does not fit two).
 __host__ __device__ constexpr int mfma_width(int ks) { return ks <= 4 ? 4 : 2; }
-__host__ __device__ constexpr int mfma_waves(int ks, int mode) { return mode != 1 || ks <= 2 ? 2 : 1; }
+__host__ __device__ constexpr int mfma_waves(int ks, int mode) {
+  return mode == 3 ? 1 : (mode != 1 || ks <= 2 ? 2 : 1);
+}
 
 template <int W>
 using vec_t = uint32_t __attribute__((ext_vector_type(W)));
@@ -216,7 +219,7 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
                                                col_of(t) < c1, io, pre);
       t = t2;
     }
-  } else if constexpr (MODE == 2) {
+  } else if constexpr (MODE == 2 || MODE == 3) {
     vec_t<W> x[KS][4];
     uint32_t t = wave;
     if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));

@@ -91,6 +91,58 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
+  // Re-encode of up to 64 objects (one segment each): one flat tile walk over
+  // the interior tiles of every object select_mapping gave 1<<31, so the grid
+  // streams them back to back (the refill crosses objects) instead of
+  // restarting its walk per object; then their edge steps.
+  bool flat = false;
+  if constexpr (MODE == 1) {
+    if (nobj <= 64 && nseg == 1) {
+      flat = true;
+      const bool selm = lane < nobj && mapping[lane] != 0 && flags[lane] == 0;
+      const uint64_t sel = __ballot(selm);
+      const uint32_t count = (uint32_t)__popcll(sel);
+      const uint64_t lim = (uint64_t)(k - 1) * L + col0;
+      uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+      if (end_max > nvec) end_max = nvec;
+      const uint32_t nint = (uint32_t)(end_max / TCV);
+      auto nth = [&](uint32_t i) {  // object of the i-th selected slot
+        uint64_t b = sel;
+        for (uint32_t q = 0; q < i; ++q) b &= b - 1;
+        return (uint32_t)__builtin_ctzll(b);
+      };
+      auto slot_of = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
+      auto colb_of = [&](uint32_t t) { return ((t % nint) * (16 * W) + ln * W) << 2; };
+      const uint32_t T = count * nint;
+      apply::NoPre pre;
+      uint32_t t = wave;
+      apply::vec_t<W> x[KS][4];
+      if (t < T) apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(nth(t / nint))), soff,
+                                                    colb_of(t));
+      while (t < T) {
+        const uint32_t tn = t + nwaves;
+        const uint32_t o = nth(t / nint);
+        const uint32_t mo = mapping[o];
+        const MfmaIO io{0x80808080u ^ be(mo), mo};
+        char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
+        if (tn < T)
+          apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(nth(tn / nint))),
+                                                          soff, colb_of(tn), lds, lrowc, loff, MT, rows, lane, lg, ob,
+                                                          colb_of(t), true, io, pre);
+        else
+          apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg,
+                                                           ob, colb_of(t), true, io, pre);
+        t = tn;
+      }
+      for (uint32_t i = 0; i < count; ++i) {
+        const uint32_t o = nth(i);
+        uint8_t* const slot = slot_of(o);
+        (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word, mapping[o],
+                                  rows, k, cs, coeff, out_idx, (uint64_t)nint * TCV, nvec,
+                                  nvec + (ncols & 3), nvec, lane, wave, nwaves);
+      }
+    }
+  }
   for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
     const Segment sg = segment_of(wi, nseg, nvec);
     const uint32_t obj = sg.obj;
@@ -98,6 +150,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
     uint32_t m = 0;
     if constexpr (MODE == 1) {
+      if (flat) break;  // the flat walk below did every object
       m = mapping[obj];
       if (m == 0 || flags[obj] != 0) continue;  // uniform per block
     }
@@ -225,11 +278,19 @@ hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
 // The refill form (2) is the product for the decode and the re-encode; the
 // speculative encode takes the no-prefetch form (0): with the MapToGF flags
 // the refill form needs more than 256 VGPRs at four K steps and spills.  Env
-// SLIME_RS_MFMA_MODE=0/1 forces a form for A/B.
+// SLIME_RS_MFMA_ENC_FORM=3 runs it on the refill form at one wave per SIMD
+// instead, SLIME_RS_MFMA_MODE=0/1 forces a form elsewhere (A/B only).
+int enc_form0() {
+  static const int f = [] {
+    const char* e = getenv("SLIME_RS_MFMA_ENC_FORM");
+    return e && e[0] == '3' ? 3 : 0;
+  }();
+  return f;
+}
 template <int KS>
 hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
-  const int form = mfma_kernel_form();
-  switch (form == 2 && a.phase == 0 ? 0 : form) {
+  if (a.phase == 0) return enc_form0() == 3 ? enc_form<KS, 3>(a, s) : enc_form<KS, 0>(a, s);
+  switch (mfma_kernel_form()) {
     case 0: return enc_form<KS, 0>(a, s);
     case 1: return enc_form<KS, 1>(a, s);
     default: return enc_form<KS, 2>(a, s);

@@ -69,7 +69,7 @@ for step in "$@"; do
           WB="--steps 3 --warmup 1 $NOLEGS"
           for shp in "64 80 $E16" "80 100 $E16,16,17,18,19" "40 56 $E16"; do
             set -- $shp
-            for v in "mfma:SLIME_RS_MFMA=1" "valu:SLIME_RS_MFMA=0"; do
+            for v in "mfma:SLIME_RS_MFMA=1" "mfma_enc3:SLIME_RS_MFMA_ENC_FORM=3" "valu:SLIME_RS_MFMA=0"; do
               run wbytes_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
             done
           done ;;
