@@ -112,26 +112,43 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
         return (uint32_t)__builtin_ctzll(b);
       };
       auto slot_of = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
-      auto colb_of = [&](uint32_t t) { return ((t % nint) * (16 * W) + ln * W) << 2; };
+      // The flat tile space f < T (object nth(f / nint), tile f % nint) is cut
+      // into G contiguous streams walked by 8 waves each, as the speculative
+      // pass's segments are: all waves on one window of one object streamed
+      // at 2.3 TB/s (profiles/r03/s35_mfma_bytes/).
       const uint32_t T = count * nint;
+      const uint32_t G = nwaves / 8 ? nwaves / 8 : 1;
+      const uint32_t len = (T + G - 1) / G;
+      auto flat = [&](uint32_t t) { return (t % G) * len + t / G; };  // < T for every visited t
+      auto colb_of = [&](uint32_t f) { return ((f % nint) * (16 * W) + ln * W) << 2; };
+      auto next = [&](uint32_t t) {  // the wave's next visited index (or >= G * len)
+        for (t += nwaves; t < G * len && flat(t) >= T; t += nwaves) {
+        }
+        return t;
+      };
       apply::NoPre pre;
       uint32_t t = wave;
+      if (t < G * len && flat(t) >= T) t = next(t);
       apply::vec_t<W> x[KS][4];
-      if (t < T) apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(nth(t / nint))), soff,
-                                                    colb_of(t));
-      while (t < T) {
-        const uint32_t tn = t + nwaves;
-        const uint32_t o = nth(t / nint);
+      if (t < G * len)
+        apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(nth(flat(t) / nint))), soff,
+                                           colb_of(flat(t)));
+      while (t < G * len) {
+        const uint32_t tn = next(t);
+        const uint32_t f = flat(t);
+        const uint32_t o = nth(f / nint);
         const uint32_t mo = mapping[o];
         const MfmaIO io{0x80808080u ^ be(mo), mo};
         char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
-        if (tn < T)
-          apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(nth(tn / nint))),
-                                                          soff, colb_of(tn), lds, lrowc, loff, MT, rows, lane, lg, ob,
-                                                          colb_of(t), true, io, pre);
-        else
+        if (tn < G * len) {
+          const uint32_t fn = flat(tn);
+          apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(nth(fn / nint))),
+                                                          soff, colb_of(fn), lds, lrowc, loff, MT, rows, lane, lg, ob,
+                                                          colb_of(f), true, io, pre);
+        } else {
           apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg,
-                                                           ob, colb_of(t), true, io, pre);
+                                                           ob, colb_of(f), true, io, pre);
+        }
         t = tn;
       }
       for (uint32_t i = 0; i < count; ++i) {
