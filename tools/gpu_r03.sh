@@ -80,6 +80,11 @@ for step in "$@"; do
     # kernel times of the wide byte path (64/80, 32 x 256 MiB): rocprofv3 stats
     wprof) run wprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof" -o bench --output-format csv -- \
              python3 bench.py --need 64 --total 80 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --warmup 1 $NOLEGS ;;
+    # C2 and buffer placement: the default (2 MiB chunks, unprobed below 16 GiB), probed, hipMalloc
+    c2place) run c2p_default 300 python bench.py --preset c2 --bytes-path 0 --steps 10 $NOLEGS &&
+             run c2p_probe1 300 env SLIME_RS_PLACEMENT_PROBE_GIB=1 python bench.py --preset c2 --bytes-path 0 --steps 10 $NOLEGS &&
+             run c2p_torch 300 python bench.py --preset c2 --allocator torch --bytes-path 0 --steps 10 $NOLEGS &&
+             run c2p_default2 300 python bench.py --preset c2 --bytes-path 0 --steps 10 $NOLEGS ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
