@@ -85,6 +85,16 @@ for step in "$@"; do
              run c2p_probe1 300 env SLIME_RS_PLACEMENT_PROBE_GIB=1 python bench.py --preset c2 --bytes-path 0 --steps 10 $NOLEGS &&
              run c2p_torch 300 python bench.py --preset c2 --allocator torch --bytes-path 0 --steps 10 $NOLEGS &&
              run c2p_default2 300 python bench.py --preset c2 --bytes-path 0 --steps 10 $NOLEGS ;;
+    # matrix-core kernel geometry: column segments per object (window per shard) x grid
+    mfmageo) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          G="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
+          for sg in 1 2 4 8 16; do
+            run mgeo_6480_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
+          done
+          for sg in 1 2 4; do
+            run mgeo_6480_s${sg}_g1024 300 env SLIME_RS_SEGMENTS=$sg SLIME_RS_GRID_TARGET=1024 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
+            run mgeo_80100_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 80 --total 100 --objects 32 --erase $E16,16,17,18,19 $G || exit 1
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
