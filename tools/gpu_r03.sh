@@ -95,6 +95,13 @@ for step in "$@"; do
             run mgeo_6480_s${sg}_g1024 300 env SLIME_RS_SEGMENTS=$sg SLIME_RS_GRID_TARGET=1024 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
             run mgeo_80100_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 80 --total 100 --objects 32 --erase $E16,16,17,18,19 $G || exit 1
           done ;;
+    # 17 <= k <= 32: matrix cores (SLIME_RS_MFMA_MINK=17) vs the VALU k-template kernels
+    mfmak32) G="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
+          for shp in "32 40 0,1,2,3,4,5,6,7" "24 32 0,1,2,3,4,5,6,7" "20 24 0,1,2,3" "17 20 0,1,2"; do
+            set -- $shp
+            run mk32_$1_$2_mfma 300 env SLIME_RS_MFMA_MINK=17 python bench.py --need $1 --total $2 --objects 32 --erase $3 $G || exit 1
+            run mk32_$1_$2_valu 300 python bench.py --need $1 --total $2 --objects 32 --erase $3 $G || exit 1
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
