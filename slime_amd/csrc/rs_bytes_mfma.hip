@@ -99,7 +99,8 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   if constexpr (MODE == 1) {
     if (nobj <= 64 && nseg == 1) {
       flat = true;
-      const bool selm = lane < nobj && mapping[lane] != 0 && flags[lane] == 0;
+      const uint32_t mlane = lane < nobj ? mapping[lane] : 0u;  // object `lane`'s mapping, read once
+      const bool selm = lane < nobj && mlane != 0 && flags[lane] == 0;
       const uint64_t sel = __ballot(selm);
       const uint32_t count = (uint32_t)__popcll(sel);
       const uint64_t lim = (uint64_t)(k - 1) * L + col0;
@@ -137,7 +138,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
         const uint32_t tn = next(t);
         const uint32_t f = flat(t);
         const uint32_t o = nth(f / nint);
-        const uint32_t mo = mapping[o];
+        const uint32_t mo = __builtin_amdgcn_readlane(mlane, o);  // no memory round trip per tile
         const MfmaIO io{0x80808080u ^ be(mo), mo};
         char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
         if (tn < G * len) {
@@ -151,12 +152,15 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
         }
         t = tn;
       }
+      // Edge steps: object i's on waves offset by i * nwaves / count, so the
+      // objects' (serial, VALU) edge steps run side by side.
       for (uint32_t i = 0; i < count; ++i) {
         const uint32_t o = nth(i);
         uint8_t* const slot = slot_of(o);
-        (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word, mapping[o],
-                                  rows, k, cs, coeff, out_idx, (uint64_t)nint * TCV, nvec,
-                                  nvec + (ncols & 3), nvec, lane, wave, nwaves);
+        const uint32_t wrel = (wave + nwaves - (uint32_t)((uint64_t)i * nwaves / count)) % nwaves;
+        (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word,
+                                  __builtin_amdgcn_readlane(mlane, o), rows, k, cs, coeff, out_idx,
+                                  (uint64_t)nint * TCV, nvec, nvec + (ncols & 3), nvec, lane, wrel, nwaves);
       }
     }
   }
