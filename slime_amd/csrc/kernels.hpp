@@ -45,8 +45,9 @@ bool mfma_eligible(const ApplyLaunch& a);
 hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream);
 int matrix_core_mode();
 void set_matrix_core_mode(int m);
-// Smallest k that takes the matrix cores (env SLIME_RS_MFMA_MINK, tuning;
-// default 33) and the kernel form (env SLIME_RS_MFMA_MODE: 2 K-step refill,
+// Smallest k whose byte-path launches take the matrix cores (env
+// SLIME_RS_MFMA_MINK, tuning; default 33: the symbol path also takes them for
+// 17 <= k <= 32 when k * rows >= 128, rs_apply_mfma.hip) and the kernel form (env SLIME_RS_MFMA_MODE: 2 K-step refill,
 // the product; 1 two tile buffers; 0 no prefetch).
 uint32_t mfma_min_k();
 int mfma_kernel_form();

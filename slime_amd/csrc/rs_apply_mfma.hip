@@ -22,17 +22,29 @@ static std::atomic<int> g_mfma{[] {
 }()};
 int matrix_core_mode() { return g_mfma.load(std::memory_order_relaxed); }
 void set_matrix_core_mode(int m) { g_mfma.store(m, std::memory_order_relaxed); }
-uint32_t mfma_min_k() {
+// SLIME_RS_MFMA_MINK, or 0 when unset (the product rule below).
+static uint32_t forced_min_k() {
   static const uint32_t v = [] {
     const char* e = getenv("SLIME_RS_MFMA_MINK");
     const long long x = e ? atoll(e) : 0;
-    return x > 0 ? (uint32_t)x : 33u;
+    return x > 0 ? (uint32_t)x : 0u;
   }();
   return v;
 }
+uint32_t mfma_min_k() { return forced_min_k() ? forced_min_k() : 33u; }
+
+// Which launches take the matrix cores (product rule, measured on one box,
+// profiles/r03/s37_mfma_k32/): every k >= 33, and 17 <= k <= 32 when the
+// column's k x rows multiply-accumulates reach 128 -- 24/32 0.646 -> 0.739,
+// 32/40 0.676 -> 0.738, while 20/24 (80 per column) ties and 17/20 (51)
+// loses 4% (0.739 -> 0.709).
+static bool mfma_wanted(uint32_t k, uint32_t rows) {
+  if (forced_min_k()) return k >= forced_min_k();
+  return k >= 33 || (k >= 17 && k * rows >= 128);
+}
 
 bool mfma_eligible(const ApplyLaunch& a) {
-  if (!a.mfma || !a.vec_ok || !matrix_core_mode() || a.k < mfma_min_k()) return false;
+  if (!a.mfma || !a.vec_ok || !matrix_core_mode() || !mfma_wanted(a.k, a.rows)) return false;
   if (!mfma::supported(a.rows, a.k)) return false;
   // 32-bit per-lane byte offsets from each object's base (see the kernel).
   const uint64_t lim = 1ull << 32;

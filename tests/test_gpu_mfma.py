@@ -1,5 +1,6 @@
 """GPU parity of the matrix-core apply kernel (rs_apply_mfma.hip): wide codes
-(k >= 33, up to 32 output rows) as an exact int8-limb product on
+(k >= 33, and 17 <= k <= 32 with k x rows >= 128; up to 32 output rows) as an
+exact int8-limb product on
 v_mfma_i32_16x16x64_i8, against the C oracle (applyMatrix,
 internal/rs/vector.go:90-102) and against the VALU kernels in the same process
 (slime_rs_kernel_matrix_cores 0/1).  Bit-exact: integer field arithmetic.
@@ -59,7 +60,7 @@ def _apply_ref(coeff, x):
 
 
 @pytest.mark.parametrize("need,total", [(33, 34), (33, 50), (40, 56), (47, 48), (48, 64), (64, 80), (80, 100),
-                                        (64, 96), (99, 100)])
+                                        (64, 96), (99, 100), (17, 25), (24, 32), (31, 40), (20, 24)])
 @pytest.mark.parametrize("L", [1, 5, 64, 67, 1001, 4096 + 3])
 def test_encode_vs_oracle(torch_dev, matrix_cores, need, total, L):
     torch = torch_dev
