@@ -102,6 +102,14 @@ for step in "$@"; do
             run mk32_$1_$2_mfma 300 env SLIME_RS_MFMA_MINK=17 python bench.py --need $1 --total $2 --objects 32 --erase $3 $G || exit 1
             run mk32_$1_$2_valu 300 python bench.py --need $1 --total $2 --objects 32 --erase $3 $G || exit 1
           done ;;
+    # HBM traffic of the matrix-core kernels (FETCH_SIZE / WRITE_SIZE passes): 64/80 with the byte leg, 40/48 symbol only
+    wpmc) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          W6480="python3 bench.py --need 64 --total 80 --objects 32 --erase $E16 --steps 2 --warmup 1 $NOLEGS"
+          W4048="python3 bench.py --need 40 --total 48 --objects 32 --erase 0,1,2,3,4,5,6,7 --steps 2 --warmup 1 --bytes-path 0 $NOLEGS"
+          run wpmc_6480_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/wpmc_6480_fetch" -o pmc --output-format csv -- $W6480 &&
+          run wpmc_6480_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/wpmc_6480_write" -o pmc --output-format csv -- $W6480 &&
+          run wpmc_4048_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/wpmc_4048_fetch" -o pmc --output-format csv -- $W4048 &&
+          run wpmc_4048_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/wpmc_4048_write" -o pmc --output-format csv -- $W4048 ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
