@@ -51,6 +51,9 @@ void set_matrix_core_mode(int m);
 // the product; 1 two tile buffers; 0 no prefetch).
 uint32_t mfma_min_k();
 int mfma_kernel_form();
+// The product rule (rs_apply_mfma.hip): k >= 33, or 17 <= k <= 32 with
+// k * rows >= 128 multiply-accumulates per column; SLIME_RS_MFMA_MINK forces k >= n.
+bool mfma_wanted(uint32_t k, uint32_t rows);
 
 // Row stride (words) of a device coefficient table: k rounded up to 16 words,
 // so every 16-coefficient chunk of a row is one aligned s_load_dwordx16.
@@ -184,8 +187,10 @@ inline dim3 bytes_grid(uint64_t ncols, uint64_t work, uint32_t nseg, uint64_t ta
 }
 hipError_t launch_decode_bytes(const BytesLaunch& a, hipStream_t stream);
 // Wide codes on the matrix cores (rs_bytes_mfma.hip): eligibility (table,
-// mode, k >= mfma_min_k(), shape, chunk offsets under 4 GiB) and the launches.
-bool bytes_mfma_eligible(const BytesLaunch& a);
+// mode, mfma_wanted -- for the encode only from need 25, below which the VALU
+// queue encode's mid-object switch wins -- shape, chunk offsets under 4 GiB)
+// and the launches.
+bool bytes_mfma_eligible(const BytesLaunch& a, bool encode);
 hipError_t launch_encode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_decode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t stream);

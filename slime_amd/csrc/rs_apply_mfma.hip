@@ -38,7 +38,7 @@ uint32_t mfma_min_k() { return forced_min_k() ? forced_min_k() : 33u; }
 // column's k x rows multiply-accumulates reach 128 -- 24/32 0.646 -> 0.739,
 // 32/40 0.676 -> 0.738, while 20/24 (80 per column) ties and 17/20 (51)
 // loses 4% (0.739 -> 0.709).
-static bool mfma_wanted(uint32_t k, uint32_t rows) {
+bool mfma_wanted(uint32_t k, uint32_t rows) {
   if (forced_min_k()) return k >= forced_min_k();
   return k >= 33 || (k >= 17 && k * rows >= 128);
 }

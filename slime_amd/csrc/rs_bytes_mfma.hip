@@ -328,8 +328,12 @@ hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
 
 }  // namespace
 
-bool bytes_mfma_eligible(const BytesLaunch& a) {
-  if (!a.mfma || !matrix_core_mode() || a.k < 17 || a.k < mfma_min_k() || !mfma::supported(a.rows, a.k)) return false;
+bool bytes_mfma_eligible(const BytesLaunch& a, bool encode) {
+  if (!a.mfma || !matrix_core_mode() || a.k < 17 || !mfma_wanted(a.k, a.rows) || !mfma::supported(a.rows, a.k))
+    return false;
+  // need 17..24 encodes on the VALU queue kernel, whose mid-object switch
+  // redoes only part of a 1<<31 object (SLIME_RS_MFMA_MINK below 25 forces).
+  if (encode && a.k < 25 && mfma_min_k() >= 25) return false;
   if (!pipelined_kernels()) return false;  // SLIME_RS_PIPE=0 / kernel_pipeline(0): the non-pipelined VALU forms
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   // 32-bit byte offsets from the window base: every chunk the launch reads

@@ -184,7 +184,7 @@ def _byte_objects(rng, S, n):
 
 @pytest.mark.parametrize("need,total,S", [(33, 50, (1 << 20) + 7), (40, 56, 3 * (1 << 20) + 3), (64, 80, (4 << 20) + 1),
                                           (80, 100, 2 << 20), (99, 100, 99999), (47, 48, 65537), (64, 96, 5 << 20),
-                                          (48, 64, 777)])
+                                          (48, 64, 777), (32, 40, (1 << 20) + 3), (28, 36, 77777), (25, 33, 4096)])
 def test_bytes_encode_objects_vs_oracle(torch_dev, matrix_cores, need, total, S):
     torch = torch_dev
     from slime_amd import device as D
@@ -211,7 +211,8 @@ def test_bytes_encode_objects_vs_oracle(torch_dev, matrix_cores, need, total, S)
 
 
 @pytest.mark.parametrize("need,total,S,align", [(64, 80, (2 << 20) + 5, 256), (40, 56, 300001, 4096),
-                                                (80, 100, 1 << 20, 0), (33, 49, 123457, 0)])
+                                                (80, 100, 1 << 20, 0), (33, 49, 123457, 0), (24, 32, 300001, 0),
+                                                (32, 40, 1 << 20, 256), (17, 25, 65537, 0)])
 def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, total, S, align):
     torch = torch_dev
     from slime_amd import device as D

@@ -110,6 +110,14 @@ for step in "$@"; do
           run wpmc_6480_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/wpmc_6480_write" -o pmc --output-format csv -- $W6480 &&
           run wpmc_4048_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/wpmc_4048_fetch" -o pmc --output-format csv -- $W4048 &&
           run wpmc_4048_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/wpmc_4048_write" -o pmc --output-format csv -- $W4048 ;;
+    # 17 <= need <= 32 byte path: matrix cores (product rule) vs VALU
+    widebytes32) WB="--steps 3 --warmup 1 $NOLEGS"
+          for shp in "32 40 0,1,2,3,4,5,6,7" "28 36 0,1,2,3,4,5,6,7" "24 32 0,1,2,3,4,5,6,7"; do
+            set -- $shp
+            for v in "mfma:SLIME_RS_MFMA=1" "valu:SLIME_RS_MFMA=0"; do
+              run wb32_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
+            done
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
