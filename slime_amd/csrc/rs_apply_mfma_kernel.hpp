@@ -56,12 +56,20 @@ __device__ __forceinline__ uint64_t mfma_recombine(const i32x4& d, uint64_t R) {
 __device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
 #endif
 
+#ifndef SLIME_MFMA_W4_MAX_KS
+#define SLIME_MFMA_W4_MAX_KS 4  // 5 (four-column tiles in two passes) spills 9 VGPRs at two waves per SIMD
+#endif
+__host__ __device__ constexpr int mfma_w4_max_ks() { return SLIME_MFMA_W4_MAX_KS; }
+
 // Waves per SIMD the kernel is compiled for (registers permitting): two for
 // the no-prefetch and refill forms (W = 4 up to k = 64, W = 2 above: at most
 // 64 data VGPRs, the accumulators in VGPRs), two for the two-buffer form up
 // to two K steps, else one; form 3 is the refill form at one wave per SIMD
 // (for kernels whose extra state does not fit two).
-__host__ __device__ constexpr int mfma_width(int ks) { return ks <= 4 ? 4 : 2; }
+__host__ __device__ constexpr int mfma_width(int ks) { return ks <= mfma_w4_max_ks() ? 4 : 2; }
+// Column passes per K loop (mfma_rows): 2 where four-column tiles need their
+// accumulators halved to fit two waves per SIMD.
+__host__ __device__ constexpr int mfma_halves(int ks) { return ks > 4 && ks <= mfma_w4_max_ks() ? 2 : 1; }
 __host__ __device__ constexpr int mfma_waves(int ks, int mode) {
   return mode == 3 ? 1 : (mode != 1 || ks <= 2 ? 2 : 1);
 }
@@ -122,45 +130,65 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
                                           const uint32_t* __restrict__ loff, uint32_t mb, uint32_t MT, uint32_t rows,
                                           uint32_t lane, uint32_t g, char* __restrict__ ob, uint32_t colb, bool store,
                                           MfmaIO io, Pre& pre) {
-  i32x4 acc[4][W];
+  // NH passes over the K steps, each for W / NH of the lane's columns (its
+  // accumulators and B fragments shrink by NH; the A fragments are read NH
+  // times from LDS); the results wait in `out` for one W-wide store per row.
+  constexpr int NH = mfma_halves(KS);
+  constexpr int CW = W / NH;
+  uint32_t out[4][W];
 #pragma unroll
-  for (int q = 0; q < KS; ++q) {
-    // B fragments of K step q: b[c] = the lane's four shards at column nW+c.
-    i32x4 b[W];
+  for (int h = 0; h < NH; ++h) {
+    i32x4 acc[4][CW];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      pre(x[q][jj]);
+    for (int q = 0; q < KS; ++q) {
+      // B fragments of K step q: b[c] = the lane's four shards at column nW + h CW + c.
+      i32x4 b[CW];
 #pragma unroll
-      for (int c = 0; c < W; ++c) b[c][jj] = (int)(x[q][jj][c] ^ io.xin);
-    }
-    if constexpr (REFILL) {
+      for (int jj = 0; jj < 4; ++jj) {
+        if (h == 0) pre(x[q][jj]);
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ibn + (uint32_t)(soff[q][jj] + colbn));
+        for (int c = 0; c < CW; ++c) b[c][jj] = (int)(x[q][jj][h * CW + c] ^ io.xin);
+      }
+      if constexpr (REFILL) {
+        if (h == NH - 1) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ibn + (uint32_t)(soff[q][jj] + colbn));
+        }
+      }
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        if (mb + mm < MT) {
+          const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
+#pragma unroll
+          for (int c = 0; c < CW; ++c)
+            acc[mm][c] =
+                __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], q == 0 ? i32x4{0, 0, 0, 0} : acc[mm][c], 0, 0, 0);
+        }
+      }
+      // Keep step q's refill loads in step q: scheduled all at the top they
+      // would double the live data registers (and halve the occupancy).
+      if constexpr (REFILL) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int mm = 0; mm < 4; ++mm) {
-      if (mb + mm < MT) {
-        const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
+      const uint32_t i = 4 * (mb + mm) + g;
+      if (mb + mm < MT && i < rows && store) {
+        const uint64_t R = lrowc[i];
 #pragma unroll
-        for (int c = 0; c < W; ++c)
-          acc[mm][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], q == 0 ? i32x4{0, 0, 0, 0} : acc[mm][c], 0, 0, 0);
+        for (int c = 0; c < CW; ++c) {
+          const uint32_t v = fold96(mfma_recombine(acc[mm][c], R), 0) ^ io.xout;
+          out[mm][h * CW + c] = BSWAP ? __builtin_bswap32(v) : v;
+        }
       }
     }
-    // Keep step q's refill loads in step q: scheduled all at the top they
-    // would double the live data registers (and halve the occupancy).
-    if constexpr (REFILL) __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int mm = 0; mm < 4; ++mm) {
     const uint32_t i = 4 * (mb + mm) + g;
     if (mb + mm < MT && i < rows && store) {
-      const uint64_t R = lrowc[i];
       vec_t<W> r;
 #pragma unroll
-      for (int c = 0; c < W; ++c) {
-        const uint32_t v = fold96(mfma_recombine(acc[mm][c], R), 0) ^ io.xout;
-        r[c] = BSWAP ? __builtin_bswap32(v) : v;
-      }
+      for (int c = 0; c < W; ++c) r[c] = out[mm][c];
       stw<W, NTS>(ob + (uint32_t)(loff[i] + colb), r);
     }
   }

@@ -91,6 +91,7 @@ for step in "$@"; do
           for sg in 1 2 4 8 16; do
             run mgeo_6480_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
           done
+          run mgeo_80100_g768 300 env SLIME_RS_GRID_TARGET=768 python bench.py --need 80 --total 100 --objects 32 --erase $E16,16,17,18,19 $G || exit 1
           for sg in 1 2 4; do
             run mgeo_6480_s${sg}_g1024 300 env SLIME_RS_SEGMENTS=$sg SLIME_RS_GRID_TARGET=1024 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
             run mgeo_80100_s$sg 300 env SLIME_RS_SEGMENTS=$sg python bench.py --need 80 --total 100 --objects 32 --erase $E16,16,17,18,19 $G || exit 1
@@ -118,6 +119,9 @@ for step in "$@"; do
               run wb32_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
             done
           done ;;
+    g768) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
+          run g768_80100 300 env SLIME_RS_GRID_TARGET=768 python bench.py --need 80 --total 100 --objects 32 --erase $E20 --bytes-path 0 --steps 5 --warmup 2 $NOLEGS &&
+          run g512_80100 300 python bench.py --need 80 --total 100 --objects 32 --erase $E20 --bytes-path 0 --steps 5 --warmup 2 $NOLEGS ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
