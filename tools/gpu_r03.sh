@@ -122,6 +122,17 @@ for step in "$@"; do
     g768) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
           run g768_80100 300 env SLIME_RS_GRID_TARGET=768 python bench.py --need 80 --total 100 --objects 32 --erase $E20 --bytes-path 0 --steps 5 --warmup 2 $NOLEGS &&
           run g512_80100 300 python bench.py --need 80 --total 100 --objects 32 --erase $E20 --bytes-path 0 --steps 5 --warmup 2 $NOLEGS ;;
+    # shard strides off the power-of-two grid (--shard-align 192: C3 2^23 -> 2^23 + 128 symbols)
+    sstride) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          S="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
+          run ss_c3_64 300 python bench.py $S &&
+          run ss_c3_192 300 python bench.py --shard-align 192 $S &&
+          run ss_c3_320 300 python bench.py --shard-align 320 $S &&
+          run ss_c2_64 300 python bench.py --preset c2 $S &&
+          run ss_c2_192 300 python bench.py --preset c2 --shard-align 192 $S &&
+          run ss_6480_64 300 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $S &&
+          run ss_6480_192 300 python bench.py --need 64 --total 80 --objects 32 --erase $E16 --shard-align 192 $S &&
+          run ss_c3_64b 300 python bench.py $S ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
