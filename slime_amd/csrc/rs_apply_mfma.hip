@@ -4,6 +4,7 @@
 // fragments (mfma_table.hpp: rows <= 32, k <= 112).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <atomic>
 
@@ -72,9 +73,20 @@ int mfma_kernel_form() {
 }
 namespace {
 
-template <int KS, int MODE>
+// Cache policy A/B of the refill form (env SLIME_RS_MFMA_NT, two digits: loads,
+// stores; 1 = non-temporal, the product "11").
+int mfma_nt() {
+  static const int v = [] {
+    const char* e = getenv("SLIME_RS_MFMA_NT");
+    if (!e || strlen(e) != 2) return 3;
+    return (e[0] == '1' ? 2 : 0) | (e[1] == '1' ? 1 : 0);
+  }();
+  return v;
+}
+
+template <int KS, int MODE, bool NTL = kNtLoads, bool NTS = kNtStores>
 void launch_mode(const ApplyLaunch& a, hipStream_t stream, dim3 grid, uint32_t lds, uint32_t nseg) {
-  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, kNtLoads, kNtStores, MODE>), grid, dim3(apply::kBlock), lds,
+  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, NTL, NTS, MODE>), grid, dim3(apply::kBlock), lds,
                      stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride, a.out_shard_stride,
                      a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
 }
@@ -102,7 +114,14 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   switch (mode) {
     case 0: launch_mode<KS, 0>(a, stream, grid, lds, nseg); break;
     case 1: launch_mode<KS, 1>(a, stream, grid, lds, nseg); break;
-    default: launch_mode<KS, 2>(a, stream, grid, lds, nseg); break;
+    default:
+      switch (mfma_nt()) {
+        case 0: launch_mode<KS, 2, false, false>(a, stream, grid, lds, nseg); break;
+        case 1: launch_mode<KS, 2, false, true>(a, stream, grid, lds, nseg); break;
+        case 2: launch_mode<KS, 2, true, false>(a, stream, grid, lds, nseg); break;
+        default: launch_mode<KS, 2>(a, stream, grid, lds, nseg); break;
+      }
+      break;
   }
   return hipGetLastError();
 }

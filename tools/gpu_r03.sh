@@ -133,6 +133,15 @@ for step in "$@"; do
           run ss_6480_64 300 python bench.py --need 64 --total 80 --objects 32 --erase $E16 $S &&
           run ss_6480_192 300 python bench.py --need 64 --total 80 --objects 32 --erase $E16 --shard-align 192 $S &&
           run ss_c3_64b 300 python bench.py $S ;;
+    # cache policy of the matrix-core kernel (SLIME_RS_MFMA_NT=<loads><stores>, 1 = non-temporal)
+    mfmant) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          G="--bytes-path 0 --steps 5 --warmup 2 $NOLEGS"
+          for nt in 11 01 10 00 11; do
+            run mnt_6480_$nt 300 env SLIME_RS_MFMA_NT=$nt python bench.py --need 64 --total 80 --objects 32 --erase $E16 $G || exit 1
+          done
+          for nt in 11 01; do
+            run mnt_4048_$nt 300 env SLIME_RS_MFMA_NT=$nt python bench.py --need 40 --total 48 --objects 32 --erase 0,1,2,3,4,5,6,7 $G || exit 1
+          done ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
