@@ -296,21 +296,27 @@ hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The refill form (2) is the product for the decode and the re-encode; the
-// speculative encode takes the no-prefetch form (0): with the MapToGF flags
-// the refill form needs more than 256 VGPRs at four K steps and spills.  Env
-// SLIME_RS_MFMA_ENC_FORM=3 runs it on the refill form at one wave per SIMD
-// instead, SLIME_RS_MFMA_MODE=0/1 forces a form elsewhere (A/B only).
+// The refill form (2) is the product for the decode and the re-encode.  The
+// speculative encode cannot take it at two waves per SIMD: with the MapToGF
+// flags it needs more than 256 VGPRs at four K steps and spills.  Up to four K
+// steps it runs the refill form at one wave per SIMD (3), above them the
+// no-prefetch form (0) -- measured per shape (profiles/r03/s35_mfma_bytes/,
+// s36_mfma_geo/): 40/56 2.998 -> 2.890 ms and 64/80 2.718 -> 2.603 for both
+// passes with form 3, 80/100 3.529 -> 3.565.  Env SLIME_RS_MFMA_ENC_FORM=0|3
+// forces one; SLIME_RS_MFMA_MODE=0/1 forces a form elsewhere (A/B only).
+template <int KS>
 int enc_form0() {
   static const int f = [] {
     const char* e = getenv("SLIME_RS_MFMA_ENC_FORM");
-    return e && e[0] == '3' ? 3 : 0;
+    if (e && e[0] == '3') return 3;
+    if (e && e[0] == '0') return 0;
+    return KS <= 4 ? 3 : 0;
   }();
   return f;
 }
 template <int KS>
 hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
-  if (a.phase == 0) return enc_form0() == 3 ? enc_form<KS, 3>(a, s) : enc_form<KS, 0>(a, s);
+  if (a.phase == 0) return enc_form0<KS>() == 3 ? enc_form<KS, 3>(a, s) : enc_form<KS, 0>(a, s);
   switch (mfma_kernel_form()) {
     case 0: return enc_form<KS, 0>(a, s);
     case 1: return enc_form<KS, 1>(a, s);
