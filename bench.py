@@ -242,6 +242,19 @@ def _cpu_leg(OC, need: int, total: int, have: list[int], threads: int, sample_mi
             "object_passes": sum(reps), "seconds": round(dt, 2)}
 
 
+def _matrix_cores(k: int, rows: int) -> bool:
+    """Whether the library runs this shape on its matrix-core kernels (the rule
+    in rs_apply_mfma.hip mfma_wanted: k >= 33, or 17 <= k <= 32 with k x rows
+    >= 128; at most 32 output rows and k <= 112) -- for the line's labels."""
+    from slime_amd import _native as N
+    if N.lib.slime_rs_kernel_matrix_cores(-1) != 1 or rows > 32 or k > 112 or rows < 1:
+        return False
+    forced = int(os.environ.get("SLIME_RS_MFMA_MINK", "0") or 0)
+    if forced > 0:
+        return k >= forced and k >= 17
+    return k >= 33 or (k >= 17 and k * rows >= 128)
+
+
 def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, seconds: float) -> dict:
     """The reference's algorithm on host cores: the oracle's
     faithful C restatement, one object per thread as the reference runs it
@@ -353,6 +366,10 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
     kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
+    if _matrix_cores(need, total - need) and (need >= 25 or os.environ.get("SLIME_RS_MFMA_MINK")):
+        kernels["encode"] = ["encode_bytes_mfma_kernel"]
+    if _matrix_cores(need, len(erase)):
+        kernels["decode"] = ["decode_bytes_mfma_kernel"]
     replay = _bytes_traffic(args, f"{need}/{total} S={S} nobj={nobj} cs={cs}", need, kernels)
 
     def leg(what, alg, ms):
@@ -769,6 +786,8 @@ def main():
         queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1 and \
             (need <= 16 or os.environ.get("SLIME_RS_K32", "1")[:1] != "0")
         kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
+    if _matrix_cores(need, total - need) and total * SS * 4 < (1 << 32):
+        kname = "rs_apply_mfma_kernel"  # wide codes (rs_apply_mfma.hip)
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such
     # passes only when they were taken on this config AND this kernel source,
