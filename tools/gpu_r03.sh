@@ -142,6 +142,13 @@ for step in "$@"; do
           for nt in 11 01; do
             run mnt_4048_$nt 300 env SLIME_RS_MFMA_NT=$nt python bench.py --need 40 --total 48 --objects 32 --erase 0,1,2,3,4,5,6,7 $G || exit 1
           done ;;
+    # SQ counters (where wave-cycles go) for the matrix-core kernel at 64/80 and the C3 VALU kernel
+    sqpass) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+          SQC="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES"
+          run sq_6480 120 timeout -s KILL 90 rocprofv3 --pmc $SQC -d "$OUT/sq_6480" -o pmc --output-format csv -- \
+            python3 bench.py --need 64 --total 80 --objects 32 --erase $E16 --steps 2 --warmup 1 --bytes-path 0 $NOLEGS &&
+          run sq_c3 120 timeout -s KILL 90 rocprofv3 --pmc $SQC -d "$OUT/sq_c3" -o pmc --output-format csv -- \
+            python3 bench.py --steps 2 --warmup 1 --bytes-path 0 $NOLEGS ;;
     shapes) run shape_c2 300 python bench.py --preset c2 $NOLEGS &&
             run shape_c5 400 python bench.py --preset c5 --global-objects 16 $NOLEGS &&
             run shape_ns64 300 python bench.py --preset ns64 $NOLEGS --bytes-path 0 ;;
