@@ -243,3 +243,29 @@ def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, tota
         D.decode_objects(rec, slots, stride, L, 3, mapping, **cs)
         torch.cuda.synchronize()
         assert torch.equal(slots, truth), erase
+
+
+def test_objects_over_4gib_take_the_valu_kernels(torch_dev):
+    """The matrix-core kernel addresses an object with 32-bit byte offsets; a
+    layout whose object spans 4 GiB or more (here 40 shards 128 MiB + 256 B
+    apart: 5 GiB) must take the VALU kernels and still be exact."""
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, L = 40, 44, 4099
+    SS = (1 << 25) + 64  # shard stride in symbols
+    rng = np.random.default_rng(44)
+    buf = torch.zeros(total * SS, dtype=torch.int32, device="cuda")
+    data = _rand(rng, (need, L)) % P
+    for j in range(need):
+        buf[j * SS: j * SS + L] = torch.from_numpy(data[j].view(np.int32).copy()).cuda()
+    lay = D.layout_of(total, L, SS)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, 1, dst_offset=need * SS)
+    torch.cuda.synchronize()
+    ref = np.zeros((total, L), dtype=np.uint32)
+    ref[:need] = data
+    OC.encode_object(ref, need, total)
+    for i in range(need, total):
+        got = buf[i * SS: i * SS + L].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, ref[i]), i
+    del buf
+    torch.cuda.empty_cache()
