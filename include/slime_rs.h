@@ -104,7 +104,8 @@ int slime_rs_kernel_pipeline(int mode);
  * work from ticket counters (default); 0 = static shares per wave.  mode < 0
  * queries.  Results are identical; the parity tests run both. */
 int slime_rs_kernel_schedule(int mode);
-/* Wide codes (k >= 33, up to 32 output rows and k <= 112) on the matrix cores
+/* Wide codes (k >= 33, or 17 <= k <= 32 with k x rows >= 128; up to 32 output
+ * rows and k <= 112) on the matrix cores
  * (process-wide; env SLIME_RS_MFMA=0 sets the initial value): 1 = the exact
  * int8-limb kernel on v_mfma_i32_16x16x64_i8 (default), 0 = the VALU kernels.
  * mode < 0 queries.  Results are identical; the parity tests run both. */

@@ -1,7 +1,7 @@
 // Launcher of the matrix-core apply kernel (rs_apply_mfma_kernel.hpp) for wide
 // codes: applyMatrix (internal/rs/vector.go:90-102) as an exact int8-limb
 // product on v_mfma_i32_16x16x64_i8, for plans whose table carries the digit
-// fragments (mfma_table.hpp: rows <= 32, k <= 112).
+// fragments (built for k >= 17 with rows <= 32, k <= 112: mfma_table.hpp).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -14,9 +14,9 @@
 namespace slime {
 
 // Process-wide switch (env SLIME_RS_MFMA=0 sets the initial value;
-// slime_rs_kernel_matrix_cores() switches it) and the smallest k that takes
-// the matrix-core kernel (env SLIME_RS_MFMA_MINK, tuning; default 33: up to
-// k = 32 the VALU kernels are HBM-bound already).
+// slime_rs_kernel_matrix_cores() switches it).  Which shapes take the matrix
+// cores is mfma_wanted() below; env SLIME_RS_MFMA_MINK=n replaces that rule
+// by k >= n (tuning A/B only).
 static std::atomic<int> g_mfma{[] {
   const char* e = getenv("SLIME_RS_MFMA");
   return e && e[0] == '0' ? 0 : 1;

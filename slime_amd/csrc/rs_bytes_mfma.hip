@@ -1,5 +1,6 @@
 // Matrix-core form of the fused byte-domain encode and decode for wide codes
-// (need >= 33): writeChunks' MapToGF -> splitVector -> CreateParity ->
+// (bytes_mfma_eligible: need >= 33, or from need 17 (decode) / 25 (encode) when
+// need x rows >= 128): writeChunks' MapToGF -> splitVector -> CreateParity ->
 // MapFromGF (internal/store/multi/multi_store.go:526-557) and reconstruct's
 // MapToGFWith -> RecoverData -> MapFromGF (multi_store.go:185-242), on the
 // int8-limb product of rs_apply_mfma_kernel.hpp.
