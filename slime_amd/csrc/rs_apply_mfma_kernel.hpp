@@ -36,12 +36,8 @@ namespace apply {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
 // Dynamic LDS bytes of a launch: A fragments, row constants, output offsets.
-// The M tiles are padded to a multiple of 4 with zero fragments, so a row
-// block always runs its 4 M tiles unconditionally (no branch between an A
-// fragment's LDS read and its MFMAs).
-__host__ __device__ constexpr uint32_t mfma_mt4(uint32_t mt) { return (mt + 3) & ~3u; }
 __host__ __device__ constexpr uint32_t mfma_lds_bytes(uint32_t mt, uint32_t ks) {
-  return mfma_mt4(mt) * ks * mfma::kFragBytes + mfma_mt4(mt) * 4 * (8 + 4);
+  return mt * ks * mfma::kFragBytes + mt * 4 * (8 + 4);
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -71,13 +67,6 @@ __host__ __device__ constexpr int mfma_w4_max_ks() { return SLIME_MFMA_W4_MAX_KS
 // to two K steps, else one; form 3 is the refill form at one wave per SIMD
 // (for kernels whose extra state does not fit two).
 __host__ __device__ constexpr int mfma_width(int ks) { return ks <= mfma_w4_max_ks() ? 4 : 2; }
-// A fragments read one M tile ahead of the MFMAs (mfma_rows) where the
-// registers allow it at two waves per SIMD (env-free compile-time rule:
-// every K-step count but four; SLIME_MFMA_A_AHEAD4=1 to try it at four).
-#ifndef SLIME_MFMA_A_AHEAD4
-#define SLIME_MFMA_A_AHEAD4 0
-#endif
-__host__ __device__ constexpr bool mfma_a_ahead(int ks) { return ks != 4 || SLIME_MFMA_A_AHEAD4; }
 // Column passes per K loop (mfma_rows): 2 where four-column tiles need their
 // accumulators halved to fit two waves per SIMD.
 __host__ __device__ constexpr int mfma_halves(int ks) { return ks > 4 && ks <= mfma_w4_max_ks() ? 2 : 1; }
@@ -166,34 +155,14 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
           for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ibn + (uint32_t)(soff[q][jj] + colbn));
         }
       }
-      if constexpr (mfma_a_ahead(KS)) {
-        // Every M tile of the block unconditionally (fragments past MT are
-        // zero in LDS), each tile's A fragment read one tile ahead of its
-        // MFMAs: the LDS latency hides behind the previous tile's MFMAs.
-        i32x4 a = lfrag[(mb * KS + q) * 64 + lane];
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-          i32x4 an = a;
-          if (mm < 3) an = lfrag[((mb + mm + 1) * KS + q) * 64 + lane];
+      for (int mm = 0; mm < 4; ++mm) {
+        if (mb + mm < MT) {
+          const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
 #pragma unroll
           for (int c = 0; c < CW; ++c)
             acc[mm][c] =
                 __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], q == 0 ? i32x4{0, 0, 0, 0} : acc[mm][c], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          a = an;
-        }
-      } else {
-        // Four K steps at two waves per SIMD leave no registers for the
-        // read-ahead: each tile's fragment, then its MFMAs.
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-          if (mb + mm < MT) {
-            const i32x4 a = lfrag[((mb + mm) * KS + q) * 64 + lane];
-#pragma unroll
-            for (int c = 0; c < CW; ++c)
-              acc[mm][c] =
-                  __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[c], q == 0 ? i32x4{0, 0, 0, 0} : acc[mm][c], 0, 0, 0);
-          }
         }
       }
       // Keep step q's refill loads in step q: scheduled all at the top they
@@ -210,13 +179,17 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
           const uint32_t v = fold96(mfma_recombine(acc[mm][c], R), 0) ^ io.xout;
           out[mm][h * CW + c] = BSWAP ? __builtin_bswap32(v) : v;
         }
-        if (h == NH - 1) {  // the row's last pass: store it now (its registers free up)
-          vec_t<W> r;
-#pragma unroll
-          for (int c = 0; c < W; ++c) r[c] = out[mm][c];
-          stw<W, NTS>(ob + (uint32_t)(loff[i] + colb), r);
-        }
       }
+    }
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    const uint32_t i = 4 * (mb + mm) + g;
+    if (mb + mm < MT && i < rows && store) {
+      vec_t<W> r;
+#pragma unroll
+      for (int c = 0; c < W; ++c) r[c] = out[mm][c];
+      stw<W, NTS>(ob + (uint32_t)(loff[i] + colb), r);
     }
   }
 }
@@ -308,13 +281,13 @@ __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restr
                                               const uint32_t* __restrict__ out_idx, uint64_t in_unit,
                                               uint64_t out_unit, uint32_t MT, uint32_t rows, uint32_t k, uint32_t g,
                                               uint64_t** lrowc, uint32_t** loff, uint32_t (&soff)[KS][4]) {
-  const uint32_t nfrag = MT * KS * 64, nfrag4 = mfma_mt4(MT) * KS * 64;
+  const uint32_t nfrag = MT * KS * 64;
   const i32x4* gfrag = reinterpret_cast<const i32x4*>(table);
-  for (uint32_t f = threadIdx.x; f < nfrag4; f += kBlock) lds[f] = f < nfrag ? gfrag[f] : i32x4{0, 0, 0, 0};
-  *lrowc = reinterpret_cast<uint64_t*>(lds + nfrag4);
-  *loff = reinterpret_cast<uint32_t*>(*lrowc + mfma_mt4(MT) * 4);
+  for (uint32_t f = threadIdx.x; f < nfrag; f += kBlock) lds[f] = gfrag[f];
+  *lrowc = reinterpret_cast<uint64_t*>(lds + nfrag);
+  *loff = reinterpret_cast<uint32_t*>(*lrowc + MT * 4);
   const uint64_t* growc = reinterpret_cast<const uint64_t*>(table + (size_t)nfrag * 16);
-  for (uint32_t i = threadIdx.x; i < mfma_mt4(MT) * 4; i += kBlock) {
+  for (uint32_t i = threadIdx.x; i < MT * 4; i += kBlock) {
     (*lrowc)[i] = i < rows ? growc[i] : 0;
     (*loff)[i] = i < rows ? (uint32_t)(out_idx[i] * out_unit) : 0;
   }
