@@ -52,8 +52,37 @@ __device__ __forceinline__ uint64_t mfma_recombine(const i32x4& d, uint64_t R) {
   asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cc) : "v"(d[3]), "s"(16777216));
   return v;
 }
+// Four outputs' recombinations in one statement, interleaved digit by digit
+// (four independent multiply-add chains back to back instead of one chain at
+// a time, and one wait-state pad per statement instead of one per mad).
+__device__ __forceinline__ void mfma_recombine4(const i32x4& d0, const i32x4& d1, const i32x4& d2, const i32x4& d3,
+                                                uint64_t R, uint64_t (&v)[4]) {
+  v[0] = v[1] = v[2] = v[3] = R;
+  asm("v_mad_i64_i32 %0, vcc, %4, 1, %0\n\t"
+      "v_mad_i64_i32 %1, vcc, %5, 1, %1\n\t"
+      "v_mad_i64_i32 %2, vcc, %6, 1, %2\n\t"
+      "v_mad_i64_i32 %3, vcc, %7, 1, %3\n\t"
+      "v_mad_i64_i32 %0, vcc, %8, %20, %0\n\t"
+      "v_mad_i64_i32 %1, vcc, %9, %20, %1\n\t"
+      "v_mad_i64_i32 %2, vcc, %10, %20, %2\n\t"
+      "v_mad_i64_i32 %3, vcc, %11, %20, %3\n\t"
+      "v_mad_i64_i32 %0, vcc, %12, %21, %0\n\t"
+      "v_mad_i64_i32 %1, vcc, %13, %21, %1\n\t"
+      "v_mad_i64_i32 %2, vcc, %14, %21, %2\n\t"
+      "v_mad_i64_i32 %3, vcc, %15, %21, %3\n\t"
+      "v_mad_i64_i32 %0, vcc, %16, %22, %0\n\t"
+      "v_mad_i64_i32 %1, vcc, %17, %22, %1\n\t"
+      "v_mad_i64_i32 %2, vcc, %18, %22, %2\n\t"
+      "v_mad_i64_i32 %3, vcc, %19, %22, %3"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])
+      : "v"(d0[0]), "v"(d1[0]), "v"(d2[0]), "v"(d3[0]), "v"(d0[1]), "v"(d1[1]), "v"(d2[1]), "v"(d3[1]), "v"(d0[2]),
+        "v"(d1[2]), "v"(d2[2]), "v"(d3[2]), "v"(d0[3]), "v"(d1[3]), "v"(d2[3]), "v"(d3[3]), "s"(256), "s"(65536),
+        "s"(16777216)
+      : "vcc");
+}
 #else
 __device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
+__device__ void mfma_recombine4(const i32x4&, const i32x4&, const i32x4&, const i32x4&, uint64_t, uint64_t (&)[4]);
 #endif
 
 #ifndef SLIME_MFMA_W4_MAX_KS
@@ -174,10 +203,20 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
       const uint32_t i = 4 * (mb + mm) + g;
       if (mb + mm < MT && i < rows && store) {
         const uint64_t R = lrowc[i];
+        if constexpr (CW == 4 && !BSWAP) {  // (the byte kernels' extra state leaves no room for it)
+          uint64_t rv[4];
+          mfma_recombine4(acc[mm][0], acc[mm][1], acc[mm][2], acc[mm][3], R, rv);
 #pragma unroll
-        for (int c = 0; c < CW; ++c) {
-          const uint32_t v = fold96(mfma_recombine(acc[mm][c], R), 0) ^ io.xout;
-          out[mm][h * CW + c] = BSWAP ? __builtin_bswap32(v) : v;
+          for (int c = 0; c < 4; ++c) {
+            const uint32_t v = fold96(rv[c], 0) ^ io.xout;
+            out[mm][h * CW + c] = BSWAP ? __builtin_bswap32(v) : v;
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < CW; ++c) {
+            const uint32_t v = fold96(mfma_recombine(acc[mm][c], R), 0) ^ io.xout;
+            out[mm][h * CW + c] = BSWAP ? __builtin_bswap32(v) : v;
+          }
         }
       }
     }
