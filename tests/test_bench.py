@@ -145,3 +145,16 @@ def test_kernel_code_ids_name_one_kernel_each():
             assert ids[(k, need)] is not None, (k, need)
     assert len(set(ids.values())) == len(ids)
     assert kernel_code_id(lib, ("no_such_kernel",)) is None
+
+
+def test_matrix_core_labels_follow_the_library_rule():
+    """bench.py labels a wide-code line with the matrix-core kernels exactly
+    where the library routes it there (rs_apply_mfma.hip mfma_wanted: k >= 33,
+    or 17 <= k <= 32 with k x rows >= 128; at most 32 rows, k <= 112)."""
+    if os.environ.get("SLIME_RS_MFMA_MINK") or os.environ.get("SLIME_RS_MFMA", "1")[:1] == "0":
+        return  # the process was started with the rule overridden
+    bench = _load("bench.py", "bench_mod_mfma")
+    yes = [(64, 16), (33, 1), (99, 1), (112, 32), (24, 8), (32, 4), (17, 8)]
+    no = [(8, 4), (10, 4), (16, 16), (20, 4), (17, 7), (64, 33), (113, 4), (40, 0)]
+    assert all(bench._matrix_cores(k, r) for k, r in yes)
+    assert not any(bench._matrix_cores(k, r) for k, r in no)
