@@ -475,27 +475,18 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     parts = objects.split_vector(words, need)
     par = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
     t_cp = med(lambda: [rs.CreateParity(parts, need + i, par[i]) for i in range(r)])
-
-    def unchanged_write():
-        mm, w = gf.MapToGF(data)
-        ps = objects.split_vector(w, need)
-        pv = [rs.CreateParity(ps, need + i) for i in range(r)]
-        return mm, [gf.MapFromGF(mm, p) for p in ps + pv]
-
-    t_uw = med(unchanged_write)
-    mm, ref_chunks = unchanged_write()
-    ok_w = mm == box["m"] and all(bytes(c) == rc for c, rc in zip(chunks, ref_chunks))
     sym = [gf.MapToGFWith(chunks[i], m) for i in have]
     rec = [np.zeros(sym[0].size, dtype=np.uint32) for _ in range(need)]
     t_rd = med(lambda: rs.RecoverData(sym, have, rec))
-
-    def unchanged_read():
-        cs = [gf.MapToGFWith(chunks[i], m) for i in have]
-        vs = rs.RecoverData(cs, have)
-        return b"".join(gf.MapFromGF(m, v) for v in vs)[:data.size]
-
-    t_ur = med(unchanged_read)
-    ok_r = unchanged_read() == data.tobytes()
+    unchanged = unchanged_caller(data, need, total, have, chunks, m, box["m"], reps)
+    with_device_codec = None
+    prev = gf.codec_placement(1)
+    try:  # the same caller with the codec through the GPU (round 3's form), for comparison
+        u = unchanged_caller(data, need, total, have, chunks, m, box["m"], 3)
+        with_device_codec = {"write_gibs": u["write_gibs"], "read_gibs": u["read_gibs"],
+                             "split_ms": {"write": u["split_ms"]["write"], "read": u["split_ms"]["read"]}}
+    finally:
+        gf.codec_placement(prev)
     par2 = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
@@ -505,17 +496,103 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
             "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
                                "what": "the median call's split: host copies in/out, launches, waits on the device/link side "
                                        "(a large wait with normal copies = DMA contention, DESIGN.md End-to-end)"},
-            "unchanged_caller": {
-                "write_gibs": g(t_uw), "read_gibs": g(t_ur),
-                "create_parity_x_r_gibs": g(t_cp), "create_parities_batched_gibs": g(t_cps),
-                "recover_data_gibs": g(t_rd), "verified": bool(ok_w and ok_r),
-                "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF "
-                        f"(write); {need} x MapToGFWith + RecoverData + {need} x MapFromGF (read); each call "
-                        "host->GPU->host"},
+            "unchanged_caller": dict(unchanged, create_parity_x_r_gibs=g(t_cp),
+                                     create_parities_batched_gibs=g(t_cps), recover_data_reused_out_gibs=g(t_rd),
+                                     with_device_codec=with_device_codec),
             "digests": digests,
             "object_mib": obj_mib, "erased": erase, "verified": ok,
             "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
                     "PCIe-inclusive; not `value`"}
+
+
+def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
+    """multi_store.go as it is, call by call through the Go-API mirrors, on
+    fresh outputs (Go's make): writeChunks = MapToGF (:526) + splitVector
+    (:527) + r CreateParity (:528-531) + a MapFromGF per chunk (:554);
+    reconstruct's slow path = MapToGFWith per survivor (:224) + RecoverData
+    (:237) + MapFromGF per data row appended to make([]byte, 0, Size+16)
+    (:204,238-241).  Each phase is timed; the split is the median call's.
+    alloc_ms: the same fresh output buffers allocated and first touched
+    alone (page faults + zeroing), the share of the phases that is Go's make()."""
+    import numpy as np
+    from slime_amd import _native as N
+    from slime_amd import gf, objects, rs
+    r = total - need
+    pc = time.perf_counter
+
+    def write():
+        t0 = pc()
+        mm, w = gf.MapToGF(data)
+        t1 = pc()
+        ps = objects.split_vector(w, need)
+        t2 = pc()
+        pv = [rs.CreateParity(ps, need + i) for i in range(r)]
+        t3 = pc()
+        out = [gf.MapFromGF(mm, p) for p in ps + pv]
+        t4 = pc()
+        return (mm, out), [t1 - t0, t2 - t1, t3 - t2, t4 - t3]
+
+    def read():
+        t0 = pc()
+        cs = [gf.MapToGFWith(chunks[i], m) for i in have]
+        t1 = pc()
+        vs = rs.RecoverData(cs, have)
+        t2 = pc()
+        buf = np.empty(data.size + 16, dtype=np.uint8)  # make([]byte, 0, Size+16)
+        o = 0
+        for v in vs:
+            b = gf.MapFromGF(m, v)
+            n = min(len(b), buf.size - o)
+            buf[o:o + n] = np.frombuffer(b, dtype=np.uint8, count=n)
+            o += n
+        t3 = pc()
+        return buf[:data.size], [t1 - t0, t2 - t1, t3 - t2]
+
+    def median_run(fn):
+        fn()
+        runs = []
+        for _ in range(reps):
+            t0 = pc()
+            res, split = fn()
+            runs.append((pc() - t0, split, res))
+        runs.sort(key=lambda x: x[0])
+        return runs[len(runs) // 2]
+
+    t_w, sw, (mm, wc) = median_run(write)
+    t_r, sr, got = median_run(read)
+    ok_w = mm == m_fused and all(bytes(c) == bytes(x) for c, x in zip(wc, chunks))
+    ok_r = bytes(got) == data.tobytes()
+    L = chunks[0].size // 4
+
+    def alloc_write():
+        bufs = [np.empty((data.size + 3) // 4, dtype=np.uint32)] + \
+               [np.zeros(L, dtype=np.uint32) for _ in range(r)] + [bytearray(4 * L) for _ in range(total)]
+        for b in bufs:
+            np.frombuffer(b, dtype=np.uint8)[::4096] = 1
+        return None, []
+
+    def alloc_read():
+        bufs = [np.empty(L, dtype=np.uint32) for _ in range(2 * need)] + [bytearray(4 * L) for _ in range(need)] + \
+               [np.empty(data.size + 16, dtype=np.uint8)]
+        for b in bufs:
+            np.frombuffer(b, dtype=np.uint8)[::4096] = 1
+        return None, []
+
+    a_w = median_run(alloc_write)[0]
+    a_r = median_run(alloc_read)[0]
+    ms = lambda x: round(x * 1e3, 3)  # noqa: E731
+    return {"write_gibs": round(data.size / GIB / t_w, 2), "read_gibs": round(data.size / GIB / t_r, 2),
+            "split_ms": {"write": {"total": ms(t_w), "map_to_gf": ms(sw[0]), "split_vector": ms(sw[1]),
+                                   f"create_parity_x{r}": ms(sw[2]), f"map_from_gf_x{total}": ms(sw[3]),
+                                   "alloc_alone": ms(a_w)},
+                         "read": {"total": ms(t_r), f"map_to_gf_with_x{need}": ms(sr[0]), "recover_data": ms(sr[1]),
+                                  f"map_from_gf_append_x{need}": ms(sr[2]), "alloc_alone": ms(a_r)}},
+            "codec": dict(N.codec_info(), placement="device" if gf.codec_placement() else "host"),
+            "verified": bool(ok_w and ok_r),
+            "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF "
+                    f"(write); {need} x MapToGFWith + RecoverData + {need} x MapFromGF appended (read); fresh "
+                    "outputs per call as Go's make(); CreateParity/RecoverData host->GPU->host; the codec on the "
+                    "host cores (placement host) or through the GPU (with_device_codec)"}
 
 
 def digest_leg(data, need, total, chunks, have, out, med, g) -> dict:

@@ -124,12 +124,26 @@ uint32_t slime_gf_raise(uint32_t x, uint32_t n);
 /* gf.MapToGF (internal/rs/gf/map.go:15).  out must hold (len+3)/4 words.
  * Mapping 0 if every big-endian word is < p, else 1<<31 if that fits, else
  * the first fitting value from the library's random candidate stream (the
- * reference draws rand.Uint32(); see slime_gf_seed).  Runs on the GPU. */
+ * reference draws rand.Uint32(); see slime_gf_seed).  Host memory: runs on
+ * the host cores where the bytes are (slime_gf_codec_placement). */
 int slime_gf_map_to_gf(const uint8_t *in, uint64_t len, uint32_t *mapping, uint32_t *out);
-/* gf.MapToGFWith (internal/rs/gf/map.go:74). out holds (len+3)/4 words. GPU. */
+/* gf.MapToGFWith (internal/rs/gf/map.go:74). out holds (len+3)/4 words. */
 int slime_gf_map_to_gf_with(const uint8_t *in, uint64_t len, uint32_t n, uint32_t *out);
-/* gf.MapFromGF (internal/rs/gf/map.go:103). out holds 4*count bytes. GPU. */
+/* gf.MapFromGF (internal/rs/gf/map.go:103). out holds 4*count bytes. */
 int slime_gf_map_from_gf(uint32_t n, const uint32_t *in, uint64_t count, uint8_t *out);
+/* Where the three host-memory codec calls above run (process-wide; env
+ * SLIME_RS_CODEC=device sets the initial value): 0 = on the host cores, in
+ * place on the caller's buffers (AVX2 passes split over the library's copy
+ * pool; default -- the codec is a byte swap, an XOR and a compare, and the
+ * bytes are in host memory); 1 = through the GPU codec kernels and the pinned
+ * staging ring (two PCIe crossings per call).  Device-resident buffers and
+ * the fused object entry points always use the GPU codec.  mode < 0 queries.
+ * Results are identical; the parity tests run both. */
+int slime_gf_codec_placement(int mode);
+/* The host codec's instruction set ("avx2" or "scalar"; env
+ * SLIME_RS_CODEC_ISA=scalar forces the portable form) and the threads its
+ * passes use (the library's copy pool plus the calling thread). */
+int slime_gf_codec_info(const char **isa, int *threads);
 /* Seed the MapToGF fallback candidate stream (default: std::random_device,
  * like the reference's crypto-seeded math/rand, main.go:128-136). */
 void slime_gf_seed(uint64_t seed);
@@ -161,7 +175,9 @@ int slime_rs_create_parities(const uint32_t *const *data, const uint64_t *lens, 
                              uint32_t *const *out);
 /* RecoverData (internal/rs/vector.go:50).  chunks[i] has lens[i] words and
  * code-row index indices[i]; out[0..nchunks-1] each receive lens[0] words of
- * data rows 0..nchunks-1. */
+ * data rows 0..nchunks-1.  Only the erased data rows (those not among
+ * indices) are computed on the GPU; a surviving data row's inverse row is a
+ * unit row, so its output is that chunk mod p, written on the host. */
 int slime_rs_recover_data(const uint32_t *const *chunks, const uint64_t *lens, int nchunks, const int *indices,
                           int nindices, uint32_t *const *out);
 

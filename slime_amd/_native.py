@@ -87,6 +87,8 @@ SIGNATURES = [
     ("slime_gf_map_to_gf_with", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
     ("slime_gf_map_from_gf", ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     ("slime_gf_seed", None, [ctypes.c_uint64]),
+    ("slime_gf_codec_placement", ctypes.c_int, [ctypes.c_int]),
+    ("slime_gf_codec_info", ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), c_intp]),
     ("slime_rs_vandermonde_matrix", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("slime_rs_parity_matrix", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("slime_rs_parity_matrix_cached", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_u32p)]),
@@ -278,6 +280,13 @@ def digest_info() -> tuple[bool, int]:
     e, t = ctypes.c_int(), ctypes.c_int()
     check(lib.slime_rs_digest_info(ctypes.byref(e), ctypes.byref(t)))
     return bool(e.value), int(t.value)
+
+
+def codec_info() -> dict:
+    """The host codec's instruction set and the threads its passes run on (the copy pool + the caller)."""
+    isa, th = ctypes.c_char_p(), ctypes.c_int()
+    check(lib.slime_gf_codec_info(ctypes.byref(isa), ctypes.byref(th)))
+    return {"isa": isa.value.decode(), "threads": int(th.value)}
 
 
 def alloc_info(ptr: int) -> dict:

@@ -30,7 +30,8 @@ constexpr size_t kSerialBelow = 2u << 20;  // small copies: not worth a wake-up
 constexpr std::chrono::microseconds kSpin{3000};
 
 struct Job {
-  const CopyItem* pieces = nullptr;
+  void (*fn)(const void* ctx, size_t piece) = nullptr;
+  const void* ctx = nullptr;
   size_t n = 0;
   std::atomic<size_t> next{0};
   size_t done = 0;  // guarded by Pool::mu
@@ -82,7 +83,7 @@ void copy_piece(const CopyItem& it) {
 
 size_t drain(Job* j) {
   size_t did = 0;
-  for (size_t i; (i = j->next.fetch_add(1, std::memory_order_relaxed)) < j->n; ++did) copy_piece(j->pieces[i]);
+  for (size_t i; (i = j->next.fetch_add(1, std::memory_order_relaxed)) < j->n; ++did) j->fn(j->ctx, i);
   return did;
 }
 
@@ -104,13 +105,14 @@ class Pool {
   }
   int threads() const { return (int)th_.size(); }
 
-  void run(const CopyItem* pieces, size_t n) {
-    if (th_.empty()) {
-      for (size_t i = 0; i < n; ++i) copy_piece(pieces[i]);
+  void run(size_t n, void (*fn)(const void*, size_t), const void* ctx) {
+    if (th_.empty() || n == 1) {
+      for (size_t i = 0; i < n; ++i) fn(ctx, i);
       return;
     }
     Job j;
-    j.pieces = pieces;
+    j.fn = fn;
+    j.ctx = ctx;
     j.n = n;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -194,6 +196,10 @@ Pool& pool() {
 
 int copy_pool_threads() { return pool().threads(); }
 
+void parallel_pieces(size_t n, void (*fn)(const void* ctx, size_t piece), const void* ctx) {
+  if (n) pool().run(n, fn, ctx);
+}
+
 void parallel_copy(const CopyItem* items, size_t n) {
   size_t total = 0;
   for (size_t i = 0; i < n; ++i) total += items[i].bytes;
@@ -210,7 +216,8 @@ void parallel_copy(const CopyItem* items, size_t n) {
     for (size_t off = 0; off < items[i].bytes; off += kPiece)
       pieces.push_back({d + off, s + off, std::min(kPiece, items[i].bytes - off)});
   }
-  pool().run(pieces.data(), pieces.size());
+  parallel_pieces(
+      pieces.size(), [](const void* ctx, size_t i) { copy_piece(((const CopyItem*)ctx)[i]); }, pieces.data());
 }
 
 }  // namespace slime

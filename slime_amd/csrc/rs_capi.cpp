@@ -30,6 +30,7 @@
 #include "device_pool.hpp"
 #include "digest.hpp"
 #include "gfp_host.hpp"
+#include "host_codec.hpp"
 #include "host_copy.hpp"
 #include "kernels.hpp"
 #include "mfma_table.hpp"
@@ -1363,25 +1364,47 @@ int slime_rs_create_parities(const uint32_t* const* data, const uint64_t* lens, 
   return run_rows(ndata, rows, data, lens[0], out);
 }
 
-static int make_recover_plan(const PlanKey& key, slime_rs_plan** out) {
-  // kind 'R': all need data rows of the inverse of the survivors' code rows
-  // (vector.go RecoverData applies the whole inverse; surviving data rows are
-  // its unit rows, i.e. x mod p).  The staged chunks sit at inputs 0..need-1.
-  const int dev = std::get<0>(key), need = std::get<2>(key);
-  const std::vector<int>& have = std::get<4>(key);
+// The inverse rows `want` of the survivors' code rows (vector.go:69-77), as
+// a plan over the staged chunks at inputs 0..need-1, outputs 0..|want|-1.
+static int make_inverse_rows_plan(int dev, int need, const std::vector<int>& have, const std::vector<int>& want,
+                                  slime_rs_plan** out) {
   const int total = std::max(need, *std::max_element(have.begin(), have.end()) + 1);
-  std::vector<int> want(need);
-  for (int t = 0; t < need; ++t) want[t] = t;
   slime_rs_plan* tmp = nullptr;
-  if (int rc = slime_rs_plan_reconstruct(dev, need, total, have.data(), want.data(), need, &tmp)) return rc;
+  if (int rc = slime_rs_plan_reconstruct(dev, need, total, have.data(), want.data(), (int)want.size(), &tmp))
+    return rc;
   std::vector<int> pos(need);
   for (int q = 0; q < need; ++q) pos[q] = q;
   slime_rs_plan* staged = nullptr;
-  const int rc = slime_rs_plan_matrix(dev, tmp->coeff.data(), need, need, pos.data(), &staged);
+  const int rc = slime_rs_plan_matrix(dev, tmp->coeff.data(), (int)want.size(), need, pos.data(), &staged);
   destroy_plan(tmp);
   if (rc) return rc;
   *out = staged;
   return 0;
+}
+
+static int make_recover_plan(const PlanKey& key, slime_rs_plan** out) {
+  // kind 'O': all need data rows of the inverse (the fused object path
+  // rebuilds whole objects on the device).
+  const int need = std::get<2>(key);
+  std::vector<int> want(need);
+  for (int t = 0; t < need; ++t) want[t] = t;
+  return make_inverse_rows_plan(std::get<0>(key), need, std::get<4>(key), want, out);
+}
+
+// Data rows of `need` absent from the survivors `have`: the only rows of
+// RecoverData's inverse that are not unit rows (vector.go:77-85).
+static std::vector<int> erased_rows(int need, const int* have) {
+  std::vector<int> e;
+  for (int t = 0; t < need; ++t)
+    if (std::find(have, have + need, t) == have + need) e.push_back(t);
+  return e;
+}
+
+static int make_erased_rows_plan(const PlanKey& key, slime_rs_plan** out) {
+  // kind 'R': the erased data rows only.
+  const int need = std::get<2>(key);
+  const std::vector<int>& have = std::get<4>(key);
+  return make_inverse_rows_plan(std::get<0>(key), need, have, erased_rows(need, have.data()), out);
 }
 
 // RecoverData's index checks (vector.go:65-77): no non-negative index ->
@@ -1422,12 +1445,24 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   for (int i = 0; i < need; ++i)
     if (!chunks[i] || !out[i]) return fail(Status::InvalidArg, "RecoverData: null buffer");
 
-  DeviceLease dl;
-  if (int rc = dl.acquire()) return rc;
-  std::vector<int> have(indices, indices + nindices);
-  PlanRef plan;
-  if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_recover_plan)) return rc;
-  return host_apply(plan.get(), chunks, out, L);
+  // vector.go:77-85 applies the whole inverse, but the inverse row of a data
+  // shard that survived is a unit row: its output is that chunk mod p, a
+  // host pass over memory the caller already holds.  Only the erased data
+  // rows cross to the device (need chunks in, the erased rows back).
+  const std::vector<int> erased = erased_rows(need, indices);
+  if (!erased.empty()) {
+    DeviceLease dl;
+    if (int rc = dl.acquire()) return rc;
+    std::vector<int> have(indices, indices + nindices);
+    PlanRef plan;
+    if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_erased_rows_plan)) return rc;
+    std::vector<uint32_t*> rows;
+    for (int t : erased) rows.push_back(out[t]);
+    if (int rc = host_apply(plan.get(), chunks, rows.data(), L)) return rc;
+  }
+  for (int q = 0; q < need; ++q)
+    if (indices[q] < need) host_mod_p(chunks[q], L, out[indices[q]]);
+  return 0;
 }
 
 // ---- object entry points (host memory): writeChunks / reconstruct ------------------
@@ -1721,6 +1756,32 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
 }
 
 // ---- gf codec (host memory) -----------------------------------------------------------
+//
+// Where the Go API's codec calls run (slime_gf_codec_placement): on the host
+// cores, in place on the caller's buffers (host_codec.cpp, default), or
+// through the device codec and the pinned ring (the round-3 form, kept as the
+// measured alternative and exercised by the GPU tests).
+
+static std::atomic<int> g_codec_device{[] {
+  const char* e = getenv("SLIME_RS_CODEC");
+  return e && strcmp(e, "device") == 0 ? 1 : 0;
+}()};
+
+static bool codec_on_device() { return g_codec_device.load(std::memory_order_relaxed) != 0; }
+
+int slime_gf_codec_info(const char** isa, int* threads) {
+  if (isa) *isa = host_codec_isa();
+  if (threads) *threads = copy_pool_threads() + 1;
+  return 0;
+}
+
+int slime_gf_codec_placement(int mode) {
+  if (mode < 0) return g_codec_device.load();
+  if (mode > 1) return fail(Status::InvalidArg, "codec placement: 0 = host, 1 = device");
+  g_codec_device.store(mode);
+  return 0;
+}
+
 
 static int codec_setup(uint64_t bytes_needed, Workspace** wsp, WsLease& lease, DeviceLease& dl) {
   if (int rc = dl.acquire()) return rc;
@@ -1767,10 +1828,8 @@ static int pack_windows(Workspace* ws, const uint8_t* in, uint64_t len, uint32_t
       });
 }
 
-int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out) {
+static int map_to_gf_with_device(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out) {
   const uint64_t nw = (len + 3) / 4;
-  if (nw == 0) return 0;
-  if (!in || !out) return fail(Status::InvalidArg, "MapToGFWith: null buffer");
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t bbytes = round16(len);
@@ -1780,6 +1839,15 @@ int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_
   const int rc = pack_windows(ws, in, len, n, out, ws->dbuf, (uint32_t*)(ws->dbuf + bbytes), nullptr);
   if (rc) drain_stages(ws);
   return rc;
+}
+
+int slime_gf_map_to_gf_with(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out) {
+  const uint64_t nw = (len + 3) / 4;
+  if (nw == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapToGFWith: null buffer");
+  if (codec_on_device()) return map_to_gf_with_device(in, len, n, out);
+  host_pack(in, len, n, out, nullptr);
+  return 0;
 }
 
 // gf.MapToGF's choice of mapping (map.go:35-66) from the two flags already
@@ -1830,12 +1898,8 @@ static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, ui
   return choose_mapping(st, d_words, (len + 3) / 4, d_scratch, mapping);
 }
 
-int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
-  if (!mapping) return fail(Status::InvalidArg, "MapToGF: null mapping");
+static int map_to_gf_device(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
   const uint64_t nw = (len + 3) / 4;
-  *mapping = 0;
-  if (nw == 0) return 0;
-  if (!in || !out) return fail(Status::InvalidArg, "MapToGF: null buffer");
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t bbytes = round16(len), wbytes = round16(nw * 4);
@@ -1868,9 +1932,46 @@ int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint3
   return rc;
 }
 
-int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t* out) {
-  if (count == 0) return 0;
-  if (!in || !out) return fail(Status::InvalidArg, "MapFromGF: null buffer");
+// MapToGF on host memory, in place on the caller's buffers (map.go:15-67):
+// one pass packs the words (mapping 0) and notes whether 0 and 1<<31 fit;
+// a mapping other than 0 is then XORed in by a second pass.  The random
+// fallback (:64-66) probes candidates of the library's stream in order, the
+// first that fits wins (the device form's rule: choose_mapping).
+static int map_to_gf_host(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
+  const uint64_t nw = (len + 3) / 4;
+  uint32_t flags = 0, m = 0;
+  host_pack(in, len, 0, out, &flags);
+  if (flags & 1u) {
+    if (!(flags & 2u)) {
+      m = 1u << 31;  // map.go:47
+    } else {
+      bool found = false;
+      for (uint32_t tries = 0; tries < (1u << 22) && !found; ++tries) {
+        uint32_t cand;
+        {
+          std::lock_guard<std::mutex> lk(g_rng_mu);
+          cand = (uint32_t)(g_rng() >> 32);
+        }
+        if (host_mapping_fits(out, nw, cand)) m = cand, found = true;
+      }
+      if (!found) return status_of(Status::MappingFallback, "MapToGF");
+    }
+    host_xor(out, nw, m);
+  }
+  *mapping = m;
+  return 0;
+}
+
+int slime_gf_map_to_gf(const uint8_t* in, uint64_t len, uint32_t* mapping, uint32_t* out) {
+  if (!mapping) return fail(Status::InvalidArg, "MapToGF: null mapping");
+  const uint64_t nw = (len + 3) / 4;
+  *mapping = 0;
+  if (nw == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapToGF: null buffer");
+  return codec_on_device() ? map_to_gf_device(in, len, mapping, out) : map_to_gf_host(in, len, mapping, out);
+}
+
+static int map_from_gf_device(uint32_t n, const uint32_t* in, uint64_t count, uint8_t* out) {
   WsLease lease;
   Workspace* ws = nullptr;
   const size_t wbytes = round16(count * 4);
@@ -1894,6 +1995,14 @@ int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t
       });
   if (rc) drain_stages(ws);
   return rc;
+}
+
+int slime_gf_map_from_gf(uint32_t n, const uint32_t* in, uint64_t count, uint8_t* out) {
+  if (count == 0) return 0;
+  if (!in || !out) return fail(Status::InvalidArg, "MapFromGF: null buffer");
+  if (codec_on_device()) return map_from_gf_device(n, in, count, out);
+  host_unpack(in, count, n, out);
+  return 0;
 }
 
 // ---- per-call context entry points (cgo) ------------------------------------------

@@ -1,7 +1,9 @@
 """Python mirror of slime's ``internal/rs/gf`` Go API over the MI355X C-ABI.
 
-MaxVal, MInverse and Raise are host scalars; MapToGF / MapToGFWith /
-MapFromGF run their byte<->symbol codec on the GPU (gf_codec.hip).
+MaxVal, MInverse and Raise are host scalars.  MapToGF / MapToGFWith /
+MapFromGF take and return host memory, so their byte<->symbol codec runs on
+the host cores where the bytes are (host_codec.cpp; slime_gf_codec_placement
+can send it through the GPU codec kernels instead, gf_codec.hip).
 Reference: /root/reference/internal/rs/gf/{gf,map}.go.
 """
 from __future__ import annotations
@@ -42,7 +44,7 @@ def _bytes(b) -> np.ndarray:
 def MapToGF(data) -> tuple[int, np.ndarray]:
     """map.go:15 — (mapping, symbols); mapping 0, else 1<<31, else a random fitting value."""
     src = _bytes(data)
-    out = np.zeros((src.size + 3) // 4, dtype=np.uint32)
+    out = np.empty((src.size + 3) // 4, dtype=np.uint32)  # every word is written
     m = ctypes.c_uint32(0)
     N.check(lib.slime_gf_map_to_gf(src.ctypes.data if src.size else None, src.size, ctypes.byref(m),
                                    out.ctypes.data if out.size else None))
@@ -52,7 +54,7 @@ def MapToGF(data) -> tuple[int, np.ndarray]:
 def MapToGFWith(data, n: int) -> np.ndarray:
     """map.go:74 — big-endian symbols XOR n."""
     src = _bytes(data)
-    out = np.zeros((src.size + 3) // 4, dtype=np.uint32)
+    out = np.empty((src.size + 3) // 4, dtype=np.uint32)  # every word is written
     N.check(lib.slime_gf_map_to_gf_with(src.ctypes.data if src.size else None, src.size, n & 0xFFFFFFFF,
                                         out.ctypes.data if out.size else None))
     return out
@@ -71,6 +73,15 @@ def MapFromGF(n: int, v) -> bytearray:
     N.check(lib.slime_gf_map_from_gf(n & 0xFFFFFFFF, words.ctypes.data if words.size else None, words.size,
                                      ctypes.addressof(ptr) if ptr is not None else None))
     return out
+
+
+def codec_placement(mode: int | None = None) -> int:
+    """Where the three codec calls above run: 0 host cores (default), 1 GPU
+    codec kernels; None queries.  Returns the placement in force before the call."""
+    prev = int(lib.slime_gf_codec_placement(-1))
+    if mode is not None:
+        N.check(lib.slime_gf_codec_placement(int(mode)))
+    return prev
 
 
 def Seed(seed: int) -> None:

@@ -188,7 +188,16 @@ def test_host_pipeline_concurrent_callers(host_mode):
             assert np.array_equal(row, OC.create_parity(d, need + i)[1])
 
 
-def test_map_kats_on_gpu(kats):
+@pytest.fixture(params=[0, 1], ids=["host_codec", "device_codec"])
+def codec_place(request):
+    """Both placements of the host-memory codec calls (slime_gf_codec_placement)."""
+    prev = N.lib.slime_gf_codec_placement(-1)
+    N.check(N.lib.slime_gf_codec_placement(request.param))
+    yield request.param
+    N.check(N.lib.slime_gf_codec_placement(prev))
+
+
+def test_map_kats_on_gpu(kats, codec_place):
     for case in kats["map_trivial"]:
         data = bytes(case["in"])
         n, v = gf.MapToGF(data)
@@ -203,7 +212,7 @@ def test_map_kats_on_gpu(kats):
         assert np.array_equal(gf.MapToGFWith(data, n), v)
 
 
-def test_map_golden_and_random(golden):
+def test_map_golden_and_random(golden, codec_place):
     for case in golden["map"]:
         data = bytes(case["bytes"])
         n, v = gf.MapToGF(data)
@@ -220,7 +229,7 @@ def test_map_golden_and_random(golden):
         assert gf.MapFromGF(n, v) == OC.map_from_gf(n, v)
 
 
-def test_map_to_gf_high_bit_mapping():
+def test_map_to_gf_high_bit_mapping(codec_place):
     # Every word >= p forces mapping 1<<31 (map.go:47-62).
     data = bytes([0xFF, 0xFF, 0xFF, 0xFB]) * 1000 + bytes([1, 2])
     n, v = gf.MapToGF(data)

@@ -132,8 +132,9 @@ def test_compute_without_device_fails_loudly():
     with pytest.raises(slime_amd.NativeError) as e:
         rs.CreateParity([[1, 2], [3, 4]], 2)
     assert e.value.code == N.ERR_NO_DEVICE
-    with pytest.raises(slime_amd.NativeError):
-        gf.MapToGF(b"abcd")
+    with pytest.raises(slime_amd.NativeError) as e:  # data shard 1 erased: its row is computed on the GPU
+        rs.RecoverData([[1, 2], [3, 4]], [0, 2])
+    assert e.value.code == N.ERR_NO_DEVICE
     h = ctypes.c_void_p()
     assert N.lib.slime_rs_plan_encode(0, 8, 12, ctypes.byref(h)) == N.ERR_NO_DEVICE
     with pytest.raises(slime_amd.NativeError) as e:
