@@ -75,8 +75,10 @@ def parse(argv=None):
     ap.add_argument("--decode-dst", choices=["inplace", "separate"], default="inplace",
                     help="rebuild into the erased slots of each object (repair) or into a separate buffer")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle CPU path on rank 0 at N=1")
-    ap.add_argument("--cpu-sample-mib", type=int, default=64, help="object size of the CPU sample")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall time budget of the CPU sample")
+    ap.add_argument("--c5-leg", type=int, default=1,
+                    help="also run BASELINE config 5 (10/14, 64 x 1 GiB partitioned over the ranks, encode + "
+                         "decode {0,1,2,3}) and report it as c5_partitioned")
     ap.add_argument("--bytes-path", type=int, default=1,
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
     ap.add_argument("--ceilings", type=int, default=1,
@@ -117,14 +119,45 @@ def parse(argv=None):
 
 # ---- N-rank launch without torchrun ---------------------------------------------
 
+def kfd_gpus(base: str = "/sys/class/kfd/kfd/topology/nodes", dri: str = "/dev/dri") -> int:
+    """GPUs this process may open, counted from the KFD topology in sysfs
+    (nodes with SIMDs whose DRM render node is accessible), narrowed by
+    ROCR/HIP/CUDA_VISIBLE_DEVICES.  Reads files only: it never starts the HIP
+    runtime, so the launcher below can count devices before spawning ranks."""
+    try:
+        nodes = sorted((d for d in os.listdir(base) if d.isdigit()), key=int)
+    except OSError:
+        return 0
+    n = 0
+    for nd in nodes:
+        props = {}
+        try:
+            for line in open(os.path.join(base, nd, "properties")):
+                kv = line.split()
+                if len(kv) == 2:
+                    props[kv[0]] = kv[1]
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue  # a CPU node
+        minor = props.get("drm_render_minor")
+        if minor is not None and not os.access(f"{dri}/renderD{minor}", os.R_OK | os.W_OK):
+            continue  # a GPU of this node that this container may not open
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def visible_gpus() -> int:
-    """GPUs this process may use, counted without initialising the GPU (on this
-    image torch.cuda.device_count() does not start the HIP runtime).
-    SLIME_BENCH_DEVICE_COUNT stands in for it under --dry-run only (tests)."""
+    """GPUs this process may use (kfd_gpus).  SLIME_BENCH_DEVICE_COUNT stands
+    in for it under --dry-run only (tests)."""
     fake = os.environ.get("SLIME_BENCH_DEVICE_COUNT")
     if fake is not None and "--dry-run" in sys.argv[1:]:
         return int(fake)
-    return torch.cuda.device_count()
+    return kfd_gpus()
 
 
 def shared_gpu_rehearsal() -> bool:
@@ -204,28 +237,35 @@ def _cgroup_cpus() -> float | None:
         return None
 
 
-def _cpu_leg(OC, need: int, total: int, have: list[int], threads: int, sample_mib: int, seconds: float) -> dict:
-    """`threads` host threads, one object each, each running the reference's
-    per-object path until ~`seconds` of wall time: r CreateParity passes
-    (multi_store.go:528-531 -> vector.go:18-41) and one RecoverData recomputing
-    all need rows (vector.go:50-88, multi_store.go:237) on the oracle's C
-    restatement (uint64 products, `%`p twice per term, vector.go:97)."""
+def _cpu_leg(OC, sample, need: int, total: int, have: list[int], threads: int, seconds: float) -> dict:
+    """`threads` host threads, each on its own copy of the sample object, each
+    running the reference's per-object path until ~`seconds` of wall time: r
+    CreateParity passes (multi_store.go:528-531 -> vector.go:18-41) and one
+    RecoverData recomputing all need rows (vector.go:50-88, multi_store.go:237)
+    on the oracle's C restatement (uint64 products, `%`p twice per term,
+    vector.go:97).  Returns the rate and thread 0's first outputs."""
     import threading
 
     import numpy as np
 
-    L = (sample_mib << 20) // 4 // need
-    rng = np.random.default_rng(0x5113E)
-    base = rng.integers(0, 4294967291, size=(total, L), dtype=np.uint64).astype(np.uint32)
-    objs = [base.copy() for _ in range(threads)]
+    L = sample.shape[1]
+    objs = []
+    for _ in range(threads):
+        o = np.zeros((total, L), dtype=np.uint32)
+        o[:need] = sample[:need]  # the data shards; parity rows are recomputed
+        objs.append(o)
     reps = [0] * threads
+    first = {}
     deadline = time.perf_counter() + seconds
 
     def work(t, o):
         while True:
             OC.encode_object(o, need, total)
-            rc, _ = OC.recover_data([o[i] for i in have], have)
+            rc, rec = OC.recover_data([o[i] for i in have], have)
             assert rc == 0
+            if t == 0 and not first:
+                first["parity"] = o[need:].copy()
+                first["data"] = rec
             reps[t] += 1
             if time.perf_counter() >= deadline:
                 return
@@ -238,8 +278,8 @@ def _cpu_leg(OC, need: int, total: int, have: list[int], threads: int, sample_mi
         t.join()
     dt = time.perf_counter() - t0
     nbytes = 2 * sum(reps) * need * L * 4  # encode + decode of each object pass
-    return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads, "object_mib": sample_mib,
-            "object_passes": sum(reps), "seconds": round(dt, 2)}
+    return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads,
+            "object_passes": sum(reps), "seconds": round(dt, 2), "_first": first}
 
 
 def _matrix_cores(k: int, rows: int) -> bool:
@@ -255,12 +295,18 @@ def _matrix_cores(k: int, rows: int) -> bool:
     return k >= 33 or (k >= 17 and k * rows >= 128)
 
 
-def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, seconds: float) -> dict:
-    """The reference's algorithm on host cores: the oracle's
-    faithful C restatement, one object per thread as the reference runs it
-    (the RS math is single-threaded per object, multi_store.go:528-531), on 1
-    thread and on every core this process may run on (sched_getaffinity).
-    `value` is the all-core figure."""
+def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[int], seconds: float) -> dict:
+    """The reference's algorithm on host cores, on the
+    bench's own input: `sample` is one object of the timed batch copied out of
+    HBM after the timed steps (total x L symbols: its data shards and the
+    parity the GPU wrote).  The oracle's faithful C restatement runs one object
+    per thread, as the reference does (the RS math is single-threaded per
+    object, multi_store.go:528-531), on 1 thread and on every core this
+    process may run on.  `value` is the all-core figure; `verified`: the CPU's
+    parity equals the GPU's for that object and its RecoverData gives back
+    the data shards."""
+    import numpy as np
+
     from oracle import oracle_c as OC
 
     have = [i for i in range(total) if i not in erase][:need]
@@ -270,20 +316,23 @@ def cpu_baseline(need: int, total: int, erase: list[int], sample_mib: int, secon
     affinity = len(os.sched_getaffinity(0))
     quota = _cgroup_cpus()
     ncores = max(1, min(affinity, int(quota))) if quota else affinity
-    one = _cpu_leg(OC, need, total, have, 1, sample_mib, seconds * 0.4)
-    # Smaller objects when there are many cores keep the sample's memory and
-    # setup time bounded (threads x 1.5 x object bytes resident).
-    all_mib = sample_mib if ncores <= 16 else max(8, sample_mib // 4)
-    allc = _cpu_leg(OC, need, total, have, ncores, all_mib, seconds * 0.6)
+    one = _cpu_leg(OC, sample, need, total, have, 1, seconds * 0.4)
+    first = one.pop("_first")
+    ok = bool(np.array_equal(first["parity"], sample[need:])) and \
+        all(np.array_equal(first["data"][t], sample[t]) for t in range(need))
+    allc = _cpu_leg(OC, sample, need, total, have, ncores, seconds * 0.6)
+    allc.pop("_first")
+    mib = sample.shape[1] * need * 4 / (1 << 20)
     return {"value": allc["value"], "unit": "GiB/s", "cores": ncores, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": affinity,
-            "cgroup_cpu_quota": quota,
+            "cgroup_cpu_quota": quota, "verified": ok,
             "single_thread": one, "all_cores": allc,
-            "sample": f"need={need} total={total}: per object, r CreateParity passes (multi_store.go:528-531) + "
-                      f"RecoverData(erase {erase}) recomputing all need rows (vector.go:80-85); 1 thread on "
-                      f"{one['object_mib']} MiB objects ({one['object_passes']} passes in {one['seconds']} s) and "
-                      f"{ncores} threads on {all_mib} MiB objects ({allc['object_passes']} passes in "
-                      f"{allc['seconds']} s); oracle/rs_oracle.c, gcc -O2"}
+            "sample": f"{sample_name} ({mib:.0f} MiB of data shards, copied from HBM after the timed steps), "
+                      f"need={need} total={total}: per object, r CreateParity passes (multi_store.go:528-531) + "
+                      f"RecoverData(erase {erase}) recomputing all need rows (vector.go:80-85); 1 thread "
+                      f"({one['object_passes']} passes in {one['seconds']} s) and {ncores} threads on copies of it "
+                      f"({allc['object_passes']} passes in {allc['seconds']} s); oracle/rs_oracle.c, gcc -O2; "
+                      "verified = the CPU's parity equals the GPU's for this object and RecoverData returns its data"}
 
 
 def batch_empty(args, numel: int, dtype: torch.dtype, dev: int) -> torch.Tensor:
@@ -512,8 +561,9 @@ def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
     reconstruct's slow path = MapToGFWith per survivor (:224) + RecoverData
     (:237) + MapFromGF per data row appended to make([]byte, 0, Size+16)
     (:204,238-241).  Each phase is timed; the split is the median call's.
-    alloc_ms: the same fresh output buffers allocated and first touched
-    alone (page faults + zeroing), the share of the phases that is Go's make()."""
+    alloc_alone: the same fresh output buffers allocated (as the mirrors
+    allocate them) and first touched by one thread (page faults), alone --
+    the part of the phases that is Go's make()."""
     import numpy as np
     from slime_amd import _native as N
     from slime_amd import gf, objects, rs
@@ -566,13 +616,13 @@ def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
 
     def alloc_write():
         bufs = [np.empty((data.size + 3) // 4, dtype=np.uint32)] + \
-               [np.zeros(L, dtype=np.uint32) for _ in range(r)] + [bytearray(4 * L) for _ in range(total)]
+               [np.zeros(L, dtype=np.uint32) for _ in range(r)] + [gf._new_bytearray(None, 4 * L) for _ in range(total)]
         for b in bufs:
             np.frombuffer(b, dtype=np.uint8)[::4096] = 1
         return None, []
 
     def alloc_read():
-        bufs = [np.empty(L, dtype=np.uint32) for _ in range(2 * need)] + [bytearray(4 * L) for _ in range(need)] + \
+        bufs = [np.empty(L, dtype=np.uint32) for _ in range(2 * need)] + [gf._new_bytearray(None, 4 * L) for _ in range(need)] + \
                [np.empty(data.size + 16, dtype=np.uint8)]
         for b in bufs:
             np.frombuffer(b, dtype=np.uint8)[::4096] = 1
@@ -727,6 +777,147 @@ def stream_ceilings(dev: int, stream, gib: int = 4, reps: int = 5) -> dict:
     return {"torch_copy_gbs": copy, "torch_fill_gbs": fill, "bytes": f"{gib} GiB per pass, median of {reps}"}
 
 
+class SymbolBatch:
+    """One rank's batch in HBM: nobj objects of S bytes as symbol-domain shards
+    ([object][shard][SS] uint32, SS = L rounded up to --shard-align), the need
+    data shards filled with seeded symbols; the encode plan (all total-need
+    parity rows) and the decode plan (the erased rows only, rebuilt into
+    their slots in place, or into a separate buffer with --decode-dst
+    separate).  One step = one encode launch + one decode launch."""
+
+    def __init__(self, args, dev: int, seed: int, need: int, total: int, S: int, nobj: int, erase: list[int],
+                 decode_dst: str = "inplace"):
+        self.need, self.total, self.S, self.nobj, self.erase = need, total, S, nobj, erase
+        self.have = [i for i in range(total) if i not in erase][:need]
+        self.L = L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) (multi_store.go:272)
+        # Shard stride SS >= L, rounded to --shard-align so every shard base is
+        # line-aligned (L = 26843546 at C5 would put every shard 8 B off a 16 B
+        # boundary; DESIGN.md "Line-aligned segments").  The pad columns are
+        # never read or written; the algorithmic bytes are L's.
+        self.SS = SS = ceil_div(L, max(1, args.shard_align)) * max(1, args.shard_align)
+        self.lay = D.layout_of(total, L, SS)
+        self.buf = batch_empty(args, max(1, nobj) * total * SS, torch.int32, dev)
+        self.placement = D.placement(self.buf) if args.allocator == "vmm" else None
+        D.fill_symbols(self.buf, seed)
+        self.enc = D.Plan.encode(need, total, dev)
+        self.dec = D.Plan.reconstruct(need, total, self.have, erase, dev)
+        self.decode_dst = decode_dst
+        if decode_dst == "inplace":
+            # Repair: rebuilt shards go back into their erased slots (the faster
+            # placement: output streams next to the input streams, DESIGN.md).
+            self.dec.set_outputs(erase)
+            self.rec, self.rec_lay = self.buf, self.lay
+        else:
+            self.rec = batch_empty(args, max(1, nobj) * len(erase) * SS, torch.int32, dev)
+            self.rec_lay = D.layout_of(len(erase), L, SS)
+        self.stream = torch.cuda.current_stream(dev)
+
+    def encode(self, buf=None):
+        b = self.buf if buf is None else buf
+        self.enc(b, self.lay, b, self.lay, self.L, self.nobj, stream=self.stream, dst_offset=self.need * self.SS)
+
+    def decode(self, buf=None):
+        b = self.buf if buf is None else buf
+        rec, rlay = (b, self.lay) if self.decode_dst == "inplace" else (self.rec, self.rec_lay)
+        self.dec(b, self.lay, rec, rlay, self.L, self.nobj, stream=self.stream)
+
+    def rebuilt(self):
+        """The erased rows as the decode wrote them (nobj x e x L)."""
+        if self.decode_dst == "inplace":
+            return self.buf.view(self.nobj, self.total, self.SS)[:, self.erase, :self.L]
+        return self.rec.view(self.nobj, len(self.erase), self.SS)[:, :, :self.L]
+
+    def run(self, steps: int, warmup: int) -> dict:
+        """The timed region: warmup untimed steps, then exactly `steps`, bracketed
+        by a barrier and a device synchronize on both sides; HIP events on the
+        launch stream around every launch.  Checks afterwards that every rebuilt
+        shard equals the true one (the data as filled and the parity of one
+        encode: encode is idempotent on fixed data)."""
+        if self.nobj == 0:
+            batch.barrier()
+            batch.barrier()
+            return {"elapsed": 0.0, "enc_all": [0.0], "dec_all": [0.0], "ok": True}
+        self.encode()
+        truth = self.buf.view(self.nobj, self.total, self.SS)[:, self.erase, :self.L].clone()
+        for _ in range(warmup):
+            self.encode()
+            self.decode()
+        torch.cuda.synchronize()
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        batch.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for ev in events:
+            ev[0].record(self.stream)
+            self.encode()
+            ev[1].record(self.stream)
+            self.decode()
+            ev[2].record(self.stream)
+        torch.cuda.synchronize()
+        batch.barrier()
+        elapsed = time.perf_counter() - t0
+        ok = bool(torch.equal(self.rebuilt(), truth))
+        del truth
+        return {"elapsed": elapsed, "enc_all": [e[0].elapsed_time(e[1]) for e in events],
+                "dec_all": [e[1].elapsed_time(e[2]) for e in events], "ok": ok}
+
+    def alg_bytes(self) -> tuple[int, int]:
+        """Algorithmic HBM bytes per launch: encode 4L(k + r),
+        decode 4L(k + e) per object."""
+        return (self.nobj * 4 * self.L * self.total, self.nobj * 4 * self.L * (self.need + len(self.erase)))
+
+    def free(self):
+        del self.buf, self.rec
+        torch.cuda.empty_cache()
+
+
+def apply_kernel_name(need: int, rows: int, L: int, shard_bytes_span: int) -> str:
+    """The kernel the library dispatches a launch of this shape to
+    (rs_apply.hip: the pipelined kernels for shards under 4 GiB unless the
+    kernel form was switched, with the dynamic (ticket) schedule for k <= 32
+    unless switched off; wide codes on the matrix cores, rs_apply_mfma.hip)."""
+    kname = "rs_apply_kernel"
+    if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
+        queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1 and \
+            (need <= 16 or os.environ.get("SLIME_RS_K32", "1")[:1] != "0")
+        kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
+    if _matrix_cores(need, rows) and shard_bytes_span < (1 << 32):
+        kname = "rs_apply_mfma_kernel"  # wide codes (rs_apply_mfma.hip)
+    return kname
+
+
+def c5_leg(args, dev: int, rank: int, world: int) -> dict:
+    """BASELINE config 5 inside every `bench.py --gpus N` run: need=10/total=14,
+    64 x 1 GiB objects partitioned over the N ranks (batch.partition: 64 at
+    N=1, 8 each at N=8), encode all parity + decode erased {0,1,2,3}.  Objects
+    are independent (multi_store.go:528-531), so there is no exchange: each
+    rank times its share and the leg's value is all 64 objects' bytes over the
+    max-over-ranks time ("strong": total work fixed as N grows)."""
+    need, total, mib, _, glob, erase_s = PRESETS["c5"]
+    erase = [int(x) for x in erase_s.split(",")]
+    first, nobj = batch.partition(glob, world, rank)
+    S = mib << 20
+    sb = SymbolBatch(args, dev, 0xC5C5 + 7919 * rank, need, total, S, nobj, erase)
+    res = sb.run(args.steps, args.warmup)
+    enc_ms = sum(res["enc_all"]) / len(res["enc_all"])
+    dec_ms = sum(res["dec_all"]) / len(res["dec_all"])
+    enc_alg, dec_alg = sb.alg_bytes()
+    kname = apply_kernel_name(need, total - need, sb.L, total * sb.SS * 4)
+    frac = (enc_alg + dec_alg) / 2 / ((enc_ms + dec_ms) / 2 * 1e-3) / 1e9 / HBM_PEAK_GBS if nobj else None
+    mine = {"rank": rank, "objects": [first, nobj], "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+            "frac": round(frac, 4) if frac else None, "verified": res["ok"], "placement": sb.placement}
+    sb.free()
+    per_rank = [json.loads(x) for x in batch.gather_strings(json.dumps(mine))]
+    elapsed, = batch.max_over_ranks([res["elapsed"]])
+    return {"value": round(2 * glob * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s", "scaling": "strong",
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "n_ranks": world,
+            "config": f"C5: need={need} total={total}, {glob} x {mib} MiB objects partitioned over {world} rank(s); "
+                      f"encode all parity + decode erased {erase}",
+            "kernel": f"{kname}<{need},vec>", "per_rank": per_rank,
+            "frac_min": min((p["frac"] for p in per_rank if p["frac"]), default=None),
+            "verified": all(p["verified"] for p in per_rank)}
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -753,11 +944,16 @@ def main():
     if args.dry_run:
         first, count = batch.partition(args.global_objects, world, rank) if args.global_objects else \
             (rank * args.objects, args.objects)
+        c5 = batch.partition(PRESETS["c5"][4], world, rank)
         parts = batch.gather_strings(json.dumps([rank, local, first, count]))
+        c5parts = batch.gather_strings(json.dumps([rank, local, c5[0], c5[1]]))
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_ranks": world, "need": args.need, "total": args.total,
                               "object_mib": args.object_mib, "scaling": "strong" if args.global_objects else "weak",
-                              "partitions": [json.loads(p) for p in parts]}), flush=True)
+                              "partitions": [json.loads(p) for p in parts],
+                              "c5_partitioned": None if not args.c5_leg else
+                              {"need": 10, "total": 14, "object_mib": 1024, "objects": PRESETS["c5"][4],
+                               "partitions": [json.loads(p) for p in c5parts]}}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -770,101 +966,28 @@ def main():
     if not erase or len(erase) > r or len(set(erase)) != len(erase) or not all(0 <= e < total for e in erase):
         print(f"bench.py: --erase needs 1..{r} distinct shard indices below total={total}", file=sys.stderr)
         sys.exit(2)
-    have = [i for i in range(total) if i not in erase][:need]
     S = args.object_mib << 20
-    L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) symbols (multi_store.go:272)
     if args.global_objects:
         _, nobj = batch.partition(args.global_objects, world, rank)
         total_objs, scaling = args.global_objects, "strong"
     else:
         nobj, total_objs, scaling = args.objects, args.objects * world, "weak"
-    # Device layout: shard stride SS >= L symbols, rounded to --shard-align so
-    # every shard base is line-aligned (L = 26843546 at C5 would put every
-    # shard 8 B off a 16 B boundary; DESIGN.md "Line-aligned segments").  The
-    # pad columns are never read or written; the algorithmic bytes are L's.
-    SS = ceil_div(L, max(1, args.shard_align)) * max(1, args.shard_align)
-    lay = D.layout_of(total, L, SS)
 
-    buf = batch_empty(args, nobj * total * SS, torch.int32, dev)
-    # How the library placed the batch buffer: probed placements and retries
-    # (slime_rs_device_alloc, DESIGN.md "Placement").
-    placement = D.placement(buf) if args.allocator == "vmm" else None
-    # Data shards: deterministic symbols, distinct per rank (synthetic objects).
-    D.fill_symbols(buf, 0x5113E + 7919 * rank)
-    enc = D.Plan.encode(need, total, dev)
-    dec = D.Plan.reconstruct(need, total, have, erase, dev)
-    if args.decode_dst == "inplace":
-        # Repair: rebuilt shards go back into their erased slots (the faster
-        # placement: output streams next to the input streams).
-        dec.set_outputs(erase)
-        rec, rec_lay = buf, lay
-    else:
-        rec = batch_empty(args, nobj * len(erase) * SS, torch.int32, dev)
-        rec_lay = D.layout_of(len(erase), L, SS)
-    stream = torch.cuda.current_stream(dev)
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * SS)
-        if ev is not None:
-            ev[1].record(stream)
-        dec(buf, lay, rec, rec_lay, L, nobj, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
-
-    # The true contents of every erased slot, before any decode has run: data
-    # shards as filled, parity shards from one encode (encode is idempotent on
-    # fixed data, so every timed step rewrites the same parity).
-    enc(buf, lay, buf, lay, L, nobj, stream=stream, dst_offset=need * SS)
-    truth = buf.view(nobj, total, SS)[:, erase, :L].clone()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    batch.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize()
-    batch.barrier()
-    elapsed = time.perf_counter() - t0
-
-    enc_all = [e[0].elapsed_time(e[1]) for e in events]
-    dec_all = [e[1].elapsed_time(e[2]) for e in events]
+    sb = SymbolBatch(args, dev, 0x5113E + 7919 * rank, need, total, S, nobj, erase, args.decode_dst)
+    L, SS, lay, placement = sb.L, sb.SS, sb.lay, sb.placement
+    res = sb.run(args.steps, args.warmup)
+    elapsed, enc_all, dec_all, ok = res["elapsed"], res["enc_all"], res["dec_all"], res["ok"]
     enc_ms = sum(enc_all) / args.steps
     dec_ms = sum(dec_all) / args.steps
-
-    # Correctness of what was timed: every rebuilt shard equals the true one.
-    got = buf.view(nobj, total, SS)[:, erase, :L] if args.decode_dst == "inplace" \
-        else rec.view(nobj, len(erase), SS)[:, :, :L]
-    ok = bool(torch.equal(got, truth))
-    del truth
-
     elapsed, enc_ms_max, dec_ms_max, bad = batch.max_over_ranks([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0])
 
     obj_bytes = nobj * S
     total_bytes = 2 * total_objs * S * args.steps
     value = total_bytes / GIB / elapsed
-    # Algorithmic HBM bytes per launch: encode 4L(k + r),
-    # decode 4L(k + e) per object.
-    enc_alg = nobj * 4 * L * (need + r)
-    dec_alg = nobj * 4 * L * (need + len(erase))
+    enc_alg, dec_alg = sb.alg_bytes()
     launch_ms = (enc_ms + dec_ms) / 2
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
-    # The product dispatch (rs_apply.hip): the pipelined kernels for shards
-    # under 4 GiB unless the kernel form was switched (slime_rs_kernel_pipeline),
-    # with the dynamic (ticket) schedule for k <= 32 unless slime_rs_kernel_schedule
-    # switched it off (17 <= k <= 32: unless SLIME_RS_K32=0 chose the wide kernels).
-    kname = "rs_apply_kernel"
-    if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
-        queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1 and \
-            (need <= 16 or os.environ.get("SLIME_RS_K32", "1")[:1] != "0")
-        kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
-    if _matrix_cores(need, total - need) and total * SS * 4 < (1 << 32):
-        kname = "rs_apply_mfma_kernel"  # wide codes (rs_apply_mfma.hip)
+    kname = apply_kernel_name(need, r, L, total * SS * 4)
     # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
     # --pmc passes of their own).  It is replayed from the summary of such
     # passes only when they were taken on this config AND this kernel source,
@@ -883,6 +1006,12 @@ def main():
             traffic = None
     # Distinct devices across ranks (n_gpus), by PCI address.
     bdfs = batch.gather_strings(board_info(dev)["bdf"])
+    # The CPU baseline's input: object 0 of this batch as the GPU left it
+    # (data shards + the parity of the timed encodes), copied out before the
+    # buffer is freed.
+    cpu_sample = None
+    if rank == 0 and world == 1 and args.cpu_baseline and nobj:
+        cpu_sample = sb.buf.view(nobj, total, SS)[0, :, :L].cpu().numpy().view("uint32").copy()
 
     host = None
     want_host = rank == 0 and world == 1 and args.host_path
@@ -900,23 +1029,22 @@ def main():
         host = run_host_leg()
     # After the host leg: the probe's buffers go back to the driver, whose
     # wipe of freed VRAM would slow the host leg's DMA (DESIGN.md End-to-end).
-    ceilings = stream_ceilings(dev, stream) if args.ceilings else None
+    ceilings = stream_ceilings(dev, sb.stream) if args.ceilings else None
     # The same batch in a hipMalloc'd (torch.empty) buffer, a few launches: what
     # the allocator choice is worth in this process (DESIGN.md "the allocator
     # changes the odds").  Not part of `value`.
     alloc_probe = None
-    if args.allocator == "vmm" and args.alloc_probe:
+    if args.allocator == "vmm" and args.alloc_probe and nobj:
         alt = torch.empty(nobj * total * SS, dtype=torch.int32, device=f"cuda:{dev}")
         D.fill_symbols(alt, 0x5113E + 7919 * rank)
         pe, pd = [], []
         for k in range(4):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            ev[0].record(stream)
-            enc(alt, lay, alt, lay, L, nobj, stream=stream, dst_offset=need * SS)
-            ev[1].record(stream)
-            dec(alt, lay, alt if args.decode_dst == "inplace" else rec, lay if args.decode_dst == "inplace" else rec_lay,
-                L, nobj, stream=stream)
-            ev[2].record(stream)
+            ev[0].record(sb.stream)
+            sb.encode(alt)
+            ev[1].record(sb.stream)
+            sb.decode(alt)
+            ev[2].record(sb.stream)
             torch.cuda.synchronize()
             if k:
                 pe.append(ev[0].elapsed_time(ev[1]))
@@ -926,13 +1054,14 @@ def main():
         alloc_probe = {"buffer": "torch.empty (hipMalloc)", "encode_ms": round(pem, 4), "decode_ms": round(pdm, 4),
                        "frac": round((enc_alg + dec_alg) / 2 / ((pem + pdm) / 2 * 1e-3) / 1e9 / 8000.0, 4),
                        "launches": 3}
-    bytes_path = None
-    if args.bytes_path:
-        del buf, rec  # rec aliases buf for in-place repair
-        torch.cuda.empty_cache()
-        bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj)
+    sb.free()
+    bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj) if args.bytes_path else None
     if want_host and args.host_order == "after-free":
         host = run_host_leg()
+    c5 = None
+    is_c5 = (need, total, args.object_mib, args.global_objects) == (10, 14, 1024, 64)
+    if args.c5_leg and not is_c5:
+        c5 = c5_leg(args, dev, rank, world)
 
     if rank == 0:
         line = {
@@ -979,18 +1108,20 @@ def main():
             "cpu_baseline": None,
             "rehearsal": (f"{world} ranks sharing {len(set(bdfs))} GPU(s) (SLIME_BENCH_SHARE_GPU=1): "
                           "a test of the multi-rank path, not a scaling number") if shared_gpu_rehearsal() else None,
+            "c5_partitioned": c5,
             "object_bytes_path": bytes_path,
             "allocator_probe": alloc_probe,
         }
         line["device"] = board_info(dev)
         if host is not None:
             line["host_path"] = host
-        if world == 1 and args.cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(need, total, erase, args.cpu_sample_mib, args.cpu_seconds)
+        if cpu_sample is not None:
+            line["cpu_baseline"] = cpu_baseline(cpu_sample, f"object 0 of this run's batch ({args.object_mib} MiB)",
+                                                need, total, erase, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if bad:
+    if bad or (c5 is not None and not c5["verified"]):
         sys.exit(3)
 
 

@@ -4,6 +4,7 @@
 #include <immintrin.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -150,6 +151,23 @@ __attribute__((target("avx2"))) void mod_avx2(const uint32_t* in, uint64_t count
   mod_scalar(in + i, count - i, out + i);
 }
 
+// Output buffers of the Go API are fresh (Go's make, a Python bytearray or
+// numpy array): their first touch is this pass, one 4 KiB page fault at a
+// time.  Ranges of at least 4 MiB are advised to fault as 2 MiB pages
+// (transparent huge pages in "madvise" mode) before the pass writes them --
+// a hint on the 2 MiB-aligned interior only, ignored where it does not apply
+// (env SLIME_RS_CODEC_HUGEPAGE=0 turns it off).
+void advise_huge(void* p, uint64_t bytes) {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_CODEC_HUGEPAGE");
+    return !(e && e[0] == '0');
+  }();
+  constexpr uintptr_t kHuge = 2u << 20;
+  if (!on || bytes < (4u << 20)) return;
+  const uintptr_t lo = ((uintptr_t)p + kHuge - 1) & ~(kHuge - 1), hi = ((uintptr_t)p + bytes) & ~(kHuge - 1);
+  if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
+}
+
 // ---- splitting a pass into pieces ----------------------------------------------
 
 uint64_t pieces_of(uint64_t words) { return words <= kSerialWords ? 1 : (words + kPieceWords - 1) / kPieceWords; }
@@ -178,6 +196,7 @@ const char* host_codec_isa() { return use_avx2() ? "avx2" : "scalar"; }
 void host_pack(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out, uint32_t* flags) {
   const uint64_t whole = len / 4;
   const bool track = flags != nullptr;
+  advise_huge(out, 4 * ((len + 3) / 4));
   std::atomic<uint32_t> m0{0}, m1{0};
   run_pieces(whole, [&](uint64_t w0, uint64_t nw) {
     uint32_t a = 0, b = 0;
@@ -204,6 +223,7 @@ void host_pack(const uint8_t* in, uint64_t len, uint32_t n, uint32_t* out, uint3
 }
 
 void host_unpack(const uint32_t* in, uint64_t count, uint32_t n, uint8_t* out) {
+  advise_huge(out, 4 * count);
   run_pieces(count, [&](uint64_t w0, uint64_t nw) {
     if (use_avx2())
       unpack_avx2(in + w0, nw, n, out + 4 * w0);
@@ -232,6 +252,7 @@ bool host_mapping_fits(const uint32_t* w, uint64_t count, uint32_t n) {
 }
 
 void host_mod_p(const uint32_t* in, uint64_t count, uint32_t* out) {
+  if (in != out) advise_huge(out, 4 * count);
   run_pieces(count, [&](uint64_t w0, uint64_t nw) {
     if (use_avx2())
       mod_avx2(in + w0, nw, out + w0);

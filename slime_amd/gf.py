@@ -60,15 +60,22 @@ def MapToGFWith(data, n: int) -> np.ndarray:
     return out
 
 
+_new_bytearray = ctypes.pythonapi.PyByteArray_FromStringAndSize
+_new_bytearray.restype = ctypes.py_object
+_new_bytearray.argtypes = [ctypes.c_char_p, ctypes.c_ssize_t]
+
+
 def MapFromGF(n: int, v) -> bytearray:
     """map.go:103 — symbols XOR n as big-endian bytes (length 4*len(v)).
 
     Returns a bytearray: Go's []byte is mutable (and, like a bytearray, not
     usable as a map key), and the library writes the result in place with no
-    extra 4*len(v)-byte copy.  Use bytes(...) where an immutable, hashable
-    value is needed."""
+    extra 4*len(v)-byte copy.  The bytearray is created uninitialised (every
+    byte is written by the codec), so its pages are first touched by the
+    codec's threads, not by a zero-fill.  Use bytes(...) where an immutable,
+    hashable value is needed."""
     words = np.ascontiguousarray(v, dtype=np.uint32)
-    out = bytearray(words.size * 4)
+    out = _new_bytearray(None, words.size * 4)
     ptr = (ctypes.c_char * len(out)).from_buffer(out) if out else None
     N.check(lib.slime_gf_map_from_gf(n & 0xFFFFFFFF, words.ctypes.data if words.size else None, words.size,
                                      ctypes.addressof(ptr) if ptr is not None else None))

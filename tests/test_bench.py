@@ -55,6 +55,47 @@ def test_gpus_n_launches_n_ranks_that_agree_on_the_partition():
     assert line["partitions"] == [[0, 0, 0, 32], [1, 1, 32, 32]]
 
 
+def test_dry_run_reports_the_c5_partition_at_every_n():
+    """Every `bench.py --gpus N` run carries BASELINE config 5 as a second leg:
+    64 x 1 GiB objects (10/14) partitioned over the N ranks -- 32 + 32 at
+    N = 2, 8 x 8 at N = 8 -- beside the weak-scaling C3 leg."""
+    r = _bench(["--gpus", "2", "--dry-run"], SLIME_BENCH_DEVICE_COUNT="2")
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    c5 = line["c5_partitioned"]
+    assert (c5["need"], c5["total"], c5["object_mib"], c5["objects"]) == (10, 14, 1024, 64)
+    assert c5["partitions"] == [[0, 0, 0, 32], [1, 1, 32, 32]]
+    r = _bench(["--gpus", "8", "--dry-run"], SLIME_BENCH_DEVICE_COUNT="8")
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["partitions"] == [[i, i, 128 * i, 128] for i in range(8)]
+    assert line["c5_partitioned"]["partitions"] == [[i, i, 8 * i, 8] for i in range(8)]
+
+
+def test_gpu_count_reads_sysfs_not_hip(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the KFD topology (CPU nodes have no SIMDs;
+    a GPU whose render node this process cannot open is not counted) and the
+    visibility variables, without starting the HIP runtime."""
+    bench = _load("bench.py", "bench_mod_kfd")
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for i, (simds, minor) in enumerate([(0, None), (1024, 128), (1024, 129), (1024, 130)]):
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        props = f"cpu_cores_count 64\nsimd_count {simds}\n" + (f"drm_render_minor {minor}\n" if minor else "")
+        (d / "properties").write_text(props)
+    for minor in (128, 129):  # node 3's render node is not in this container
+        (dri / f"renderD{minor}").write_text("")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.kfd_gpus(str(nodes), str(dri)) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert bench.kfd_gpus(str(nodes), str(dri)) == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.kfd_gpus(str(nodes), str(dri)) == 0
+    assert bench.kfd_gpus(str(tmp_path / "absent"), str(dri)) == 0
+
+
 def test_gpus_n_beyond_visible_devices_exits_2():
     """--gpus 2 with fewer visible GPUs: exit 2 with a message, never a line
     claiming one GPU for a multi-GPU request."""

@@ -27,6 +27,8 @@ nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" 
 for step in "$@"; do
   case "$step" in
     tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct" ;;
+    kfd) run kfd 120 python -c "import sys; sys.argv=['bench.py']; sys.path.insert(0, '.'); import bench, torch; print('kfd_gpus', bench.kfd_gpus(), 'torch', torch.cuda.device_count())" ;;
+    rehearse2) SLIME_BENCH_SHARE_GPU=1 run rehearse2 400 python bench.py --gpus 2 --steps 5 --warmup 1 $NOLEGS --bytes-path 0 --ceilings 0 ;;
     tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     tests_sched) run pytest_sched 400 python -u -m pytest tests/test_gpu_schedule.py -x -v --timeout 120 --timeout-method thread ;;
     tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
