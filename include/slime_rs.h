@@ -70,6 +70,9 @@ int slime_rs_device_count(void);
  * (SLIME_RS_ANY_DEVICE, the default, returns them to the pool).  Thread-local:
  * callers whose threads migrate between calls (Go) use the *_ex forms. */
 int slime_rs_select_device(int device);
+/* The calling thread's selection (SLIME_RS_ANY_DEVICE if none): lets a scope
+ * that selects a device restore the one it found. */
+int slime_rs_selected_device(void);
 
 /* Per-call context of the *_ex entry points, for callers that must not depend
  * on thread-local state between calls (cgo: a goroutine may run consecutive
@@ -99,10 +102,15 @@ int slime_rs_host_pipeline(int mode);
  * non-pipelined forms that larger shards always take.  mode < 0 queries.
  * Results are identical; the parity tests run both. */
 int slime_rs_kernel_pipeline(int mode);
-/* Work schedule of the pipelined apply kernels for k <= 32 (process-wide; env
- * SLIME_RS_QUEUE=0 sets the initial value): 1 = dynamic, waves take units of
- * work from ticket counters (default); 0 = static shares per wave.  mode < 0
- * queries.  Results are identical; the parity tests run both. */
+/* Work schedule of the pipelined kernels for k <= 32 (process-wide; env
+ * SLIME_RS_QUEUE=0/1/2 sets the initial value): 1 = dynamic, waves take units
+ * of work from ticket counters, except inside a graph capture, where the
+ * static kernels are captured (default); 2 = dynamic inside captures too --
+ * the captured launch keeps a counter set for the graph's life (returned to
+ * the library when the graph and its execs are destroyed), so a graph holding
+ * one must not be replayed by two execs at the same time; 0 = static shares
+ * per wave.  mode < 0 queries.  Results are identical; the parity tests run
+ * every mode. */
 int slime_rs_kernel_schedule(int mode);
 /* Wide codes (k >= 33, or 17 <= k <= 32 with k x rows >= 128; up to 32 output
  * rows and k <= 112) on the matrix cores
@@ -403,6 +411,10 @@ int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
  * launch has finished (each launch leaves its set zero; DESIGN.md "Dynamic
  * schedule"). */
 int slime_rs_ticket_sets(int device, uint64_t *sets, uint64_t *held);
+/* Launches on `device` since start that ran the dynamic schedule on a counter
+ * set, and that were sent to the static kernels instead (inside a capture
+ * under mode 1, or no set to be had) -- diagnostics and tests. */
+int slime_rs_schedule_counts(int device, uint64_t *dynamic, uint64_t *fallback);
 
 /* ==== chunk and object digests ======================
  * Host computations on the library's digest threads (DESIGN.md "Chunk

@@ -14,7 +14,6 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-import threading
 
 try:  # noqa: SIM105 - see module docstring
     import torch  # noqa: F401
@@ -73,6 +72,7 @@ SIGNATURES = [
     ("slime_rs_version", ctypes.c_char_p, []),
     ("slime_rs_device_count", ctypes.c_int, []),
     ("slime_rs_select_device", ctypes.c_int, [ctypes.c_int]),
+    ("slime_rs_selected_device", ctypes.c_int, []),
     ("slime_rs_host_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
@@ -174,6 +174,7 @@ SIGNATURES = [
     ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
     ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
     ("slime_rs_ticket_sets", ctypes.c_int, [ctypes.c_int, c_u64p, c_u64p]),
+    ("slime_rs_schedule_counts", ctypes.c_int, [ctypes.c_int, c_u64p, c_u64p]),
     ("slime_rs_host_stats", ctypes.c_int, [ctypes.POINTER(HostStats), ctypes.c_int]),
     # chunk and object digests (host)
     ("slime_rs_sha256", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
@@ -307,7 +308,11 @@ def ticket_sets(device: int) -> tuple[int, int]:
     return int(s.value), int(h.value)
 
 
-_selected = threading.local()
+def schedule_counts(device: int) -> tuple[int, int]:
+    """(launches that ran the dynamic schedule on a counter set, launches sent to the static kernels)."""
+    d, f = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.slime_rs_schedule_counts(device, ctypes.byref(d), ctypes.byref(f)))
+    return int(d.value), int(f.value)
 
 
 @contextlib.contextmanager
@@ -315,20 +320,18 @@ def on_device(device: int | None):
     """Route the calling thread's host entry points (rs.*, gf.*, objects.*) to
     `device` for the block (slime_rs_select_device); None leaves the routing as
     it is (the device pool picks).  A rank that owns one GPU wraps its host
-    calls in this, so they never spread onto other ranks' devices."""
+    calls in this, so they never spread onto other ranks' devices.  On exit
+    the thread's previous selection is restored -- whether it came from an
+    enclosing block or a direct slime_rs_select_device call."""
     if device is None:
         yield
         return
-    stack = getattr(_selected, "stack", None)
-    if stack is None:
-        stack = _selected.stack = []
+    prev = int(lib.slime_rs_selected_device())
     check(lib.slime_rs_select_device(int(device)))
-    stack.append(int(device))
     try:
         yield
     finally:
-        stack.pop()
-        check(lib.slime_rs_select_device(stack[-1] if stack else ANY_DEVICE))
+        check(lib.slime_rs_select_device(prev))
 
 
 def pool_calls(device: int) -> tuple[int, int]:

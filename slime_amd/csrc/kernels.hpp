@@ -80,14 +80,14 @@ bool k32_kernels();
 // not (the form larger ones always take).  Process-wide; see rs_apply.hip.
 bool pipelined_kernels();
 void set_pipelined_kernels(bool on);
-// Work schedule of the k <= 16 pipelined apply kernels: 1 dynamic (ticket
-// counters, default), 0 static shares.  Process-wide; see rs_apply.hip.
+// Work schedule of the pipelined kernels: 1 dynamic (ticket counters) outside
+// graph captures and static inside (default), 2 dynamic in captures too, 0
+// static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
-// Whether launches may take the dynamic schedule (the mode is on).  Graph
-// capture is allowed: a launch resets its own counter set (TicketWalk::finish),
-// so a captured launch replays on the set it was captured with.
-inline bool queue_allowed(hipStream_t) { return queue_mode() == 1; }
+// Whether a launch on `s` may take the dynamic schedule under the mode (a
+// captured launch replays on the set it was captured with: mode 2 only).
+bool queue_allowed(hipStream_t s);
 // Ticket counters of the dynamic-schedule kernels (rs_apply_queue_kernel):
 // kQueueCounters draw counters + an exit counter per set (zero whenever no
 // launch holds the set).  Takes a set that no unfinished launch holds from
@@ -103,6 +103,9 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
 hipError_t warm_ticket_pool(int device);
 // Sets allocated / held by launches in flight or graphs, for `device` (tests).
 void ticket_pool_stats(int device, uint64_t* sets, uint64_t* held);
+// Launches on `device` that took a counter set (dynamic) / were sent to the
+// static kernel by with_tickets (capture under mode 1, or no set to be had).
+void schedule_counts(int device, uint64_t* dynamic, uint64_t* fallback);
 
 // Column segments per object for a launch over nobj objects of ncols
 // columns (the apply and byte kernels cut each object into this many
@@ -137,6 +140,14 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
 // (mapping 0, OR MapToGF flag bits into flags[obj]); select_mapping turns the
 // flags into mapping[] and a fallback status in place; phase 1 re-encodes the
 // objects with mapping != 0 and status == 0.  Decode uses mapping[obj].
+// What phase 0 of the fused encode did (BytesLaunch::sw): whether it ran the
+// mid-object-switching kernel, and the unit layout it ran with -- phase 1
+// redoes units by this record, never by re-deriving it from process-wide
+// state that another thread may have changed in between.
+struct SwitchRecord {
+  bool switched = false;
+  uint32_t spread = 0, nint = 0, units = 0;
+};
 struct BytesLaunch {
   uint8_t* slots;
   uint64_t slot_stride;
@@ -153,11 +164,12 @@ struct BytesLaunch {
   uint64_t ncols = 0;  // 0: the whole chunk (L columns)
   // Mid-object mapping switch (encode_bytes_queue_kernel): device scratch of
   // encode_switch_bytes(a) bytes, or null.  Phase 0 with scratch records each
-  // unit's mapping there and sets *switched when it ran the switching kernel;
-  // phase 1 given the same scratch (only if *switched) redoes just the units
-  // that used the wrong mapping.  Null: phase 1 re-encodes whole objects.
+  // unit's mapping there and fills *sw (switched + its unit layout) when it
+  // ran the switching kernel; phase 1 given the same scratch and record (only
+  // if sw->switched) redoes just the units that used the wrong mapping.
+  // Null: phase 1 re-encodes whole objects.
   uint8_t* scratch = nullptr;
-  bool* switched = nullptr;
+  SwitchRecord* sw = nullptr;
   uint64_t cstride = 0;  // bytes between a slot's chunks (0: 4L, the wire layout)
   // Matrix-core form (rs_bytes_mfma.hip): the plan's byte-order digit table
   // or null, and the highest input / output chunk index.

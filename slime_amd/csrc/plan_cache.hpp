@@ -40,10 +40,15 @@ class LruCache {
  public:
   explicit LruCache(size_t capacity) : cap_(capacity ? capacity : 1) {}
 
+  // Status get() returns when make() threw (e.g. std::bad_alloc from a host
+  // table): the build counts as failed, like a nonzero status.
+  static constexpr int kBuildThrew = -2;
+
   // The value for `key`: cached, or built by make(key, &raw) (status int, 0 =
   // ok, ownership of raw passes to the cache with `del` as its deleter).  On
-  // a failed build nothing is cached and make's status is returned; callers
-  // that waited on that build then build it themselves.
+  // a failed build -- a nonzero status or an exception (kBuildThrew) --
+  // nothing is cached, every caller waiting on that build is woken, and the
+  // failure is returned; the waiters then build it themselves.
   template <class Make, class Del>
   int get(const Key& key, std::shared_ptr<Val>* out, Make&& make, Del del) {
     for (;;) {
@@ -69,9 +74,21 @@ class LruCache {
       dropped.clear();
       if (build) {
         Val* raw = nullptr;
-        const int rc = make(key, &raw);
+        int rc;
+        try {
+          rc = make(key, &raw);
+        } catch (...) {
+          rc = kBuildThrew;
+          raw = nullptr;
+        }
         std::shared_ptr<Val> v;
-        if (rc == 0) v = std::shared_ptr<Val>(raw, del);
+        if (rc == 0) {
+          try {
+            v = std::shared_ptr<Val>(raw, del);  // on bad_alloc the constructor calls del(raw)
+          } catch (...) {
+            rc = kBuildThrew;
+          }
+        }
         {
           std::lock_guard<std::mutex> sl(slot->mu);
           slot->value = v;

@@ -217,11 +217,17 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
 // fixed number of sets.  Other streams' launches get new sets (up to
 // kMaxSets, then they too wait for the oldest holder).
 //
-// A launch captured into a graph keeps its set for the graph's life: every
-// replay leaves it zero for the next.  Captured launches never wait on
-// events from outside the capture and never create slabs: with no free set
-// they take the static kernel.  Sets come in slabs of kSlabSets, zeroed
-// synchronously when created.
+// Inside a graph capture the default schedule (mode 1) launches the static
+// kernels: a set is bound to the captured kernel node, so two execs of one
+// graph (instantiated twice, or cloned) replayed at the same time would draw
+// tickets from one set and skip each other's units.  Mode 2 captures the
+// dynamic kernels too (one exec of a graph at a time): such a launch keeps
+// its set for the graph's life -- every replay leaves it zero for the next --
+// and a HIP user object retained by the graph gives the set back to the pool
+// when the graph and its execs are destroyed.  Captured launches never wait
+// on events from outside the capture and never create slabs: with no free
+// set they take the static kernel.  Sets come in slabs of kSlabSets, zeroed
+// when created.
 namespace {
 constexpr uint32_t kSetWords = apply::ticket_set_words(kQueueCounters);
 constexpr int kSlabSets = 64;
@@ -235,16 +241,37 @@ struct TicketPool {
   std::mutex mu;
   std::vector<TicketSet> free_sets;  // zero, no launch holds them
   std::deque<TicketSet> busy;        // held by a launch, in launch order
-  uint64_t sets = 0, graph_held = 0;
+  uint64_t sets = 0, graph_held = 0, lost = 0;
+  uint64_t dynamic = 0, fallback = 0;  // launches on a set / sent to the static kernel
+  // Sets of destroyed graphs, handed back by a user-object destructor that
+  // may run on a runtime thread at any time: its own lock, never held across
+  // a HIP call, so it cannot wait on `mu`.
+  std::mutex ret_mu;
+  std::vector<TicketSet> returned;
 
+  void give_back(const TicketSet& s) {  // from a graph's user-object destructor
+    std::lock_guard<std::mutex> lk(ret_mu);
+    returned.push_back(s);
+  }
+  void drain_returned() {  // mu held
+    std::lock_guard<std::mutex> lk(ret_mu);
+    for (const TicketSet& s : returned) free_sets.push_back(s);
+    graph_held -= std::min<uint64_t>(graph_held, returned.size());
+    returned.clear();
+  }
   hipError_t grow() {  // mu held; not inside a capture
     void* p = nullptr;
     const size_t bytes = (size_t)kSlabSets * kSetWords * sizeof(uint32_t);
     if (hipError_t e = hipMalloc(&p, bytes)) return e;
-    // The null stream, then a wait for it: the zeroes are in memory before
-    // any stream (blocking or not) can launch on a set of this slab.
-    hipError_t e = hipMemset(p, 0, bytes);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    // Zeroed on a private non-blocking stream and waited for there only: the
+    // zeroes are in memory before any stream can launch on a set of this
+    // slab, and neither torch's default stream nor a capture in progress on
+    // another thread is synchronised (a legacy null-stream sync would be).
+    hipStream_t z = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&z, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, bytes, z);
+    if (e == hipSuccess) e = hipStreamSynchronize(z);
+    if (z) (void)hipStreamDestroy(z);
     if (e != hipSuccess) {
       (void)hipFree(p);
       return e;
@@ -259,6 +286,7 @@ struct TicketPool {
     return hipSuccess;
   }
   void reclaim() {  // mu held: every set whose launch has finished goes back
+    drain_returned();
     for (auto it = busy.begin(); it != busy.end();) {
       const hipError_t q = hipEventQuery(it->ev);
       if (q == hipSuccess) {
@@ -297,6 +325,43 @@ struct TicketPool {
     return true;
   }
 };
+// A captured launch's set, owned by the graph under capture: the destructor
+// of a user object the graph retains returns it to the pool.
+struct GraphSet {
+  TicketPool* pool;
+  TicketSet set;
+};
+void graph_set_release(void* p) {
+  GraphSet* g = (GraphSet*)p;
+  if (g->pool) g->pool->give_back(g->set);
+  delete g;
+}
+// Ties `set` to the graph `stream` is capturing into; false if HIP refused.
+bool bind_to_graph(TicketPool& tp, const TicketSet& set, hipStream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  if (hipStreamGetCaptureInfo_v2(stream, &st, &id, &graph, nullptr, nullptr) != hipSuccess || !graph ||
+      st != hipStreamCaptureStatusActive) {
+    (void)hipGetLastError();
+    return false;
+  }
+  GraphSet* g = new GraphSet{&tp, set};
+  hipUserObject_t obj = nullptr;
+  if (hipUserObjectCreate(&obj, g, graph_set_release, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+    (void)hipGetLastError();
+    delete g;
+    return false;
+  }
+  if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+    // The graph did not take the reference: keep the set (the object's
+    // destructor must not hand it back while the graph may replay it).
+    (void)hipGetLastError();
+    g->pool = nullptr;
+    return false;
+  }
+  return true;
+}
 TicketPool& ticket_pool(int dev) {
   static std::mutex mu;
   static auto* pools = new std::map<int, TicketPool>();  // never destroyed (see plan cache)
@@ -324,7 +389,14 @@ void ticket_pool_stats(int device, uint64_t* sets, uint64_t* held) {
   std::lock_guard<std::mutex> lock(tp.mu);
   tp.reclaim();
   *sets = tp.sets;
-  *held = tp.busy.size() + tp.graph_held;
+  *held = tp.busy.size() + tp.graph_held + tp.lost;
+}
+
+void schedule_counts(int device, uint64_t* dynamic, uint64_t* fallback) {
+  TicketPool& tp = ticket_pool(device);
+  std::lock_guard<std::mutex> lock(tp.mu);
+  *dynamic = tp.dynamic;
+  *fallback = tp.fallback;
 }
 
 hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint32_t*)>& launch, bool* launched) {
@@ -338,20 +410,39 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
   std::lock_guard<std::mutex> lock(tp.mu);
   TicketSet set;
   hipError_t e;
-  if (!tp.take(stream, cap, &set, &e)) return e;  // hipSuccess + !launched: static kernel
+  if (cap && queue_mode() != 2) {  // the static kernel inside captures (see above)
+    ++tp.fallback;
+    return hipSuccess;
+  }
+  if (!tp.take(stream, cap, &set, &e)) {  // hipSuccess + !launched: static kernel
+    if (e == hipSuccess) ++tp.fallback;
+    return e;
+  }
   e = launch(set.p);
   if (e != hipSuccess) {  // never started: the set is zero again once its holder (if any) is done
     tp.busy.push_back(set);
     return e;
   }
   *launched = true;
+  ++tp.dynamic;
   if (cap) {
-    ++tp.graph_held;  // the graph owns it from now on
+    ++tp.graph_held;  // the graph owns it from now on; its user object gives it back
+    if (!bind_to_graph(tp, set, stream)) {
+      --tp.graph_held;
+      ++tp.lost;  // held for the life of the process
+    }
     return hipSuccess;
   }
   if (const hipError_t r = hipEventRecord(set.ev, stream)) {
-    // Without the event the set's release cannot be observed: leave it held.
-    ++tp.graph_held;
+    // Without the event the set's release cannot be observed: wait for the
+    // launch here, then the set is free (zero) again.
+    (void)hipGetLastError();
+    if (hipStreamSynchronize(stream) == hipSuccess) {
+      tp.free_sets.push_back(set);
+    } else {
+      (void)hipGetLastError();
+      ++tp.lost;
+    }
     return r;
   }
   set.last = stream;
@@ -369,14 +460,19 @@ static std::atomic<int> g_pipelined{[] {
   return e && e[0] == '0' ? 0 : 1;
 }()};
 bool pipelined_kernels() { return g_pipelined.load(std::memory_order_relaxed) != 0; }
-// Work schedule of the k <= 16 pipelined kernels (process-wide): 1 = dynamic
-// (default), 0 = static shares.  Env SLIME_RS_QUEUE=0 sets the initial value;
+// Work schedule of the pipelined kernels (process-wide): 1 = dynamic outside
+// graph captures, static inside (default); 2 = dynamic in captures too; 0 =
+// static shares.  Env SLIME_RS_QUEUE=0/1/2 sets the initial value;
 // slime_rs_kernel_schedule() switches it.
 static std::atomic<int> g_queue_mode{[] {
   const char* e = getenv("SLIME_RS_QUEUE");
-  return e && e[0] == '0' ? 0 : 1;
+  return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
 }()};
 int queue_mode() { return g_queue_mode.load(std::memory_order_relaxed); }
+bool queue_allowed(hipStream_t s) {
+  const int m = queue_mode();
+  return m == 2 || (m == 1 && !capturing(s));
+}
 void set_queue_mode(int m) { g_queue_mode.store(m, std::memory_order_relaxed); }
 void set_pipelined_kernels(bool on) { g_pipelined.store(on ? 1 : 0, std::memory_order_relaxed); }
 

@@ -55,8 +55,11 @@ uint32_t switch_grid(uint64_t batch_units) {
 // with 1<<31.
 template <int K, int U, int C>
 hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
-  const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
-  if (!l.spread) return hipErrorInvalidValue;  // phase 0 cannot have switched
+  if (!a.sw || !a.sw->switched || !a.sw->spread) return hipErrorInvalidValue;  // phase 0 did not switch
+  SwitchLayout l;  // phase 0's layout, as it ran
+  l.spread = a.sw->spread;
+  l.nint = a.sw->nint;
+  l.units = a.sw->units;
   uint32_t* count = l.count(a.scratch);
   if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
   const uint64_t batch_units = (uint64_t)a.nobj * l.units;
@@ -90,7 +93,12 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
         return hipGetLastError();
       },
       launched);
-  if (*launched && record && a.switched) *a.switched = true;
+  if (*launched && record && a.sw) {
+    a.sw->switched = true;
+    a.sw->spread = l.spread;
+    a.sw->nint = l.nint;
+    a.sw->units = l.units;
+  }
   return e;
 }
 }  // namespace bytes

@@ -243,7 +243,10 @@ LruCache<PlanKey, slime_rs_plan>& plans() {
 }
 
 int cached_plan(const PlanKey& key, PlanRef* out, int (*make)(const PlanKey&, slime_rs_plan**)) {
-  return plans().get(key, out, make, destroy_plan);
+  const int rc = plans().get(key, out, make, destroy_plan);
+  if (rc == LruCache<PlanKey, slime_rs_plan>::kBuildThrew)
+    return fail(Status::Hip, "plan build failed: host allocation (exception in the plan builder)");
+  return rc;
 }
 
 // ---- per-call device workspaces (host entry points) ----------------------------
@@ -831,7 +834,10 @@ int slime_rs_kernel_pipeline(int mode) {
 
 int slime_rs_kernel_schedule(int mode) {
   if (mode < 0) return queue_mode();
-  if (mode > 1) return fail(Status::InvalidArg, "kernel_schedule: mode must be 0 (static) or 1 (dynamic)");
+  if (mode > 2)
+    return fail(Status::InvalidArg,
+                "kernel_schedule: mode must be 0 (static), 1 (dynamic outside graph captures) or 2 (dynamic also "
+                "in captures)");
   set_queue_mode(mode);
   return 0;
 }
@@ -849,6 +855,15 @@ int slime_rs_ticket_sets(int device, uint64_t* sets, uint64_t* held) {
   ticket_pool_stats(device, sets, held);
   return 0;
 }
+
+int slime_rs_schedule_counts(int device, uint64_t* dynamic, uint64_t* fallback) {
+  if (!dynamic || !fallback) return fail(Status::InvalidArg, "schedule_counts: null output");
+  if (int rc = check_device(device)) return rc;
+  schedule_counts(device, dynamic, fallback);
+  return 0;
+}
+
+int slime_rs_selected_device(void) { return t_device; }
 
 int slime_rs_select_device(int device) {
   if (device != SLIME_RS_ANY_DEVICE)
@@ -1167,13 +1182,16 @@ extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* sl
   BytesLaunch a0 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 0, status, mapping);
   ScratchLease sc;
   if (int rc = sc.take(plan->device, encode_switch_bytes(a0, s), s)) return rc;
-  bool switched = false;
+  SwitchRecord sw;
   a0.scratch = sc.ptr();
-  a0.switched = &switched;
+  a0.sw = &sw;
   HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
   BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 1, status, mapping);
-  if (switched) a1.scratch = sc.ptr();
+  if (sw.switched) {
+    a1.scratch = sc.ptr();
+    a1.sw = &sw;
+  }
   HIP_TRY(launch_encode_bytes(a1, s));
   sc.release(s);
   return 0;

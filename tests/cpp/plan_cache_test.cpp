@@ -11,12 +11,14 @@
 //   - builds run outside the cache lock: 8 threads missing 8 different keys
 //     with a 50 ms build finish in about 50 ms, not 400; 8 threads missing
 //     the SAME key share one build;
-//   - evicted values are released outside the lock (the deleter checks).
+//   - evicted values are released outside the lock (the deleter checks);
+//   - a build that throws wakes its waiters and caches nothing.
 // Usage: plan_cache_test   (exit 0 = pass)
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <new>
 #include <cstdlib>
 #include <random>
 #include <set>
@@ -230,6 +232,31 @@ int main() {
     CHECK(deleted.load() == 50 && locked.load() == 0 && g_tables.load() == 0);
     std::printf("ok   TestPlanCacheReleaseOutsideLock (50 evictions, no deleter under the lock)\n");
   }
-  std::printf("6/6 passed\n");
+  {  // a build that throws (bad_alloc in a host table): waiters wake, nothing cached, key usable again
+    LruCache<Key, FakePlan> cache(4);
+    std::atomic<int> calls{0}, threw{0};
+    auto throwing = [&](const Key& key, FakePlan** out) -> int {
+      if (calls.fetch_add(1) < 3) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(30));
+        throw std::bad_alloc();
+      }
+      return build(key, out);
+    };
+    std::vector<int> have = {0, 1, 2, 3, 4, 5, 6, 9};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 6; ++t)
+      ts.emplace_back([&] {
+        std::shared_ptr<FakePlan> p;
+        const int rc = cache.get(Key{0, 'R', 8, 0, have}, &p, throwing, del);
+        if (rc == LruCache<Key, FakePlan>::kBuildThrew && !p) ++threw;
+        else CHECK(rc == 0 && p && p->have == have);
+      });
+    for (auto& th : ts) th.join();  // a waiter left blocked forever would hang here
+    CHECK(threw.load() >= 1 && threw.load() <= 3);
+    std::shared_ptr<FakePlan> p;
+    CHECK(cache.get(Key{0, 'R', 8, 0, have}, &p, throwing, del) == 0 && is_inverse(*p, 8));
+    std::printf("ok   TestPlanCacheBuildThrows (%d of 6 callers saw the exception, none blocked)\n", threw.load());
+  }
+  std::printf("7/7 passed\n");
   return 0;
 }

@@ -1214,3 +1214,21 @@ def test_k17_to_32_byte_kernels_vs_oracle(torch_dev, kernel_form, need, total, S
     D.decode_objects(rec, slots, stride, L, 2, mapping)
     torch.cuda.synchronize()
     assert torch.equal(slots, truth), erase
+
+
+def test_on_device_restores_the_threads_previous_selection():
+    """N.on_device restores whatever the thread had selected before the block:
+    a direct slime_rs_select_device call, an enclosing block, or nothing."""
+    assert N.lib.slime_rs_selected_device() == N.ANY_DEVICE
+    N.check(N.lib.slime_rs_select_device(0))
+    try:
+        with N.on_device(0):
+            with N.on_device(0):
+                assert N.lib.slime_rs_selected_device() == 0
+            assert N.lib.slime_rs_selected_device() == 0
+        assert N.lib.slime_rs_selected_device() == 0, "the direct selection survives the block"
+    finally:
+        N.check(N.lib.slime_rs_select_device(N.ANY_DEVICE))
+    with N.on_device(0):
+        pass
+    assert N.lib.slime_rs_selected_device() == N.ANY_DEVICE

@@ -10,7 +10,9 @@ launches on one stream and on two streams.  Every launch leaves its counter
 set zero and the library hands a set only to a launch no unfinished launch
 shares it with, whatever the stream: hipStreamPerThread from two threads, a
 stream destroyed with its launch in flight and its handle reused, and a
-launch captured into a graph and replayed are all exact.
+launch captured into a graph and replayed are all exact.  Graph captures take
+the static kernels by default (mode 1) and the dynamic ones under mode 2,
+whose sets go back to the pool when the graph and its execs die.
 """
 import ctypes
 import threading
@@ -60,9 +62,9 @@ def _encode_ref(h, need, total):
 
 
 def test_schedule_switch_rejects_unknown_modes(schedule):
-    assert schedule(-1) in (0, 1)
-    for m in (0, 1):
-        assert schedule(2) != 0 and schedule(-1) in (0, 1)
+    assert schedule(-1) in (0, 1, 2)
+    for m in (0, 1, 2):
+        assert schedule(3) != 0 and schedule(-1) in (0, 1, 2)
         assert schedule(m) == 0 and schedule(-1) == m
 
 
@@ -160,15 +162,17 @@ def test_dynamic_schedule_full_batch_matches_static(torch_dev, schedule):
     assert torch.equal(first, buf.view(nobj, total, L)[:, need:])
 
 
-def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
-    """A captured launch replays with the same arguments, its ticket counter
-    set included: each replay leaves the set zero for the next, so captured
-    launches keep the dynamic schedule (the graph holds one set per captured
-    queue launch).  Replay a captured encode and repair three times over
-    changing data, every time exact."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_graph_captured_launches_replay_exactly(torch_dev, schedule, mode):
+    """A captured launch replays with the same arguments.  Mode 1 (default)
+    captures the static kernels (no counter set bound to the graph); mode 2
+    captures the dynamic ones, each holding its counter set for the graph's
+    life (every replay leaves it zero for the next).  Replay a captured encode
+    and repair three times over changing data, every time exact; destroying
+    the graph gives mode 2's sets back."""
     torch = torch_dev
     from slime_amd import device as D
-    assert schedule(1) == 0
+    assert schedule(mode) == 0
     need, total, nobj, L = 8, 12, 9, 3 * 768 * 4 + 5
     erase = [0, 3, 8, 11]
     have = [i for i in range(total) if i not in erase][:need]
@@ -183,13 +187,18 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
         enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
     torch.cuda.synchronize()
     _, held0 = N.ticket_sets(0)
+    dyn0, fb0 = N.schedule_counts(0)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         enc(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)
         rec(buf, lay, out, D.layout_of(len(erase), L), L, nobj, stream=s)
     torch.cuda.synchronize()
     _, held1 = N.ticket_sets(0)
-    assert held1 == held0 + 2, "both captured launches took the dynamic schedule"
+    dyn1, fb1 = N.schedule_counts(0)
+    if mode == 2:
+        assert held1 == held0 + 2 and dyn1 == dyn0 + 2, "both captured launches took the dynamic schedule"
+    else:
+        assert held1 == held0 and fb1 == fb0 + 2, "both captured launches took the static kernels"
     rng = np.random.default_rng(5)
     for _ in range(3):
         h = _objects(rng, nobj, total, L)
@@ -203,6 +212,144 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule):
         r = out.cpu().numpy().view(np.uint32).reshape(nobj, len(erase), L)
         for i, t in enumerate(erase):
             assert np.array_equal(r[:, i], (ref[:, t].astype(np.uint64) % P).astype(np.uint32)), t
+    del g
+    torch.cuda.synchronize()
+    assert _held_settles(held0), "the destroyed graph's counter sets went back to the pool"
+
+
+def _held_settles(want, tries=200):
+    """Sets held, polled until it equals `want` (a user object's destructor may
+    run on a runtime thread shortly after the graph is destroyed)."""
+    import time
+    for _ in range(tries):
+        if N.ticket_sets(0)[1] == want:
+            return True
+        time.sleep(0.01)
+    return False
+
+
+class _Graphs:
+    """Stream capture and graph execs through the HIP runtime torch loaded."""
+
+    def __init__(self):
+        h = _hip()
+        V, P_ = ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)
+        for name, args in [("hipStreamBeginCapture", [V, ctypes.c_int]), ("hipStreamEndCapture", [V, P_]),
+                           ("hipGraphInstantiate", [P_, V, V, V, ctypes.c_size_t]), ("hipGraphLaunch", [V, V]),
+                           ("hipGraphExecDestroy", [V]), ("hipGraphDestroy", [V])]:
+            getattr(h, name).argtypes = args
+        self.h = h
+
+    def capture(self, stream, fn):
+        g = ctypes.c_void_p()
+        assert self.h.hipStreamBeginCapture(ctypes.c_void_p(stream), 2) == 0  # hipStreamCaptureModeRelaxed
+        fn()
+        assert self.h.hipStreamEndCapture(ctypes.c_void_p(stream), ctypes.byref(g)) == 0
+        return g.value
+
+    def instantiate(self, graph):
+        e = ctypes.c_void_p()
+        assert self.h.hipGraphInstantiate(ctypes.byref(e), ctypes.c_void_p(graph), None, None, 0) == 0
+        return e.value
+
+    def launch(self, exec_, stream):
+        assert self.h.hipGraphLaunch(ctypes.c_void_p(exec_), ctypes.c_void_p(stream)) == 0
+
+    def destroy(self, graph=None, exec_=None):
+        if exec_ is not None:
+            assert self.h.hipGraphExecDestroy(ctypes.c_void_p(exec_)) == 0
+        if graph is not None:
+            assert self.h.hipGraphDestroy(ctypes.c_void_p(graph)) == 0
+
+
+def test_graph_held_sets_return_when_graphs_die(torch_dev, schedule):
+    """Mode 2: capture, replay and destroy 2000 single-launch graphs.  Each
+    captured launch's counter set is bound to its graph by a user object and
+    comes back when the graph dies, so the held count returns to its baseline,
+    the pool does not grow past its first slabs, and a later uncaptured launch
+    still takes the dynamic schedule (rs_apply_queue_kernel)."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(2) == 0
+    G = _Graphs()
+    need, total, nobj, L = 4, 6, 2, 4096 + 4
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    rng = np.random.default_rng(77)
+    h = _objects(rng, nobj, total, L)
+    buf = torch.from_numpy(h.view(np.int32).reshape(-1).copy()).cuda()
+    ref = _encode_ref(h, need, total)
+    s = torch.cuda.Stream()
+    plan(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)  # warm
+    torch.cuda.synchronize()
+    sets0, held0 = N.ticket_sets(0)
+    for i in range(2000):
+        buf.view(nobj, total, L)[:, need:].zero_()
+        torch.cuda.synchronize()
+        g = G.capture(s.cuda_stream, lambda: plan(buf, lay, buf, lay, L, nobj, stream=s.cuda_stream,
+                                                    dst_offset=need * L))
+        e = G.instantiate(g)
+        G.launch(e, s.cuda_stream)
+        torch.cuda.synchronize()
+        if i % 250 == 0:
+            assert np.array_equal(buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L), ref), i
+        G.destroy(graph=g, exec_=e)
+    torch.cuda.synchronize()
+    assert _held_settles(held0), (N.ticket_sets(0), held0)
+    sets1, _ = N.ticket_sets(0)
+    assert sets1 == sets0, "the sets came back: no new slabs for 2000 graphs"
+    dyn0, _ = N.schedule_counts(0)
+    buf.view(nobj, total, L)[:, need:].zero_()
+    plan(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    dyn1, _ = N.schedule_counts(0)
+    assert dyn1 == dyn0 + 1, "an uncaptured launch after the graphs still runs the dynamic schedule"
+    assert np.array_equal(buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L), ref)
+
+
+def test_graph_exec_keeps_its_set_after_the_graph_is_destroyed(torch_dev, schedule):
+    """Mode 2, the torch pattern: the graph is destroyed right after it is
+    instantiated, and the exec alone holds the captured set.  Two execs of one
+    graph replayed one after the other, with uncaptured launches on another
+    stream in between, are exact; the set is held until the last exec dies."""
+    torch = torch_dev
+    from slime_amd import device as D
+    assert schedule(2) == 0
+    G = _Graphs()
+    need, total, nobj, L = 8, 12, 5, 3 * 768 * 4 + 7
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    rng = np.random.default_rng(78)
+    buf = torch.zeros(nobj * total * L, dtype=torch.int32, device="cuda")
+    s, other = torch.cuda.Stream(), torch.cuda.Stream()
+    plan(buf, lay, buf, lay, L, nobj, stream=s, dst_offset=need * L)  # warm
+    torch.cuda.synchronize()
+    _, held0 = N.ticket_sets(0)
+    g = G.capture(s.cuda_stream, lambda: plan(buf, lay, buf, lay, L, nobj, stream=s.cuda_stream,
+                                                dst_offset=need * L))
+    e1, e2 = G.instantiate(g), G.instantiate(g)
+    G.destroy(graph=g)
+    torch.cuda.synchronize()
+    assert _held_settles(held0 + 1, tries=20), "the execs keep the captured set"
+    side = [(_objects(rng, 3, total, 999), 3, 999) for _ in range(4)]
+    for rep, ex in enumerate([e1, e2, e1, e2]):
+        h = _objects(rng, nobj, total, L)
+        buf.copy_(torch.from_numpy(h.view(np.int32).reshape(-1)))
+        sh, sn, sL = side[rep]
+        sbuf = torch.from_numpy(sh.view(np.int32).reshape(-1).copy()).cuda()
+        torch.cuda.synchronize()
+        G.launch(ex, s.cuda_stream)
+        plan(sbuf, D.layout_of(total, sL), sbuf, D.layout_of(total, sL), sL, sn, stream=other,
+             dst_offset=need * sL)  # uncaptured, concurrent: must get another set
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L), _encode_ref(h, need, total))
+        assert np.array_equal(sbuf.cpu().numpy().view(np.uint32).reshape(sn, total, sL), _encode_ref(sh, need, total))
+    G.destroy(exec_=e1)
+    torch.cuda.synchronize()
+    assert _held_settles(held0 + 1, tries=20), "one exec is still alive"
+    G.destroy(exec_=e2)
+    torch.cuda.synchronize()
+    assert _held_settles(held0), "the last exec died: the set is back"
 
 
 def test_graph_captured_byte_path_replays_exactly(torch_dev):
