@@ -1036,6 +1036,7 @@ def main():
     alloc_probe = None
     if args.allocator == "vmm" and args.alloc_probe and nobj:
         alt = torch.empty(nobj * total * SS, dtype=torch.int32, device=f"cuda:{dev}")
+        alt_probe = D.probe_placement(alt)  # fresh: the probe overwrites it
         D.fill_symbols(alt, 0x5113E + 7919 * rank)
         pe, pd = [], []
         for k in range(4):
@@ -1051,9 +1052,14 @@ def main():
                 pd.append(ev[1].elapsed_time(ev[2]))
         del alt
         pem, pdm = sorted(pe)[1], sorted(pd)[1]
+        kept = (placement or {}).get("probes") or [{}]
         alloc_probe = {"buffer": "torch.empty (hipMalloc)", "encode_ms": round(pem, 4), "decode_ms": round(pdm, 4),
                        "frac": round((enc_alg + dec_alg) / 2 / ((pem + pdm) / 2 * 1e-3) / 1e9 / 8000.0, 4),
-                       "launches": 3}
+                       "launches": 3, "probe_gbs": round(alt_probe, 1),
+                       "library_buffer_probe_gbs": kept[(placement or {}).get("chosen") or 0].get("probe_gbs"),
+                       "threshold_gbs": float(D.lib.slime_rs_placement_threshold()),
+                       "what": "slime_rs_probe_placement over the fresh hipMalloc buffer before it was filled, "
+                               "beside the probe of the library buffer that was kept"}
     sb.free()
     bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj) if args.bytes_path else None
     if want_host and args.host_order == "after-free":

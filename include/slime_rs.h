@@ -345,6 +345,21 @@ typedef struct slime_rs_alloc_info {
   uint64_t probe_chunk[4]; /* each probed placement's chunk size (0: hipMalloc) */
 } slime_rs_alloc_info_t;
 int slime_rs_device_alloc_info(const void *ptr, slime_rs_alloc_info_t *info);
+/* The same placement probe over a caller's own device range [ptr, ptr+bytes)
+ * on `device` (e.g. a hipMalloc'd or torch batch buffer): *gbs = GB/s of
+ * algorithmic traffic of the C3-shaped read/write walk, 0 when the range is
+ * too small to measure (under ~400 MB).  The physical placement of a large
+ * buffer fixes, for its whole life, whether the kernels stream in the fast
+ * mode (~6.2 TB/s at C3) or the slow one (~5.3): a buffer that probes below
+ * slime_rs_placement_threshold() is worth re-allocating, or allocating with
+ * slime_rs_device_alloc, which probes and re-places by itself.
+ * OVERWRITES the range: probe a buffer before filling it.  The range must lie
+ * inside one device allocation on `device` (else SLIME_RS_ERR_INVALID_ARG).
+ * Synchronous. */
+int slime_rs_probe_placement(void *ptr, uint64_t bytes, int device, double *gbs);
+/* The fast-mode threshold of the probe, GB/s (env SLIME_RS_PLACEMENT_MIN_GBS,
+ * default 6100: the C3 apply kernel at <= 8.45 ms). */
+double slime_rs_placement_threshold(void);
 /* Frees a buffer from slime_rs_device_alloc (its base).  Waits for the device
  * first (hipDeviceSynchronize), so work still queued on it cannot fault.
  * Returns SLIME_RS_ERR_INVALID_ARG for other pointers. */

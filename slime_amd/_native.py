@@ -80,6 +80,9 @@ SIGNATURES = [
     ("slime_rs_device_alloc", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("slime_rs_device_free", ctypes.c_int, [ctypes.c_void_p]),
     ("slime_rs_device_alloc_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AllocInfo)]),
+    ("slime_rs_probe_placement", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    ("slime_rs_placement_threshold", ctypes.c_double, []),
     ("slime_gf_max_val", ctypes.c_uint32, []),
     ("slime_gf_minverse", ctypes.c_uint32, [ctypes.c_uint32]),
     ("slime_gf_raise", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),

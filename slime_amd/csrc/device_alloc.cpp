@@ -188,7 +188,7 @@ int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
   info.kind = 0;
   info.chunk_bytes = best.chunk;
   if (probe_gib > 0 && (double)bytes >= probe_gib * (1ull << 30)) {
-    const double want = env_double("SLIME_RS_PLACEMENT_MIN_GBS", 6100.0);
+    const double want = slime_rs_placement_threshold();
     double best_gbs = placement_probe(device, (uint8_t*)va, bytes);
     info.probe_gbs[0] = best_gbs;
     info.probe_chunk[0] = best.chunk;
@@ -228,6 +228,51 @@ int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
     dev_buffers()[va] = std::move(best);
   }
   *ptr = va;
+  return 0;
+}
+
+double slime_rs_placement_threshold(void) { return env_double("SLIME_RS_PLACEMENT_MIN_GBS", 6100.0); }
+
+// The allocator's probe over a caller's range.  The range must lie inside one
+// device allocation (hipMalloc, or a slime_rs_device_alloc buffer): the probe
+// kernel writes to all of it.
+int slime_rs_probe_placement(void* ptr, uint64_t bytes, int device, double* gbs) {
+  if (!ptr || !gbs) return fail(Status::InvalidArg, "probe_placement: null ptr or output");
+  *gbs = 0;
+  if (((uintptr_t)ptr & 3u) != 0) return fail(Status::InvalidArg, "probe_placement: ptr not 4-byte aligned");
+  if (int rc = check_device(device)) return rc;
+  DeviceScope ds(device);
+  const uintptr_t p0 = (uintptr_t)ptr, p1 = p0 + bytes;
+  bool inside = false;
+  {
+    std::lock_guard<std::mutex> lock(g_vmm_mu);
+    for (const auto& kv : dev_buffers()) {
+      const uintptr_t b0 = (uintptr_t)kv.first, b1 = b0 + kv.second.bytes;
+      if (p0 >= b0 && p1 <= b1) {
+        if (kv.second.device != device) return fail(Status::InvalidArg, "probe_placement: buffer is on another device");
+        inside = true;
+        break;
+      }
+    }
+  }
+  if (!inside) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(Status::InvalidArg, "probe_placement: not a device allocation");
+    }
+    hipPointerAttribute_t attr = {};
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess || attr.type != hipMemoryTypeDevice ||
+        attr.device != device) {
+      (void)hipGetLastError();
+      return fail(Status::InvalidArg, "probe_placement: not device memory of this device");
+    }
+    if (p0 < (uintptr_t)base || p1 > (uintptr_t)base + size)
+      return fail(Status::InvalidArg, "probe_placement: range exceeds its allocation");
+  }
+  *gbs = placement_probe(device, (uint8_t*)ptr, bytes);
+  if (hipError_t e = hipDeviceSynchronize()) return fail_hip(e, "probe_placement");
   return 0;
 }
 

@@ -9,6 +9,7 @@ PyTorch here is plumbing only: memory, streams, events.
 from __future__ import annotations
 
 import ctypes
+import logging
 from typing import Optional, Sequence
 
 import numpy as np
@@ -38,6 +39,12 @@ _TYPESTR = {torch.int32: "<i4", torch.uint8: "|u1", torch.int64: "<i8", torch.ui
 
 
 _deferred_frees: list = []  # buffers dropped while a graph capture was running
+_log = logging.getLogger("slime_amd")
+# Storage bases whose placement is known: slime_rs_device_alloc buffers (probed
+# and re-placed when created) and caller buffers probed by probe_placement.
+_known_placement: set = set()
+_warned_placement: set = set()
+PLACEMENT_WARN_BYTES = 16 << 30
 
 
 def _capturing() -> bool:
@@ -69,6 +76,7 @@ class _DeviceBuffer:
         p = ctypes.c_void_p()
         N.check(lib.slime_rs_device_alloc(device, max(1, numel * itemsize), ctypes.byref(p)))
         self.ptr = p.value
+        _known_placement.add(self.ptr)
         self.__cuda_array_interface__ = {"shape": (numel,), "typestr": _TYPESTR[dtype], "data": (self.ptr, False),
                                          "strides": None, "version": 3, "stream": None}
 
@@ -78,6 +86,7 @@ class _DeviceBuffer:
                 if _capturing():
                     _deferred_frees.append(self.ptr)
                 else:
+                    _known_placement.discard(self.ptr)
                     lib.slime_rs_device_free(ctypes.c_void_p(self.ptr))  # waits for the device, then unmaps
                     release_deferred()
             except Exception:  # pragma: no cover - interpreter shutdown
@@ -103,6 +112,41 @@ def placement(t: torch.Tensor) -> dict:
     """How device_empty placed t's buffer (slime_rs_device_alloc_info): the
     placements probed, their probe rates and the one kept."""
     return N.alloc_info(t.data_ptr())
+
+
+def probe_placement(t: torch.Tensor) -> float:
+    """The library's placement probe over a caller's FRESH buffer t (it
+    overwrites t): GB/s of the C3-shaped read/write walk over its storage, 0
+    if too small to measure (slime_rs_probe_placement).  Logs a warning when
+    the rate is below the fast-mode threshold: such a buffer runs the kernels
+    about 10% slower for its whole life -- re-allocate it, or use
+    device_empty(), which probes and re-places by itself."""
+    dev = _dev_index(t)
+    base = t.untyped_storage().data_ptr()
+    nbytes = t.untyped_storage().nbytes()
+    gbs = ctypes.c_double()
+    N.check(lib.slime_rs_probe_placement(ctypes.c_void_p(base), nbytes, dev, ctypes.byref(gbs)))
+    _known_placement.add(base)
+    want = float(lib.slime_rs_placement_threshold())
+    if 0 < gbs.value < want:
+        _log.warning("slime_amd: buffer at 0x%x (%.1f GiB) probes %.0f GB/s, below the fast placement's %.0f: "
+                     "the kernels will stream ~10%% slower on it; allocate batches with "
+                     "slime_amd.device.device_empty (slime_rs_device_alloc)", base, nbytes / 2**30, gbs.value, want)
+    return gbs.value
+
+
+def _note_unprobed(t: torch.Tensor) -> None:
+    """Once per storage: a >= 16 GiB caller buffer whose placement nobody probed
+    (not from device_empty, never passed to probe_placement)."""
+    st = t.untyped_storage()
+    base = st.data_ptr()
+    if st.nbytes() < PLACEMENT_WARN_BYTES or base in _known_placement or base in _warned_placement:
+        return
+    _warned_placement.add(base)
+    _log.warning("slime_amd: %.1f GiB batch buffer at 0x%x has an unprobed physical placement; about 40%% of large "
+                 "hipMalloc buffers land in the slow mode (~10%% slower kernels for the buffer's life).  Allocate "
+                 "with slime_amd.device.device_empty, or call probe_placement() on the fresh buffer "
+                 "(DESIGN.md §4)", st.nbytes() / 2**30, base)
 
 
 def layout_of(nshards: int, L: int, shard_stride: Optional[int] = None) -> N.Layout:
@@ -175,6 +219,9 @@ class Plan:
         self._check_extent(src, src_offset, src_layout, L, nobj, self.in_max)
         self._check_extent(dst, dst_offset, dst_layout, L, nobj,
                            self.rows - 1 if self.out_max is None else self.out_max)
+        _note_unprobed(src)
+        if dst.data_ptr() != src.data_ptr():
+            _note_unprobed(dst)
         N.check(lib.slime_rs_plan_execute(self._h, ctypes.c_void_p(src.data_ptr() + 4 * src_offset), src_layout,
                                           ctypes.c_void_p(dst.data_ptr() + 4 * dst_offset), dst_layout, L, nobj,
                                           _stream_handle(self.device, stream)))

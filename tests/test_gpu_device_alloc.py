@@ -145,3 +145,64 @@ def test_placement_probe_skips_small_buffers_and_fast_ones(torch_dev, monkeypatc
     big = D.device_empty(4 << 30, torch.int32)
     info = D.placement(big)
     assert len(info["probes"]) == 1 and info["retries"] == 0 and info["chosen"] == 0
+
+
+def test_probe_placement_of_caller_buffers(torch_dev, caplog):
+    """slime_rs_probe_placement over a caller's fresh buffer: the library's
+    buffer (probed and re-placed when created) ranks at least as fast as a
+    torch.empty (hipMalloc) buffer of the same size, within noise; a slow
+    caller buffer is logged; ranges outside an allocation are refused."""
+    import logging
+    torch = torch_dev
+    from slime_amd import device as D
+    n = (20 << 30) // 4
+    lib_buf = D.device_empty(n, torch.int32, 0)
+    lib_gbs = D.probe_placement(lib_buf)
+    del lib_buf
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    with caplog.at_level(logging.WARNING, logger="slime_amd"):
+        t_gbs = D.probe_placement(t)
+    want = float(N.lib.slime_rs_placement_threshold())
+    assert lib_gbs > 0 and t_gbs > 0
+    assert lib_gbs >= 0.97 * t_gbs, (lib_gbs, t_gbs)
+    assert (t_gbs < want) == any("probes" in r.getMessage() for r in caplog.records), (t_gbs, want)
+    gbs = ctypes.c_double()
+    # past the end of the allocation: refused before any launch
+    rc = N.lib.slime_rs_probe_placement(ctypes.c_void_p(t.data_ptr()), t.numel() * 4 + (64 << 20), 0,
+                                        ctypes.byref(gbs))
+    assert rc == N.ERR_INVALID_ARG and gbs.value == 0
+    host = np.zeros(1 << 20, dtype=np.uint8)
+    assert N.lib.slime_rs_probe_placement(ctypes.c_void_p(host.ctypes.data), host.size, 0,
+                                          ctypes.byref(gbs)) == N.ERR_INVALID_ARG
+    # a small range: nothing to measure, no launch
+    small = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
+    assert D.probe_placement(small) == 0.0
+    del t
+    torch.cuda.empty_cache()
+
+
+def test_plan_warns_once_about_an_unprobed_large_buffer(torch_dev, caplog):
+    """A >= 16 GiB caller buffer handed to a plan without a placement probe is
+    logged once (its placement decides the kernels' speed); device_empty
+    buffers are not."""
+    import logging
+    torch = torch_dev
+    from slime_amd import device as D
+    need, total, nobj = 8, 12, 16
+    L = (17 << 30) // 4 // (nobj * total)
+    plan = D.Plan.encode(need, total)
+    lay = D.layout_of(total, L)
+    with caplog.at_level(logging.WARNING, logger="slime_amd"):
+        t = torch.zeros(nobj * total * L, dtype=torch.int32, device="cuda")
+        plan(t, lay, t, lay, L, nobj, dst_offset=need * L)
+        plan(t, lay, t, lay, L, nobj, dst_offset=need * L)
+        torch.cuda.synchronize()
+        warned = [r for r in caplog.records if "unprobed" in r.getMessage()]
+        assert len(warned) == 1
+        del t
+        torch.cuda.empty_cache()
+        b = D.device_empty(nobj * total * L, torch.int32, 0)
+        plan(b, lay, b, lay, L, nobj, dst_offset=need * L)
+        torch.cuda.synchronize()
+        assert len([r for r in caplog.records if "unprobed" in r.getMessage()]) == 1
+        del b
