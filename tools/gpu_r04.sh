@@ -26,6 +26,7 @@ run() {  # run <name> <limit-seconds> <command...>
 nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
 for step in "$@"; do
   case "$step" in
+    tests_alloc) run pytest_alloc 400 python -u -m pytest tests/test_gpu_device_alloc.py -x -q --timeout 200 --timeout-method thread ;;
     tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct" ;;
     kfd) run kfd 120 python -c "import sys; sys.argv=['bench.py']; sys.path.insert(0, '.'); import bench, torch; print('kfd_gpus', bench.kfd_gpus(), 'torch', torch.cuda.device_count())" ;;
     rehearse2) SLIME_BENCH_SHARE_GPU=1 run rehearse2 400 python bench.py --gpus 2 --steps 5 --warmup 1 $NOLEGS --bytes-path 0 --ceilings 0 ;;
