@@ -31,7 +31,11 @@ using apply::MfmaIO;
 // MapToGF's flags over every loaded data word (encode, speculative pass) in
 // two registers: the unsigned maximum of the words (bit0: >= p) and their
 // signed maximum (the unsigned maximum of word ^ 1<<31; bit1: >= p) --
-// a byte swap and two max per word.
+// a byte swap (v_perm_b32) and two max per word, as one asm chain per word.
+// Written in C, the compiler batched the byte swaps of a K step ahead of its
+// MFMAs and the refill form spilled 56 VGPRs at four K steps (64/80); the
+// chain keeps one temporary live, and the refill form fits two waves per
+// SIMD at every K step count (247 VGPRs at four, -Rpass-analysis).
 struct FlagPre {
   uint32_t umax = 0;
   int32_t smax = INT32_MIN;
@@ -40,9 +44,14 @@ struct FlagPre {
     constexpr int W = sizeof(V) / sizeof(uint32_t);
 #pragma unroll
     for (int c = 0; c < W; ++c) {
-      const uint32_t w = be(v[c]);
-      umax = umax > w ? umax : w;
-      smax = smax > (int32_t)w ? smax : (int32_t)w;
+      uint32_t t;
+      const uint32_t w = v[c];
+      asm volatile(
+          "v_perm_b32 %0, %3, %3, %4\n\t"
+          "v_max_u32 %1, %1, %0\n\t"
+          "v_max_i32 %2, %2, %0"
+          : "=&v"(t), "+v"(umax), "+v"(smax)
+          : "v"(w), "s"(0x00010203u));
     }
   }
   __device__ __forceinline__ uint32_t bits() const {
@@ -297,27 +306,33 @@ hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The refill form (2) is the product for the decode and the re-encode.  The
-// speculative encode cannot take it at two waves per SIMD: with the MapToGF
-// flags it needs more than 256 VGPRs at four K steps and spills.  Up to four K
-// steps it runs the refill form at one wave per SIMD (3), above them the
-// no-prefetch form (0) -- measured per shape (profiles/r03/s35_mfma_bytes/,
-// s36_mfma_geo/): 40/56 2.998 -> 2.890 ms and 64/80 2.718 -> 2.603 for both
-// passes with form 3, 80/100 3.529 -> 3.565.  Env SLIME_RS_MFMA_ENC_FORM=0|3
-// forces one; SLIME_RS_MFMA_MODE=0/1 forces a form elsewhere (A/B only).
+// The refill form (2) is the product for the decode, the re-encode and the
+// speculative encode.  Round 3's speculative encode could not take it at two
+// waves per SIMD (MapToGF's flags, written in C, spilled at four K steps) and
+// ran form 3 (refill at one wave per SIMD) up to four K steps, form 0 above
+// (profiles/r03/s35_mfma_bytes/, s36_mfma_geo/); the flags' asm chain
+// (FlagPre) removed the spill.  Env SLIME_RS_MFMA_ENC_FORM=0|2|3 forces one
+// form for the speculative pass (A/B); SLIME_RS_MFMA_MODE=0/1 forces a form
+// elsewhere.
 template <int KS>
 int enc_form0() {
   static const int f = [] {
     const char* e = getenv("SLIME_RS_MFMA_ENC_FORM");
     if (e && e[0] == '3') return 3;
     if (e && e[0] == '0') return 0;
-    return KS <= 4 ? 3 : 0;
+    return 2;
   }();
   return f;
 }
 template <int KS>
 hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
-  if (a.phase == 0) return enc_form0<KS>() == 3 ? enc_form<KS, 3>(a, s) : enc_form<KS, 0>(a, s);
+  if (a.phase == 0) {
+    switch (enc_form0<KS>()) {
+      case 0: return enc_form<KS, 0>(a, s);
+      case 3: return enc_form<KS, 3>(a, s);
+      default: return enc_form<KS, 2>(a, s);
+    }
+  }
   switch (mfma_kernel_form()) {
     case 0: return enc_form<KS, 0>(a, s);
     case 1: return enc_form<KS, 1>(a, s);

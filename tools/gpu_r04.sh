@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0"
+NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0"
 
 run() {  # run <name> <limit-seconds> <command...>
   local name=$1 lim=$2; shift 2
@@ -29,7 +29,6 @@ for step in "$@"; do
     tests_alloc) run pytest_alloc 400 python -u -m pytest tests/test_gpu_device_alloc.py -x -q --timeout 200 --timeout-method thread ;;
     tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct" ;;
     kfd) run kfd 120 python -c "import sys; sys.argv=['bench.py']; sys.path.insert(0, '.'); import bench, torch; print('kfd_gpus', bench.kfd_gpus(), 'torch', torch.cuda.device_count())" ;;
-    rehearse2) SLIME_BENCH_SHARE_GPU=1 run rehearse2 400 python bench.py --gpus 2 --steps 5 --warmup 1 $NOLEGS --bytes-path 0 --ceilings 0 ;;
     tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     tests_sched) run pytest_sched 400 python -u -m pytest tests/test_gpu_schedule.py -x -v --timeout 120 --timeout-method thread ;;
     tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
@@ -55,6 +54,7 @@ for step in "$@"; do
             --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
           run bpmc_c5_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/bpmc_c5_write" -o pmc \
             --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
+    tests_mfma_bytes) run pytest_mfma_bytes 400 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 200 --timeout-method thread -k "byte or bytes or encode_objects or decode_objects" ;;
     mfma_tests) run pytest_mfma 600 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 300 --timeout-method thread ;;
     # wide codes: matrix-core kernel (default), its non-pipelined form, the VALU kernels
     # wide codes: matrix-core kernel forms (SLIME_RS_MFMA_MODE 2 = K-step refill, default; 1 two tile
@@ -73,7 +73,7 @@ for step in "$@"; do
           WB="--steps 3 --warmup 1 $NOLEGS"
           for shp in "64 80 $E16" "80 100 $E16,16,17,18,19" "40 56 $E16"; do
             set -- $shp
-            for v in "mfma:SLIME_RS_MFMA=1" "mfma_enc3:SLIME_RS_MFMA_ENC_FORM=3" "valu:SLIME_RS_MFMA=0"; do
+            for v in "mfma:SLIME_RS_MFMA=1" "enc0:SLIME_RS_MFMA_ENC_FORM=0" "enc3:SLIME_RS_MFMA_ENC_FORM=3"; do
               run wbytes_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
             done
           done ;;
@@ -163,7 +163,7 @@ for step in "$@"; do
     hosttrace) run hosttrace 300 python tools/host_trace.py &&
                run hosttrace_2d 300 env SLIME_RS_DMA_2D=1 python tools/host_trace.py &&
                run hosttrace_b 300 python tools/host_trace.py ;;
-    rehearse2) run rehearse2 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 &&
+    rehearse2) run rehearse2 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --bytes-path 0 &&
                run rehearse2_c5 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --preset c5 --global-objects 8 --steps 3 --warmup 1 &&
                run rehearse2_torchrun 400 env SLIME_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 ;;
     placeforce) run placeforce 300 env SLIME_RS_PLACEMENT_MIN_GBS=99999 python bench.py --cpu-baseline 0 --host-path 0 --bytes-path 0 --steps 20 &&
