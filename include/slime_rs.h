@@ -427,8 +427,10 @@ int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
  * schedule"). */
 int slime_rs_ticket_sets(int device, uint64_t *sets, uint64_t *held);
 /* Launches on `device` since start that ran the dynamic schedule on a counter
- * set, and that were sent to the static kernels instead (inside a capture
- * under mode 1, or no set to be had) -- diagnostics and tests. */
+ * set, and that asked for one and were sent to the static kernels instead
+ * (no set to be had) -- diagnostics and tests.  Launches the mode itself
+ * keeps on the static kernels (mode 0, captures under mode 1) count in
+ * neither. */
 int slime_rs_schedule_counts(int device, uint64_t *dynamic, uint64_t *fallback);
 
 /* ==== chunk and object digests ======================

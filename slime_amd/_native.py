@@ -312,7 +312,7 @@ def ticket_sets(device: int) -> tuple[int, int]:
 
 
 def schedule_counts(device: int) -> tuple[int, int]:
-    """(launches that ran the dynamic schedule on a counter set, launches sent to the static kernels)."""
+    """(launches that ran the dynamic schedule on a counter set, launches that asked for one and got none)."""
     d, f = ctypes.c_uint64(), ctypes.c_uint64()
     check(lib.slime_rs_schedule_counts(device, ctypes.byref(d), ctypes.byref(f)))
     return int(d.value), int(f.value)

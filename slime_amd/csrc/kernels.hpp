@@ -103,8 +103,8 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
 hipError_t warm_ticket_pool(int device);
 // Sets allocated / held by launches in flight or graphs, for `device` (tests).
 void ticket_pool_stats(int device, uint64_t* sets, uint64_t* held);
-// Launches on `device` that took a counter set (dynamic) / were sent to the
-// static kernel by with_tickets (capture under mode 1, or no set to be had).
+// Launches on `device` that took a counter set (dynamic) / asked with_tickets
+// for one and were sent to the static kernel (no set to be had).
 void schedule_counts(int device, uint64_t* dynamic, uint64_t* fallback);
 
 // Column segments per object for a launch over nobj objects of ncols

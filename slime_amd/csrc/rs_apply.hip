@@ -410,10 +410,7 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
   std::lock_guard<std::mutex> lock(tp.mu);
   TicketSet set;
   hipError_t e;
-  if (cap && queue_mode() != 2) {  // the static kernel inside captures (see above)
-    ++tp.fallback;
-    return hipSuccess;
-  }
+  if (cap && queue_mode() != 2) return hipSuccess;  // the static kernel inside captures (see above)
   if (!tp.take(stream, cap, &set, &e)) {  // hipSuccess + !launched: static kernel
     if (e == hipSuccess) ++tp.fallback;
     return e;

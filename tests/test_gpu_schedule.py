@@ -198,7 +198,7 @@ def test_graph_captured_launches_replay_exactly(torch_dev, schedule, mode):
     if mode == 2:
         assert held1 == held0 + 2 and dyn1 == dyn0 + 2, "both captured launches took the dynamic schedule"
     else:
-        assert held1 == held0 and fb1 == fb0 + 2, "both captured launches took the static kernels"
+        assert held1 == held0 and dyn1 == dyn0, "both captured launches took the static kernels"
     rng = np.random.default_rng(5)
     for _ in range(3):
         h = _objects(rng, nobj, total, L)
