@@ -147,6 +147,7 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
 struct SwitchRecord {
   bool switched = false;
   uint32_t spread = 0, nint = 0, units = 0;
+  uint32_t nseg = 0;  // matrix-core form: the column segments per object phase 0 ran with
 };
 struct BytesLaunch {
   uint8_t* slots;
@@ -182,6 +183,7 @@ hipError_t launch_encode_bytes(const BytesLaunch& a, hipStream_t stream);
 // phase 0 would not run the switching (dynamic-schedule) kernel.
 uint64_t encode_switch_bytes(const BytesLaunch& a, hipStream_t stream);
 uint64_t encode_switch_bytes_k32(const BytesLaunch& a, hipStream_t stream);
+uint64_t encode_switch_bytes_mfma(const BytesLaunch& a);
 // 17 <= need <= 32 through the pipelined k-template byte kernels (rs_bytes_k32.hip).
 hipError_t launch_encode_bytes_k32(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_decode_bytes_k32(const BytesLaunch& a, hipStream_t stream);

@@ -289,7 +289,9 @@ uint64_t encode_switch_bytes(const BytesLaunch& a, hipStream_t s) {
     case 14: return enc_switch_bytes<14>(a, s);
     case 15: return enc_switch_bytes<15>(a, s);
     case 16: return enc_switch_bytes<16>(a, s);
-    default: return a.k <= 32 && pipe_ok(a) && k32_kernels() ? encode_switch_bytes_k32(a, s) : 0;
+    default:
+      if (bytes_mfma_eligible(a, true)) return encode_switch_bytes_mfma(a);
+      return a.k <= 32 && pipe_ok(a) && k32_kernels() ? encode_switch_bytes_k32(a, s) : 0;
   }
 }
 

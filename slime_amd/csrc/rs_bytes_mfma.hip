@@ -18,9 +18,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 #include "rs_apply_mfma_kernel.hpp"
 #include "rs_bytes_kernel.hpp"
+#include "rs_bytes_launch.hpp"
 
 namespace slime {
 namespace bytes {
@@ -59,6 +62,57 @@ struct FlagPre {
   }
 };
 
+// Mid-object mapping switch on the matrix cores (phase 0 with a scratch
+// record): the refill walk of one segment's interior tiles [c0, c1) of object
+// obj, but each tile takes its mapping from flags[obj] as phase 0 found it so
+// far -- 1<<31 once some word >= p has been seen (map.go:35-62) -- and lane 0
+// records it (rec[t], one byte per tile, 2 = "no interior tile" before the
+// pass).  The flags word for tile t+1 is loaded while tile t computes; the
+// wave's own flag bits are published after every tile.  Phase 1 then redoes
+// only the tiles an object mapped with 1<<31 encoded with 0 (the tiles before
+// its first word >= p), not the whole object.  A stale flags read only delays
+// the switch: the record says what each tile wrote.
+__device__ __forceinline__ uint32_t flags_now(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int KS, int W>
+__device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, char* __restrict__ ob,
+                                                 const uint32_t (&soff)[KS][4], const i32x4* __restrict__ lfrag,
+                                                 const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
+                                                 uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
+                                                 uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves,
+                                                 uint32_t* __restrict__ fobj, uint8_t* __restrict__ rec, FlagPre& pre,
+                                                 uint32_t& sent) {
+  constexpr uint32_t TC = 16 * W;
+  const uint32_t ntiles = (c1 - c0) / TC;  // interior: whole tiles only
+  auto colb_of = [&](uint32_t t) { return (c0 + t * TC + n * W) << 2; };
+  uint32_t t = wave;
+  if (t >= ntiles) return;
+  apply::vec_t<W> x[KS][4];
+  apply::mfma_load_tile<KS, W, true>(x, ib, soff, colb_of(t));
+  uint32_t f = flags_now(fobj);
+  while (t < ntiles) {
+    const uint32_t tn = t + nwaves;
+    const uint32_t m = (__builtin_amdgcn_readfirstlane(f) & 1u) ? 0x80000000u : 0u;
+    if (lane == 0) rec[t] = m ? 1 : 0;
+    if (tn < ntiles) f = flags_now(fobj);  // tile tn's mapping, in flight during tile t
+    const MfmaIO io{0x80808080u ^ be(m), m};
+    if (tn < ntiles)
+      apply::mfma_tile<KS, W, true, true, true, true>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane,
+                                                      g, ob, colb_of(t), true, io, pre);
+    else
+      apply::mfma_tile<KS, W, true, true, false, true>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob,
+                                                       colb_of(t), true, io, pre);
+    const uint32_t fb = pre.bits();
+    const uint32_t wf = (__ballot(fb & 1u) ? 1u : 0u) | (__ballot(fb & 2u) ? 2u : 0u);
+    if (wf & ~sent) {
+      if (lane == 0) atomicOr(fobj, wf);
+      sent |= wf;
+    }
+    t = tn;
+  }
+}
+
 // The edge steps of one segment (vectors [e0, u1)), out of line: inlined,
 // their registers would crowd the matrix-core walk's (two waves per SIMD).
 template <bool F>
@@ -84,7 +138,8 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                          uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
                          const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
                          const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
-                         const uint32_t* __restrict__ mapping, uint32_t nseg) {
+                         const uint32_t* __restrict__ mapping, uint32_t nseg, uint8_t* __restrict__ record,
+                         uint32_t units) {
   constexpr int W = apply::mfma_width(KS);
   constexpr uint32_t TCV = 4 * W;  // tile width in 16-byte vectors
   constexpr bool F = MODE == 0;
@@ -198,10 +253,21 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     if (nint) {
       if constexpr (F) {
         FlagPre pre;
-        apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
-                                                        reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT, rows,
-                                                        lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io,
-                                                        pre);
+        bool walked = false;
+        if constexpr (FORM == 2) {
+          if (record) {  // the mid-object switch (mfma_switch_walk)
+            uint32_t sent = 0;
+            mfma_switch_walk<KS, W>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), soff, lds,
+                                    lrowc, loff, MT, rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves,
+                                    flags + obj, record + (uint64_t)obj * units + v0 / TCV, pre, sent);
+            walked = true;
+          }
+        }
+        if (!walked)
+          apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
+                                                          reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT,
+                                                          rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave,
+                                                          nwaves, io, pre);
         fbits = pre.bits();
       } else {
         apply::NoPre pre;
@@ -221,6 +287,113 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
       const uint32_t wf = (a1 ? 1u : 0u) | (a2 ? 2u : 0u);
       if (wf && lane == 0) atomicOr(&flags[obj], wf);
     }
+  }
+}
+
+// The redo list of a switched matrix-core phase 0: every interior tile of an
+// object whose mapping came out 1<<31 (status 0) that phase 0 encoded with
+// mapping 0 (record 0; 1 = encoded with 1<<31, 2 = not an interior tile), as
+// entries obj * units + tile; *count (zero on entry) receives their number.
+__global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* __restrict__ record,
+                                                                const uint32_t* __restrict__ mapping,
+                                                                const uint32_t* __restrict__ status, uint32_t nobj,
+                                                                uint32_t units, uint32_t* __restrict__ list,
+                                                                uint32_t* __restrict__ count) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t total = (uint64_t)nobj * units;
+  for (uint64_t base = wave * 64; base < total; base += nwaves * 64) {
+    const uint64_t e = base + lane;
+    bool need = false;
+    if (e < total) {
+      const uint32_t o = (uint32_t)(e / units);
+      need = mapping[o] != 0 && status[o] == 0 && record[e] == 0;
+    }
+    const uint64_t mask = __ballot(need);
+    if (!mask) continue;
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
+    at = __builtin_amdgcn_readfirstlane(at);
+    if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
+  }
+}
+
+// Phase 1 after a switched matrix-core phase 0: the listed interior tiles
+// re-encoded with their object's mapping (one refill walk over the list, the
+// next entry's data streaming in behind the current one's math, across
+// objects), then every edge range of the objects mapped with 1<<31, segment
+// by segment as phase 0 cut them (phase 0 writes edges with mapping 0).
+template <int KS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, 2)))) void
+encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk,
+                              uint64_t col0, uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
+                              const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
+                              const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ status,
+                              const uint32_t* __restrict__ mapping, uint32_t nseg, const uint32_t* __restrict__ list,
+                              const uint32_t* __restrict__ count, uint32_t units) {
+  constexpr int W = apply::mfma_width(KS);
+  constexpr uint32_t TCV = 4 * W;
+  extern __shared__ i32x4 lds[];
+  const uint32_t MT = (rows + 3) / 4;
+  const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
+  uint64_t* lrowc;
+  uint32_t* loff;
+  uint32_t soff[KS][4];
+  apply::mfma_prologue<KS>(lds, table, nullptr, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  const uint32_t cs = apply::wide_coeff_stride(k);
+  const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
+  const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint64_t nvec = ncols >> 2;
+  auto slot_of = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
+  auto colb_of = [&](uint32_t e) { return ((e % units) * (16 * W) + ln * W) << 2; };
+  const uint32_t n = *count;
+  apply::NoPre pre;
+  uint32_t t = wave;
+  if (t < n) {
+    apply::vec_t<W> x[KS][4];
+    uint32_t e = list[t];
+    apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(e / units)), soff, colb_of(e));
+    uint32_t mo = mapping[e / units];
+    while (t < n) {
+      const uint32_t tn = t + nwaves;
+      const uint32_t en = tn < n ? list[tn] : e;
+      const uint32_t mn = tn < n ? mapping[en / units] : mo;
+      const uint32_t o = e / units;
+      const uint32_t m = __builtin_amdgcn_readfirstlane(mo);
+      const MfmaIO io{0x80808080u ^ be(m), m};
+      char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
+      if (tn < n)
+        apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(en / units)), soff,
+                                                        colb_of(en), lds, lrowc, loff, MT, rows, lane, lg, ob,
+                                                        colb_of(e), true, io, pre);
+      else
+        apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg, ob,
+                                                         colb_of(e), true, io, pre);
+      t = tn;
+      e = en;
+      mo = mn;
+    }
+  }
+  // Edge ranges of the switched objects, per phase-0 segment; object i's
+  // ranges start on waves offset by i * nwaves / nobj so they run side by side.
+  for (uint64_t wi = 0; wi < (uint64_t)nobj * nseg; ++wi) {
+    const Segment sg = segment_of(wi, nseg, nvec);
+    const uint32_t m = mapping[sg.obj];
+    if (m == 0 || status[sg.obj] != 0) continue;  // uniform
+    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
+    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
+    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    if (end_max > sg.v1) end_max = sg.v1;
+    const uint32_t nint = end_max > sg.v0 ? (uint32_t)((end_max - sg.v0) / TCV) : 0u;
+    const uint64_t e0 = sg.v0 + (uint64_t)nint * TCV;
+    if (e0 >= u1) continue;
+    uint8_t* const slot = slot_of(sg.obj);
+    const uint32_t wrel = (wave + nwaves - (uint32_t)(wi * nwaves / ((uint64_t)nobj * nseg))) % nwaves;
+    (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word, m, rows, k, cs,
+                              coeff, out_idx, e0, nvec, u1, sg.v1, lane, wrel, nwaves);
   }
 }
 
@@ -274,6 +447,14 @@ namespace {
 
 using apply::kBlock;
 
+// Interior tiles per object the switch record covers (one byte each).
+template <int KS>
+uint32_t switch_units(const BytesLaunch& a) {
+  constexpr uint64_t TCV = 4 * apply::mfma_width(KS);
+  const uint64_t nvec = (a.ncols ? a.ncols : a.L) >> 2;
+  return (uint32_t)((nvec + TCV - 1) / TCV);
+}
+
 template <int KS, int FORM>
 hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
@@ -281,15 +462,49 @@ hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
   const uint64_t blocks = 256ull * apply::mfma_waves(KS, FORM);
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
+    // The mid-object switch runs on the refill form when the caller handed
+    // scratch for its record (never inside a graph capture).
+    uint8_t* record = nullptr;
+    uint32_t units = 0;
+    if (FORM == 2 && a.scratch && a.sw) {
+      units = switch_units<KS>(a);
+      bytes::SwitchLayout l;
+      l.units = units;
+      record = l.record(a.scratch, a.nobj);
+      if (hipError_t e = hipMemsetAsync(record, 2, (uint64_t)a.nobj * units, s)) return e;
+    }
     hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0, FORM>),
                        bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
                        a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma, a.coeff,
-                       a.out_idx, a.flags, a.mapping, nseg);
-  } else {
-    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1, FORM>), bytes_grid(ncols, 1, 1, blocks, 1),
-                       dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj,
-                       a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, 1u);
+                       a.out_idx, a.flags, a.mapping, nseg, record, units);
+    if (hipError_t e = hipGetLastError()) return e;
+    if (record) {
+      a.sw->switched = true;
+      a.sw->units = units;
+      a.sw->nseg = nseg;
+    }
+    return hipSuccess;
   }
+  if (FORM == 2 && a.scratch && a.sw && a.sw->switched && a.sw->units) {
+    // Phase 1 after the switch: the list of tiles to redo, then the redo.
+    bytes::SwitchLayout l;
+    l.units = a.sw->units;
+    uint32_t* count = l.count(a.scratch);
+    if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
+    const uint64_t total = (uint64_t)a.nobj * l.units;
+    const uint64_t lblocks = std::min<uint64_t>(1024, (total + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(bytes::mfma_redo_list_kernel, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(kBlock), 0, s,
+                       l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.list(a.scratch), count);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_redo_kernel<KS>), dim3((uint32_t)(256ull * apply::mfma_waves(KS, 2))),
+                       dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S,
+                       a.nobj, a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, a.sw->nseg,
+                       l.list(a.scratch), count, l.units);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1, FORM>), bytes_grid(ncols, 1, 1, blocks, 1),
+                     dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj,
+                     a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u);
   return hipGetLastError();
 }
 
@@ -333,6 +548,7 @@ hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
       default: return enc_form<KS, 2>(a, s);
     }
   }
+  if (a.scratch && a.sw && a.sw->switched) return enc_form<KS, 2>(a, s);  // the switch's redo
   switch (mfma_kernel_form()) {
     case 0: return enc_form<KS, 0>(a, s);
     case 1: return enc_form<KS, 1>(a, s);
@@ -349,6 +565,24 @@ hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
 }
 
 }  // namespace
+
+// Scratch of the matrix-core mid-object switch (bytes::SwitchLayout: count,
+// redo list, one record byte per interior tile), or 0 when phase 0 will not
+// run the switching walk (another speculative form forced).
+uint64_t encode_switch_bytes_mfma(const BytesLaunch& a) {
+  if (a.phase != 0 || a.nobj == 0) return 0;
+  uint32_t units = 0;
+  switch (mfma::ksteps(a.k)) {
+    case 2: units = enc_form0<2>() == 2 ? switch_units<2>(a) : 0; break;
+    case 3: units = enc_form0<3>() == 2 ? switch_units<3>(a) : 0; break;
+    case 4: units = enc_form0<4>() == 2 ? switch_units<4>(a) : 0; break;
+    case 5: units = enc_form0<5>() == 2 ? switch_units<5>(a) : 0; break;
+    case 6: units = enc_form0<6>() == 2 ? switch_units<6>(a) : 0; break;
+    case 7: units = enc_form0<7>() == 2 ? switch_units<7>(a) : 0; break;
+    default: return 0;
+  }
+  return units ? 256 + 5ull * a.nobj * units : 0;
+}
 
 bool bytes_mfma_eligible(const BytesLaunch& a, bool encode) {
   if (!a.mfma || !matrix_core_mode() || a.k < 17 || !mfma_wanted(a.k, a.rows) || !mfma::supported(a.rows, a.k))

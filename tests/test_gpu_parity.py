@@ -602,11 +602,17 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total
 
 @pytest.mark.parametrize("need,total,S,nobj", [(8, 12, 16 << 20, 12), (10, 14, (8 << 20) + 5, 12),
                                                (4, 6, (6 << 20) + 3, 18), (20, 24, (4 << 20) + 1, 6),
-                                               (3, 5, 1 << 20, 36), (16, 20, (5 << 20) + 2, 6)])
+                                               (3, 5, 1 << 20, 36), (16, 20, (5 << 20) + 2, 6),
+                                               # the matrix-core encode's switch (rs_bytes_mfma.hip): 2..5 K
+                                               # steps, four- and two-column lane tiles, many segments
+                                               (25, 32, (3 << 20) + 1, 8), (40, 48, (4 << 20) + 2, 8),
+                                               (64, 80, (8 << 20) + 3, 8), (80, 100, (6 << 20) + 1, 8),
+                                               (33, 40, (2 << 20) + 7, 16)])
 def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
-    """The dynamic-schedule encode switches an object to 1<<31 as soon as a
-    word >= p has been seen and the second pass redoes only the units encoded
-    before that (rs_bytes_kernel.hpp).  Objects with that word at the start,
+    """The dynamic-schedule encode (and the matrix-core encode of wide codes)
+    switches an object to 1<<31 as soon as a word >= p has been seen and the
+    second pass redoes only the units (tiles) encoded before that
+    (rs_bytes_kernel.hpp, rs_bytes_mfma.hip).  Objects with that word at the start,
     a quarter, half, 90 % and the last whole word, two such words, none, and
     one that needs the random fallback (a word >= p after a word 1<<31 cannot
     map); every chunk byte against the reference framing (map.go:15-67,

@@ -35,6 +35,9 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    profdrv) run profdrv 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 &&
+          run prof_summary 120 sh -c "python3 tools/prof_summary.py \$(dirname \$(find $OUT/prof -name bench_kernel_trace.csv | head -1)) > $OUT/prof_summary.json" ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
             python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
     pmc_fetch) run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc \
@@ -54,6 +57,7 @@ for step in "$@"; do
             --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
           run bpmc_c5_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/bpmc_c5_write" -o pmc \
             --output-format csv -- python3 bench.py --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
+    tests_switch) run pytest_switch 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "mid_object_switch or encode_objects or write_chunks" ;;
     tests_mfma_bytes) run pytest_mfma_bytes 400 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 200 --timeout-method thread -k "byte or bytes or encode_objects or decode_objects" ;;
     mfma_tests) run pytest_mfma 600 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 300 --timeout-method thread ;;
     # wide codes: matrix-core kernel (default), its non-pipelined form, the VALU kernels
@@ -73,7 +77,7 @@ for step in "$@"; do
           WB="--steps 3 --warmup 1 $NOLEGS"
           for shp in "64 80 $E16" "80 100 $E16,16,17,18,19" "40 56 $E16"; do
             set -- $shp
-            for v in "mfma:SLIME_RS_MFMA=1" "enc0:SLIME_RS_MFMA_ENC_FORM=0" "enc3:SLIME_RS_MFMA_ENC_FORM=3"; do
+            for v in "mfma:SLIME_RS_MFMA=1" "enc0:SLIME_RS_MFMA_ENC_FORM=0"; do
               run wbytes_$1_$2_${v%%:*} 300 env ${v#*:} python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
             done
           done ;;
