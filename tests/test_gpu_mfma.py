@@ -230,6 +230,17 @@ def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, tota
     status = torch.empty(3, dtype=torch.int32, device="cuda")
     D.encode_objects(plan, slots, stride, S, 3, mapping, status, **cs)
     torch.cuda.synchronize()
+    # The chunks the repair must restore are pinned to the oracle's framing
+    # (map.go:15-113, multi_store.go:526-557) first, so every repaired byte is
+    # checked against the oracle, not only against the kernel's own encode.
+    from test_gpu_parity import _oracle_chunks
+    h = slots.cpu().numpy()
+    ms = mapping.cpu().numpy().view(np.uint32)
+    for o, obj in enumerate(objs):
+        m, want = _oracle_chunks(obj, need, total)
+        assert ms[o] == m, o
+        for c in range(total):
+            assert h[o * stride + c * chunk: o * stride + c * chunk + 4 * L].tobytes() == want[c], (o, c)
     truth = slots.clone()
     r = total - need
     for erase in (list(range(min(r, 16))), sorted(rng.choice(total, size=min(r, 20), replace=False).tolist()),
