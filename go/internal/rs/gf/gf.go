@@ -1,8 +1,11 @@
 // Package gf: GF(2^32-5) scalars and the byte<->symbol mapping of slime.
 //
-// Drop-in replacement for encryptio/slime's internal/rs/gf backed by the
-// MI355X codec in libslime_rs.so (include/slime_rs.h): MapToGF, MapToGFWith
-// and MapFromGF run on the GPU; MInverse and Raise are host scalars.
+// Drop-in replacement for encryptio/slime's internal/rs/gf backed by
+// libslime_rs.so (include/slime_rs.h): MapToGF, MapToGFWith and MapFromGF
+// take and return host bytes, so the library runs them on the host cores in
+// place on these slices (AVX2 passes over its copy pool; the GPU codec kernels
+// serve device-resident buffers and the fused object entry points);
+// MInverse and Raise are host scalars.
 package gf
 
 /*
@@ -21,8 +24,9 @@ import (
 
 const MaxVal = 1<<32 - 5
 
-// Device is the GPU MapToGF / MapToGFWith / MapFromGF run on; -1
-// (C.SLIME_RS_ANY_DEVICE, the default) lets libslime_rs's device pool pick.
+// Device is the GPU MapToGF / MapToGFWith / MapFromGF would use if the
+// library's codec placement sends them to the GPU (slime_gf_codec_placement);
+// -1 (C.SLIME_RS_ANY_DEVICE, the default) lets libslime_rs's device pool pick.
 var Device = -1
 
 const detailCap = 512

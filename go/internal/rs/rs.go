@@ -187,7 +187,8 @@ func CreateParities(data [][]uint32, total int) [][]uint32 {
 }
 
 // RecoverData rebuilds all data vectors from exactly len(chunks) surviving code
-// rows with the given indices (internal/rs/vector.go:50), on the GPU.
+// rows with the given indices (internal/rs/vector.go:50): the erased data rows
+// on the GPU, the surviving ones (unit rows of the inverse) on the host.
 func RecoverData(chunks [][]uint32, indices []int) [][]uint32 {
 	if len(chunks) != len(indices) {
 		panic("RecoverData: len(chunks) != len(indices)")
