@@ -34,7 +34,8 @@ using apply::MfmaIO;
 // MapToGF's flags over every loaded data word (encode, speculative pass) in
 // two registers: the unsigned maximum of the words (bit0: >= p) and their
 // signed maximum (the unsigned maximum of word ^ 1<<31; bit1: >= p) --
-// a byte swap (v_perm_b32) and two max per word, as one asm chain per word.
+// a byte swap (v_perm_b32) per word and one v_max3 of each kind per two
+// words, as one asm chain per pair.
 // Written in C, the compiler batched the byte swaps of a K step ahead of its
 // MFMAs and the refill form spilled 56 VGPRs at four K steps (64/80); the
 // chain keeps one temporary live, and the refill form fits two waves per
@@ -45,16 +46,18 @@ struct FlagPre {
   template <class V>
   __device__ __forceinline__ void operator()(const V& v) {
     constexpr int W = sizeof(V) / sizeof(uint32_t);
+    static_assert(W % 2 == 0, "pairs of words");
 #pragma unroll
-    for (int c = 0; c < W; ++c) {
-      uint32_t t;
-      const uint32_t w = v[c];
+    for (int c = 0; c < W; c += 2) {  // two words per v_max3: 2 VALU ops per word
+      uint32_t t0, t1;
+      const uint32_t w0 = v[c], w1 = v[c + 1];
       asm volatile(
-          "v_perm_b32 %0, %3, %3, %4\n\t"
-          "v_max_u32 %1, %1, %0\n\t"
-          "v_max_i32 %2, %2, %0"
-          : "=&v"(t), "+v"(umax), "+v"(smax)
-          : "v"(w), "s"(0x00010203u));
+          "v_perm_b32 %0, %4, %4, %6\n\t"
+          "v_perm_b32 %1, %5, %5, %6\n\t"
+          "v_max3_u32 %2, %2, %0, %1\n\t"
+          "v_max3_i32 %3, %3, %0, %1"
+          : "=&v"(t0), "=&v"(t1), "+v"(umax), "+v"(smax)
+          : "v"(w0), "v"(w1), "s"(0x00010203u));
     }
   }
   __device__ __forceinline__ uint32_t bits() const {
@@ -350,31 +353,47 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
   auto slot_of = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
   auto colb_of = [&](uint32_t e) { return ((e % units) * (16 * W) + ln * W) << 2; };
   const uint32_t n = *count;
+  // The list (ascending tiles of each object, roughly) is cut into G
+  // contiguous streams of 8 waves each, as the re-encode's flat walk: all
+  // waves on one window of one object streamed at 2.3 TB/s
+  // (profiles/r03/s35_mfma_bytes/).  Entry i of stream s is list[s*len + i];
+  // wave (s, r) takes i = r, r + 8, ...  The list word and the mapping of the
+  // entry after next are loaded one entry ahead, so the refill's addresses
+  // never wait on a dependent load.
+  const uint32_t G = nwaves / 8 ? nwaves / 8 : 1;
+  const uint32_t len = (n + G - 1) / G;
+  const uint32_t sid = wave / 8 < G ? wave / 8 : G - 1, r8 = wave % 8;
+  const uint32_t lo = sid * len, hi = std::min(n, lo + len);
   apply::NoPre pre;
-  uint32_t t = wave;
-  if (t < n) {
+  uint32_t i = lo + r8;
+  if (wave / 8 < G && i < hi) {
     apply::vec_t<W> x[KS][4];
-    uint32_t e = list[t];
-    apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(e / units)), soff, colb_of(e));
+    uint32_t e = list[i];
     uint32_t mo = mapping[e / units];
-    while (t < n) {
-      const uint32_t tn = t + nwaves;
-      const uint32_t en = tn < n ? list[tn] : e;
-      const uint32_t mn = tn < n ? mapping[en / units] : mo;
+    uint32_t en = i + 8 < hi ? list[i + 8] : e;
+    uint32_t mn = i + 8 < hi ? mapping[en / units] : mo;
+    apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(e / units)), soff, colb_of(e));
+    while (i < hi) {
+      const uint32_t in_ = i + 8;
+      // entry in_ + 8's list word and mapping, in flight during this tile
+      const uint32_t enn = in_ + 8 < hi ? list[in_ + 8] : en;
       const uint32_t o = e / units;
       const uint32_t m = __builtin_amdgcn_readfirstlane(mo);
       const MfmaIO io{0x80808080u ^ be(m), m};
       char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
-      if (tn < n)
+      if (in_ < hi)
         apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(en / units)), soff,
                                                         colb_of(en), lds, lrowc, loff, MT, rows, lane, lg, ob,
                                                         colb_of(e), true, io, pre);
       else
         apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg, ob,
                                                          colb_of(e), true, io, pre);
-      t = tn;
+      const uint32_t mnn = in_ + 8 < hi ? mapping[enn / units] : mn;
+      i = in_;
       e = en;
       mo = mn;
+      en = enn;
+      mn = mnn;
     }
   }
   // Edge ranges of the switched objects, per phase-0 segment; object i's
