@@ -444,9 +444,9 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
 
 def _bytes_traffic(args, config: str, need: int, kernels: dict) -> dict:
     """PMC bytes per step of the byte path's kernels at `config`, replayed from
-    profiles/r03/pmc_bytes.json only where every kernel's machine code matches
+    profiles/r04/pmc_bytes.json only where every kernel's machine code matches
     this build (slime_amd/codeobj.py); {} otherwise."""
-    path = os.path.join(ROOT, "profiles", "r03", "pmc_bytes.json")
+    path = os.path.join(ROOT, "profiles", "r04", "pmc_bytes.json")
     try:
         entries = json.load(open(path))
     except (OSError, ValueError):
@@ -461,7 +461,7 @@ def _bytes_traffic(args, config: str, need: int, kernels: dict) -> dict:
                    for n in names):
             return {}
         out[what] = sum(ks[n]["hbm_bytes"] for n in names)
-    out["source"] = f"replayed: profiles/r03/pmc_bytes.json (session {e.get('session', '?')}, matching machine code)"
+    out["source"] = f"replayed: profiles/r04/pmc_bytes.json (session {e.get('session', '?')}, matching machine code)"
     return out
 
 

@@ -219,6 +219,19 @@ __device__ __forceinline__ Segment segment_of(uint64_t wi, uint32_t nseg, uint64
   return g;
 }
 
+// Interior vectors of an encode window: vectors v (from the window's column
+// 0) whose four words in the last data chunk (k-1) -- hence in every data
+// chunk -- are whole object words, so no splitVector padding, partial last
+// word or data-chunk tail is involved: lim + 4v + 3 < whole, with whole = nw
+// (S a multiple of 4) or nw - 1 (the last word partial).  Objects whose size
+// fills every chunk exactly (256 MiB at 8/12 and 64/80) are all interior.
+__host__ __device__ inline uint64_t interior_vectors(uint64_t S, uint64_t L, uint64_t col0, uint32_t k) {
+  const uint64_t nw = (S + 3) / 4;
+  const uint64_t whole = S % 4 ? nw - 1 : nw;
+  const uint64_t lim = (uint64_t)(k - 1) * L + col0;
+  return whole > lim ? (whole - lim) / 4 : 0;
+}
+
 // MODE 0: speculative encode with m = 0, OR-ing MapToGF's flag bits into
 //         flags[obj] (the caller's status array, zeroed first).
 // MODE 1: re-encode objects with mapping[obj] != 0 and status[obj] == 0.
@@ -508,8 +521,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_pipe_kernel(
     uint8_t* const par = slot + (uint64_t)K * chunk;
     // Interior tiles st < nint: end = v0 + (st+1)*64U <= v1 and
     // (K-1)L + col0 + 4*end < first_tail_word.
-    const uint64_t lim = (uint64_t)(K - 1) * L + col0;
-    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    uint64_t end_max = interior_vectors(S, L, col0, K);
     if (end_max > v1) end_max = v1;
     const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / (64 * U)) : 0u;
     const uint8_t* cb[K];
@@ -637,14 +649,11 @@ __global__ __launch_bounds__(kBlock) void decode_bytes_queue_kernel(
 
 // Interior tiles of an encode window (encode_bytes_pipe_kernel's pipelined
 // prefix, the same count for every object): tiles t with (t+1)*64U <= nvec
-// whose highest word (last data chunk, last unit) is below the object's last
-// word.  Host and device compute it alike (the redo list needs the count).
+// of interior vectors.  Host and device compute it alike (the redo list
+// needs the count).
 __host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L, uint64_t col0, uint64_t ncols, int K,
                                                           int U) {
-  const uint64_t nw = (S + 3) / 4;
-  const uint64_t first_tail_word = nw ? nw - 1 : 0;
-  const uint64_t lim = (uint64_t)(K - 1) * L + col0;
-  uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+  uint64_t end_max = interior_vectors(S, L, col0, (uint32_t)K);
   const uint64_t nvec = ncols >> 2;
   if (end_max > nvec) end_max = nvec;
   return (uint32_t)(end_max / (64 * (uint64_t)U));
@@ -1138,8 +1147,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_wide_pipe_kernel(
     uint8_t* const par = slot + (uint64_t)k * chunk;
     // Interior tiles t < nint: end = v0 + 64(t+1) <= v1 and
     // (k-1)L + col0 + 4*end < first_tail_word.
-    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
-    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    uint64_t end_max = interior_vectors(S, L, col0, k);
     if (end_max > v1) end_max = v1;
     const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / 64) : 0u;
     Flags fl;

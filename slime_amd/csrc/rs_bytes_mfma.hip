@@ -171,8 +171,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
       const bool selm = lane < nobj && mlane != 0 && flags[lane] == 0;
       const uint64_t sel = __ballot(selm);
       const uint32_t count = (uint32_t)__popcll(sel);
-      const uint64_t lim = (uint64_t)(k - 1) * L + col0;
-      uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+      uint64_t end_max = interior_vectors(S, L, col0, k);
       if (end_max > nvec) end_max = nvec;
       const uint32_t nint = (uint32_t)(end_max / TCV);
       auto nth = [&](uint32_t i) {  // object of the i-th selected slot
@@ -247,8 +246,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     uint8_t* const par = slot + (uint64_t)k * chunk;
     // Interior tiles: whole tiles of the segment whose columns are below the
     // object's last word in the last data chunk (k-1), hence in every chunk.
-    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
-    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
+    uint64_t end_max = interior_vectors(S, L, col0, k);
     if (end_max > v1) end_max = v1;
     const uint32_t nint = end_max > v0 ? (uint32_t)((end_max - v0) / TCV) : 0u;
     const MfmaIO io{0x80808080u ^ be(m), m};
@@ -396,23 +394,39 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
       mn = mnn;
     }
   }
-  // Edge ranges of the switched objects, per phase-0 segment; object i's
-  // ranges start on waves offset by i * nwaves / nobj so they run side by side.
-  for (uint64_t wi = 0; wi < (uint64_t)nobj * nseg; ++wi) {
-    const Segment sg = segment_of(wi, nseg, nvec);
-    const uint32_t m = mapping[sg.obj];
-    if (m == 0 || status[sg.obj] != 0) continue;  // uniform
-    const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
-    const uint64_t lim = (uint64_t)(k - 1) * L + col0;
-    uint64_t end_max = first_tail_word > lim ? (first_tail_word - lim - 1) >> 2 : 0;
-    if (end_max > sg.v1) end_max = sg.v1;
-    const uint32_t nint = end_max > sg.v0 ? (uint32_t)((end_max - sg.v0) / TCV) : 0u;
-    const uint64_t e0 = sg.v0 + (uint64_t)nint * TCV;
-    if (e0 >= u1) continue;
-    uint8_t* const slot = slot_of(sg.obj);
-    const uint32_t wrel = (wave + nwaves - (uint32_t)(wi * nwaves / ((uint64_t)nobj * nseg))) % nwaves;
-    (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word, m, rows, k, cs,
-                              coeff, out_idx, e0, nvec, u1, sg.v1, lane, wrel, nwaves);
+  // Edge ranges of the switched objects, per phase-0 segment (none when the
+  // objects fill their chunks exactly).  The switched objects are found 64 at
+  // a time with one ballot (a serial scan of every object's mapping and status
+  // put two dependent loads per object in front of every wave); object i's
+  // ranges start on waves offset by i * nwaves / count so they run side by side.
+  const uint64_t iv = interior_vectors(S, L, col0, k);
+  uint32_t nsel = 0;
+  for (uint32_t ob = 0; ob < nobj; ob += 64) {
+    const uint32_t ol = ob + lane;
+    nsel += (uint32_t)__popcll(__ballot(ol < nobj && mapping[ol] != 0 && status[ol] == 0));
+  }
+  uint32_t si = 0;
+  for (uint32_t ob = 0; ob < nobj && nsel; ob += 64) {
+    const uint32_t ol = ob + lane;
+    const uint32_t ml = ol < nobj ? mapping[ol] : 0u;
+    uint64_t sel = __ballot(ol < nobj && ml != 0 && status[ol] == 0);
+    for (; sel; sel &= sel - 1, ++si) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(sel);
+      const uint32_t o = ob + b;
+      const uint32_t m = __builtin_amdgcn_readlane(ml, b);
+      uint8_t* const slot = slot_of(o);
+      const uint32_t wrel = (wave + nwaves - (uint32_t)((uint64_t)si * nwaves / nsel)) % nwaves;
+      for (uint32_t seg = 0; seg < nseg; ++seg) {
+        const Segment sg = segment_of((uint64_t)o * nseg + seg, nseg, nvec);
+        const uint64_t u1 = sg.last ? nvec + (ncols & 3) : sg.v1;
+        const uint64_t end_max = iv < sg.v1 ? iv : sg.v1;
+        const uint32_t nint = end_max > sg.v0 ? (uint32_t)((end_max - sg.v0) / TCV) : 0u;
+        const uint64_t e0 = sg.v0 + (uint64_t)nint * TCV;
+        if (e0 < u1)
+          (void)encode_edges<false>(slot, slot + (uint64_t)k * chunk, chunk, L, col0, ow, first_tail_word, m, rows, k,
+                                    cs, coeff, out_idx, e0, nvec, u1, sg.v1, lane, wrel, nwaves);
+      }
+    }
   }
 }
 

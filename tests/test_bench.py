@@ -147,14 +147,14 @@ def test_committed_traffic_matches_shipped_kernel_code():
 
 
 def test_committed_byte_traffic_matches_shipped_kernel_code():
-    """The byte path's PMC summary (profiles/r03/pmc_bytes.json, replayed into
+    """The byte path's PMC summary (profiles/r04/pmc_bytes.json, replayed into
     object_bytes_path) covers C3 and C5 on 256 B chunk strides, was measured on
     the machine code of every kernel it names, and its first pass and repair
     move their algorithmic bytes 4L(k+r) / 4L(k+e)."""
     import sys
     sys.path.insert(0, ROOT)
     from slime_amd.codeobj import kernel_code_id
-    entries = json.load(open(os.path.join(ROOT, "profiles", "r03", "pmc_bytes.json")))
+    entries = json.load(open(os.path.join(ROOT, "profiles", "r04", "pmc_bytes.json")))
     lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
     shapes = {"8/12 S=268435456 nobj=128 cs=33554432": (8, 12, 8388608, 128),
               "10/14 S=1073741824 nobj=16 cs=107374336": (10, 14, 26843546, 16)}
@@ -164,7 +164,7 @@ def test_committed_byte_traffic_matches_shipped_kernel_code():
         ks = e["kernels"]
         for name, k in ks.items():
             assert k["kernel_code"] == kernel_code_id(lib, (f"{name}ILi{need}E",)), \
-                f"{name}<{need}> changed since its PMC passes: re-run tools/gpu_r03.sh bpmc_c3 bpmc_c5"
+                f"{name}<{need}> changed since its PMC passes: re-run tools/gpu_r04.sh bpmc_c3 bpmc_c5"
         alg = nobj * 4 * L * total
         assert abs(ks["encode_bytes_queue_kernel"]["hbm_bytes"] / alg - 1) < 0.01
         assert abs(ks["decode_bytes_queue_kernel"]["hbm_bytes"] / (nobj * 4 * L * (need + 4)) - 1) < 0.01
