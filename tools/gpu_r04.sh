@@ -86,6 +86,15 @@ for step in "$@"; do
            run mink1_c5 300 env SLIME_RS_MFMA_MINK=1 python bench.py --preset c5 --global-objects 16 --bytes-path 0 --steps 5 $NOLEGS &&
            run mink1_c2 300 env SLIME_RS_MFMA_MINK=1 python bench.py --preset c2 --bytes-path 0 --steps 5 $NOLEGS ;;
     # kernel times of the wide byte path (64/80, 32 x 256 MiB): rocprofv3 stats
+    wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
+          for v in "f2:SLIME_RS_MFMA_ENC_FORM=2" "f0:SLIME_RS_MFMA_ENC_FORM=0"; do
+            run wprof80_${v%%:*} 300 env ${v#*:} rocprofv3 --kernel-trace --stats -d "$OUT/wprof80_${v%%:*}" -o bench --output-format csv -- \
+              python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS || exit 1
+            run wprof96_${v%%:*} 300 env ${v#*:} rocprofv3 --kernel-trace --stats -d "$OUT/wprof96_${v%%:*}" -o bench --output-format csv -- \
+              python3 bench.py --need 96 --total 100 --objects 32 --erase 0,1,2,3 --steps 3 --warmup 1 $NOLEGS || exit 1
+            run wprof48_${v%%:*} 300 env ${v#*:} rocprofv3 --kernel-trace --stats -d "$OUT/wprof48_${v%%:*}" -o bench --output-format csv -- \
+              python3 bench.py --need 48 --total 64 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --warmup 1 $NOLEGS || exit 1
+          done ;;
     wprof) run wprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof" -o bench --output-format csv -- \
              python3 bench.py --need 64 --total 80 --objects 32 --erase 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15 --steps 3 --warmup 1 $NOLEGS ;;
     # C2 and buffer placement: the default (2 MiB chunks, unprobed below 16 GiB), probed, hipMalloc
