@@ -23,6 +23,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -403,6 +404,16 @@ size_t obj_window_bytes() {
     return (size_t)(v < 1 ? 1 : v > 256 ? 256 : v) << 20;
   }();
   return b;
+}
+
+// RecoverData runs its unit rows (present data shards, host mod p) on a side
+// thread beside the device pipeline (env SLIME_RS_RECOVER_OVERLAP=0: after it).
+bool recover_overlap() {
+  static const bool on = [] {
+    const char* e = getenv("SLIME_RS_RECOVER_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 enum class HostPipe : int { Staged = 0, Register = 1, Direct = 2 };
@@ -1468,19 +1479,38 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   // host pass over memory the caller already holds.  Only the erased data
   // rows cross to the device (need chunks in, the erased rows back).
   const std::vector<int> erased = erased_rows(need, indices);
-  if (!erased.empty()) {
-    DeviceLease dl;
-    if (int rc = dl.acquire()) return rc;
-    std::vector<int> have(indices, indices + nindices);
-    PlanRef plan;
-    if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_erased_rows_plan)) return rc;
-    std::vector<uint32_t*> rows;
-    for (int t : erased) rows.push_back(out[t]);
-    if (int rc = host_apply(plan.get(), chunks, rows.data(), L)) return rc;
+  auto unit_rows = [&] {
+    for (int q = 0; q < need; ++q)
+      if (indices[q] < need) host_mod_p(chunks[q], L, out[indices[q]]);
+  };
+  if (erased.empty()) {
+    unit_rows();
+    return 0;
   }
-  for (int q = 0; q < need; ++q)
-    if (indices[q] < need) host_mod_p(chunks[q], L, out[indices[q]]);
-  return 0;
+  DeviceLease dl;
+  if (int rc = dl.acquire()) return rc;
+  std::vector<int> have(indices, indices + nindices);
+  PlanRef plan;
+  if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_erased_rows_plan)) return rc;
+  std::vector<uint32_t*> rows;
+  for (int t : erased) rows.push_back(out[t]);
+  // The unit rows read the same chunks the device pipeline stages and write
+  // outputs it never touches, so they run beside it: while the pipeline
+  // waits on DMA and the kernel, the host cores do the mod-p pass.
+  const size_t unit_bytes = (size_t)(need - (int)erased.size()) * L * 4;
+  std::thread side;
+  if (recover_overlap() && unit_bytes >= (4u << 20)) {
+    try {
+      side = std::thread(unit_rows);
+    } catch (...) {  // no thread to be had: run them after the pipeline
+    }
+  }
+  const int rc = host_apply(plan.get(), chunks, rows.data(), L);
+  if (side.joinable())
+    side.join();
+  else
+    unit_rows();
+  return rc;
 }
 
 // ---- object entry points (host memory): writeChunks / reconstruct ------------------

@@ -207,6 +207,13 @@ for step in "$@"; do
            run c2blk_dec 300 python tools/apply_variants.py --need 4 --total 6 --mib 64 --nobj 32 --decode 1 --separate 0 --variants 13 --blocks 128,192,256,320 --nseg 2 --rounds 6 --queue 400802 ;;
     torchrun1) run torchrun1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 2 ;;
     gpus2) python bench.py --gpus 2 --steps 1 --warmup 0 > "$OUT/gpus2.log" 2>&1; echo "gpus2 rc=$? (2 expected on a 1-GPU box)" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/gpus2.log" ;;
+    # host leg only (unchanged caller, write_chunks/reconstruct): RecoverData overlap and copy-pool size, alternated twice
+    hostab) HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
+            for rep in 1 2; do
+              for v in "base:SLIME_RS_RECOVER_OVERLAP=1" "noov:SLIME_RS_RECOVER_OVERLAP=0" "t8:SLIME_RS_COPY_THREADS=8" "t8noov:SLIME_RS_COPY_THREADS=8 SLIME_RS_RECOVER_OVERLAP=0"; do
+                run hostab_${v%%:*}_$rep 300 env ${v#*:} python bench.py $HA || exit 1
+              done
+            done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
