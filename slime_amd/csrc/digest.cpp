@@ -1,6 +1,7 @@
 // Chunk and object digests (digest.hpp): SHA-256 with the x86 SHA extensions
 // or a portable loop, FNV-1a-64, and the digest thread pool.
 #include "digest.hpp"
+#include "host_copy.hpp"
 
 #include <cpuid.h>
 #include <immintrin.h>
@@ -174,10 +175,7 @@ class Pool {
 int default_threads() {
   const char* s = getenv("SLIME_RS_DIGEST_THREADS");
   if (s && *s) return std::max(0, std::min(atoi(s), 256));
-  cpu_set_t set;
-  int cpus = 16;
-  if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
-  return std::max(0, std::min(cpus, 16) - 1);
+  return std::max(0, std::min(usable_cpus(), 16) - 1);
 }
 
 Pool& pool() {

@@ -2,7 +2,9 @@
 #include "host_copy.hpp"
 
 #include <emmintrin.h>
+#include <sched.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -180,9 +182,29 @@ class Pool {
   std::vector<std::thread> th_;
 };
 
+int usable_cpus_uncached() {
+  cpu_set_t set;
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+      const long q = (atol(quota) + period - 1) / period;
+      if (q > 0 && q < n) n = (int)q;
+    }
+    fclose(f);
+  }
+  return n < 1 ? 1 : n;
+}
+
+// Workers beside the calling thread (env SLIME_RS_COPY_THREADS, 0..64).
+// Default: half the usable CPUs, 1..8.  On the 16-CPU share of the GPU box
+// 8 workers ran the host codec's MapFromGF 1.3-1.6x faster than 4
+// (profiles/r04/s7_hostab); more CPUs than that are left to the caller's
+// own concurrency (a storage server runs many calls at once).
 int env_threads() {
   const char* s = getenv("SLIME_RS_COPY_THREADS");
-  if (!s || !*s) return 4;
+  if (!s || !*s) return std::min(8, std::max(1, usable_cpus_uncached() / 2));
   const int v = atoi(s);
   return v < 0 ? 0 : (v > 64 ? 64 : v);
 }
@@ -195,6 +217,13 @@ Pool& pool() {
 }  // namespace
 
 int copy_pool_threads() { return pool().threads(); }
+
+// A container's share of a large host sees every CPU in its mask but may
+// run only its quota.
+int usable_cpus() {
+  static const int n = usable_cpus_uncached();
+  return n;
+}
 
 void parallel_pieces(size_t n, void (*fn)(const void* ctx, size_t piece), const void* ctx) {
   if (n) pool().run(n, fn, ctx);

@@ -26,4 +26,8 @@ void parallel_pieces(size_t n, void (*fn)(const void* ctx, size_t piece), const 
 // Threads the pool runs besides the caller (env SLIME_RS_COPY_THREADS, default 4).
 int copy_pool_threads();
 
+// CPUs this process may run on: its affinity mask capped by the cgroup
+// CPU quota (cpu.max), at least 1.
+int usable_cpus();
+
 }  // namespace slime

@@ -23,7 +23,6 @@
 #include <mutex>
 #include <random>
 #include <string>
-#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -404,16 +403,6 @@ size_t obj_window_bytes() {
     return (size_t)(v < 1 ? 1 : v > 256 ? 256 : v) << 20;
   }();
   return b;
-}
-
-// RecoverData runs its unit rows (present data shards, host mod p) on a side
-// thread beside the device pipeline (env SLIME_RS_RECOVER_OVERLAP=0: after it).
-bool recover_overlap() {
-  static const bool on = [] {
-    const char* e = getenv("SLIME_RS_RECOVER_OVERLAP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 enum class HostPipe : int { Staged = 0, Register = 1, Direct = 2 };
@@ -1494,23 +1483,12 @@ int slime_rs_recover_data(const uint32_t* const* chunks, const uint64_t* lens, i
   if (int rc = cached_plan(PlanKey{dl.device, 'R', need, 0, have}, &plan, make_erased_rows_plan)) return rc;
   std::vector<uint32_t*> rows;
   for (int t : erased) rows.push_back(out[t]);
-  // The unit rows read the same chunks the device pipeline stages and write
-  // outputs it never touches, so they run beside it: while the pipeline
-  // waits on DMA and the kernel, the host cores do the mod-p pass.
-  const size_t unit_bytes = (size_t)(need - (int)erased.size()) * L * 4;
-  std::thread side;
-  if (recover_overlap() && unit_bytes >= (4u << 20)) {
-    try {
-      side = std::thread(unit_rows);
-    } catch (...) {  // no thread to be had: run them after the pipeline
-    }
-  }
-  const int rc = host_apply(plan.get(), chunks, rows.data(), L);
-  if (side.joinable())
-    side.join();
-  else
-    unit_rows();
-  return rc;
+  // The unit rows run after the pipeline, not beside it on a side thread:
+  // that form measured no faster (fresh-page faults of both compete,
+  // MEASUREMENTS.md round 4, profiles/r04/s7_hostab).
+  if (int rc = host_apply(plan.get(), chunks, rows.data(), L)) return rc;
+  unit_rows();
+  return 0;
 }
 
 // ---- object entry points (host memory): writeChunks / reconstruct ------------------
