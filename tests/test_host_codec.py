@@ -138,6 +138,41 @@ def test_recover_data_all_data_present_is_host_mod_p():
             assert np.array_equal(g, w)
 
 
+def test_concurrent_callers_share_the_pool():
+    """Several threads in the codec at once (a proxy serves many requests,
+    main.go:107-109): their multi-piece jobs interleave on one copy pool; every
+    result must equal the oracle's for its own input."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    rng = np.random.default_rng(11)
+    cases = []
+    for t in range(12):
+        nwords = (3 << 18) + 17 * t  # 3 MiB and a little: several pieces per call
+        words = rng.integers(0, 0x7FFFFFF0, size=nwords, dtype=np.uint32)
+        if t % 3 == 1:
+            words[nwords // 3] = BREAKS_0  # 1<<31 objects in the mix
+        data = words.astype(">u4").tobytes() + bytes([t + 1])
+        rc, n, v = OC.map_to_gf(data)
+        assert rc == 0
+        cases.append((data, n, v, OC.map_from_gf(n, v)))
+
+    def one(i):
+        data, n, v, back = cases[i % len(cases)]
+        for _ in range(3):
+            n2, v2 = gf.MapToGF(data)
+            if n2 != n or not np.array_equal(v2, v):
+                return f"MapToGF case {i}"
+            if not np.array_equal(gf.MapToGFWith(data, n), v):
+                return f"MapToGFWith case {i}"
+            if bytes(gf.MapFromGF(n, v)) != back:
+                return f"MapFromGF case {i}"
+        return None
+
+    with ThreadPoolExecutor(max_workers=6) as ex:
+        errors = [e for e in ex.map(one, range(24)) if e]
+    assert not errors, errors
+
+
 def test_codec_placement_knob():
     assert N.lib.slime_gf_codec_placement(-1) == 0
     with pytest.raises(N.NativeError):
