@@ -355,9 +355,12 @@ bool bind_to_graph(TicketPool& tp, const TicketSet& set, hipStream_t stream) {
   }
   if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
     // The graph did not take the reference: keep the set (the object's
-    // destructor must not hand it back while the graph may replay it).
+    // destructor must not hand it back while the graph may replay it), and
+    // drop our reference so the object and `g` are freed.
     (void)hipGetLastError();
     g->pool = nullptr;
+    (void)hipUserObjectRelease(obj, 1);
+    (void)hipGetLastError();
     return false;
   }
   return true;
