@@ -8,7 +8,7 @@ SRC      := slime_amd/csrc
 OBJ      := build/obj
 LIB      := slime_amd/lib/libslime_rs.so
 
-OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_apply_mfma.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/rs_bytes_mfma.o $(OBJ)/gf_codec.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/host_codec.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/rs_capi.o
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_apply_mfma.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/rs_bytes_mfma.o $(OBJ)/gf_codec.o $(OBJ)/host_blit.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/host_codec.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 CXXTEST  := tests/cpp/rs_host_test
@@ -61,6 +61,10 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# Host-call latency through the C-ABI alone (tools only): make tools/latency_c
+tools/latency_c: tools/latency_c.cpp include/slime_rs.h $(LIB)
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs -Wl,-rpath,'$$ORIGIN/../slime_amd/lib'
 
 # Micro-benchmarks (tools only): make ubench
 ubench: tools/libubench.so

@@ -103,7 +103,7 @@ def parse(argv=None):
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
-    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
+    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
                          "used only when its config and the kernel's machine code match this build)")
     args = ap.parse_args(argv)
@@ -540,6 +540,7 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     t_cps = med(lambda: rs.CreateParities(parts, total, par2))
     g = lambda t: round(data.size / GIB / t, 2)  # noqa: E731
     digests = digest_leg(data, need, total, chunks, have, out, med, g)
+    latency = latency_leg(need, total, erase)
     return {"write_chunks_gibs": g(t_w), "reconstruct_gibs": g(t_r), "write_chunks_zero_copy_gibs": g(t_wz),
             "link": link_probe(obj_mib),
             "pipeline_split": {"write_chunks": split_w, "reconstruct": split_r,
@@ -549,9 +550,57 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
                                      create_parities_batched_gibs=g(t_cps), recover_data_reused_out_gibs=g(t_rd),
                                      with_device_codec=with_device_codec),
             "digests": digests,
+            "latency": latency,
             "object_mib": obj_mib, "erased": erase, "verified": ok,
             "what": "host bytes -> pinned 3-stage ring -> fused byte kernels -> host chunk bytes (and back), "
                     "PCIe-inclusive; not `value`"}
+
+
+def latency_leg(need, total, erase, sizes_kib=(4, 64, 1024, 8192), reps=25) -> dict:
+    """Per-call latency from host memory at request-body sizes (a proxy serves
+    objects of every size, main.go:107-109): median and p90 microseconds of the
+    fused write_chunks / reconstruct and of the unchanged Go API's
+    CreateParity (one row) / RecoverData, caller-reused outputs."""
+    import numpy as np
+    from slime_amd import gf, objects, rs
+    have = [i for i in range(total) if i not in erase][:need]
+    pc = time.perf_counter
+
+    def stats(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = pc()
+            fn()
+            ts.append(pc() - t0)
+        ts.sort()
+        return {"p50_us": round(ts[len(ts) // 2] * 1e6, 1), "p90_us": round(ts[(9 * len(ts)) // 10] * 1e6, 1)}
+
+    rows, ok = [], True
+    rng = np.random.default_rng(0x1A7)
+    for kib in sizes_kib:
+        data = rng.integers(0, 256, size=kib << 10, dtype=np.uint8)
+        cb = objects.chunk_size(data.size, need)
+        chunks = [np.zeros(cb, dtype=np.uint8) for _ in range(total)]
+        out = np.zeros(data.size, dtype=np.uint8)
+        box = {}
+        w = stats(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
+        surv = [chunks[i] for i in have]
+        rc = stats(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
+        ok = ok and bool(np.array_equal(out, data))
+        m, words = gf.MapToGF(data)
+        parts = objects.split_vector(words, need)
+        par = np.zeros(parts[0].size, dtype=np.uint32)
+        cp = stats(lambda: rs.CreateParity(parts, need, par))
+        sym = [gf.MapToGFWith(chunks[i], m) for i in have]
+        rec = [np.zeros(sym[0].size, dtype=np.uint32) for _ in range(need)]
+        rd = stats(lambda: rs.RecoverData(sym, have, rec))
+        ok = ok and all(np.array_equal(rec[i], parts[i]) for i in range(need))
+        rows.append({"object_kib": kib, "write_chunks": w, "reconstruct": rc, "create_parity_one_row": cp,
+                     "recover_data": rd})
+    return {"sizes": rows, "reps": reps, "erased": erase, "verified": ok,
+            "what": "wall time per host call (host bytes in, host bytes out, PCIe and launch included), "
+                    "median and 90th percentile"}
 
 
 def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:

@@ -119,6 +119,27 @@ uint32_t object_segments(uint32_t nobj, uint64_t ncols);
 // 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
 // Env SLIME_RS_SEGMENTS forces a count (tuning).  0 when the launch has too
 // many units for 32-bit tickets (the caller takes the static kernel).
+// Walk units of a queue launch over nobj objects of ncols columns (4 columns
+// a lane, 64 U lanes a tile, C tiles a unit, `spread` segments an object:
+// TicketWalk's numbering, empty units included).
+inline uint64_t queue_units(uint32_t nobj, uint64_t ncols, int U, int C, uint32_t spread) {
+  const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
+  const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C), s = spread ? spread : 1;
+  return (uint64_t)nobj * s * ((groups + s - 1) / s) * 4;
+}
+
+// Blocks of a queue launch with `units` walk units: the full grid, or one
+// wave per unit (4 waves a block) when there are fewer.  Every wave of a
+// queue launch draws from the counters and counts itself out with
+// memory-side atomics (TicketWalk::finish): a full grid over the few units
+// of a host call on a small object spent ~20 us there, against ~2 us of
+// work (profiles/r04/s8_lat*).  Edge tiles and column tails are strided over
+// whatever grid runs, so any grid is correct.
+inline uint64_t queue_blocks(uint64_t full, uint64_t units) {
+  const uint64_t want = (units + 3) / 4;
+  return want < 1 ? 1 : want < full ? want : full;
+}
+
 inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
   const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
   const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
@@ -208,6 +229,17 @@ bool bytes_mfma_eligible(const BytesLaunch& a, bool encode);
 hipError_t launch_encode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_decode_bytes_mfma(const BytesLaunch& a, hipStream_t stream);
 hipError_t launch_select_mapping(uint32_t* mapping, uint32_t* status, uint32_t nobj, hipStream_t stream);
+
+// --- small host<->device transfers as one kernel (host_blit.hip) ----------
+// dst/src: device addresses (device memory, or pinned host memory mapped
+// into the device's address space); any alignment.
+struct BlitSpan {
+  void* dst;
+  const void* src;
+  uint64_t bytes;
+};
+constexpr int kBlitSpans = 32;  // spans per launch (larger lists take several)
+hipError_t launch_blit(const BlitSpan* spans, int n, hipStream_t stream);
 
 // --- byte <-> symbol codec (internal/rs/gf/map.go) -------------------------
 // Pack len bytes big-endian into ceil(len/4) words (zero low bytes in a partial

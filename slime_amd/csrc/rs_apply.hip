@@ -185,7 +185,7 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
   const Geometry& geo = geometry();
-  const uint64_t blocks = geo.target ? geo.target : kQueueBlocks;
+  const uint64_t blocks = queue_blocks(geo.target ? geo.target : kQueueBlocks, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(
       stream,
       [&](uint32_t* set) {

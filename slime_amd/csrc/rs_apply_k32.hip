@@ -29,7 +29,7 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
   const ApplyGeometry& geo = apply_geometry();
-  const uint64_t blocks = geo.target ? geo.target : 256;
+  const uint64_t blocks = queue_blocks(geo.target ? geo.target : 256, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(
       stream,
       [&](uint32_t* set) {

@@ -416,8 +416,26 @@ struct TicketWalk {
         ntiles(ntiles_),
         lane(lane_) {
     p = hw_xcc_id() % NC;
+    if (!skip_empty()) return;
     if (!SYNC) request();
     next_unit();
+  }
+  // Partitions with no units at all (a launch of fewer than NC groups: a
+  // host call on a small object) are passed over without a draw -- each draw
+  // is a memory-side atomic round trip of about a microsecond, and a wave
+  // that asked all NC counters spent most of such a launch on them.
+  // Partition p holds units iff p < ngrp_all, so the empty ones are the tail
+  // p..NC-1: counted dry at once, the walk goes on at partition 0.  false:
+  // every partition is dry (live cleared).
+  __device__ __forceinline__ bool skip_empty() {
+    if (p < ngrp_all) return true;
+    dry += NC - p;
+    p = 0;
+    if (ngrp_all == 0 || dry >= NC) {
+      live = false;
+      return false;
+    }
+    return true;
   }
   __device__ __forceinline__ void request() {
     pend = 0;
@@ -435,18 +453,19 @@ struct TicketWalk {
         fresh = false;
       } else {
         if (SYNC) request();
-        l = __builtin_amdgcn_readfirstlane(pend);
+        l = __builtin_amdgcn_readlane(pend, 0);  // lane 0 drew it, whatever the exec mask
         bl = l + 1;
         bn = TB - 1;
       }
       const uint32_t units = 4 * ((ngrp_all + NC - 1 - p) / NC);
       if (l >= units) {
-        if (++dry == NC) {
+        if (++dry >= NC) {
           live = false;
           return;
         }
         p = p + 1 == NC ? 0 : p + 1;
         bn = 0;
+        if (!skip_empty()) return;
         if (fresh && !SYNC) request();  // else the batch's successor is already pending
         continue;
       }

@@ -124,7 +124,8 @@ hipError_t dec_pipe(const BytesLaunch& a, hipStream_t s) {
         s,
         [&](uint32_t* set) {
           hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, QU, queue_tiles<QU>(), kQueueCounters>),
-                             dim3((uint32_t)kQueueBlocks), dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
+                             dim3((uint32_t)queue_blocks(kQueueBlocks, queue_units(a.nobj, ncols, QU, queue_tiles<QU>(), spread))),
+                             dim3(kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
                              ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, set, spread);
           return hipGetLastError();
         },

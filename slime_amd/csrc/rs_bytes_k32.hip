@@ -65,7 +65,8 @@ hipError_t dec_k32(const BytesLaunch& a, hipStream_t s) {
         s,
         [&](uint32_t* set) {
           hipLaunchKernelGGL((bytes::decode_bytes_queue_kernel<K, 1, kQueueTiles, kQueueCounters>),
-                             dim3((uint32_t)kBlocks), dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
+                             dim3((uint32_t)queue_blocks(kBlocks, queue_units(a.nobj, ncols, 1, kQueueTiles, spread))),
+                             dim3(apply::kBlock), 0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0,
                              ncols, a.nobj, a.rows, a.coeff, a.in_idx, a.out_idx, a.mapping, set, spread);
           return hipGetLastError();
         },

@@ -87,7 +87,8 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       s,
       [&](uint32_t* set) {
         hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>),
-                           dim3(switch_grid<K>((uint64_t)a.nobj * l.units)), dim3(apply::kBlock), 0, s,
+                           dim3((uint32_t)queue_blocks(switch_grid<K>((uint64_t)a.nobj * l.units), (uint64_t)a.nobj * l.units)),
+                           dim3(apply::kBlock), 0, s,
                            a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                            a.out_idx, a.flags, set, l.spread, record, l.units);
         return hipGetLastError();

@@ -357,6 +357,15 @@ struct Workspace {
     HIP_TRY(hipEventCreateWithFlags(&cev, hipEventDisableTiming));
     return 0;
   }
+  // Every stage stream waits for the work queued on `stream` so far (a
+  // call's setup: zeroed flags, the mapping) -- ordering on the device, no
+  // host round trip.
+  int fence_stages(int nstages) {
+    if (int rc = ensure_stages()) return rc;
+    HIP_TRY(hipEventRecord(cev, stream));
+    for (int s = 0; s < nstages && s < kMaxStages; ++s) HIP_TRY(hipStreamWaitEvent(sst[s], cev, 0));
+    return 0;
+  }
 };
 
 PerDeviceFreeList<Workspace> g_ws_free;  // most recently released first (device_pool.hpp)
@@ -521,8 +530,37 @@ bool dma_2d() {
   return on;
 }
 
+// Windows moving at most this many bytes one way go as one copy kernel over
+// the mapped pinned ring instead of copy-engine transfers (host_blit.hip):
+// env SLIME_RS_BLIT_KIB, default 4096; 0 = always the copy engines.
+uint64_t blit_max_bytes() {
+  static const uint64_t b = [] {
+    const char* e = getenv("SLIME_RS_BLIT_KIB");
+    const long long v = e ? atoll(e) : 4096;
+    return v > 0 ? (uint64_t)v << 10 : 0ull;
+  }();
+  return b;
+}
+
 int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
               hipStream_t st) {
+  uint64_t total = 0;
+  for (const Span& s : sp) total += s.bytes;
+  if (total && total <= blit_max_bytes()) {
+    std::vector<BlitSpan> bl;
+    bl.reserve(sp.size());
+    for (size_t i = 0; i < sp.size();) {  // neighbours contiguous on both sides merge, as below
+      size_t j = i + 1, bytes = sp[i].bytes;
+      while (j < sp.size() && sp[j].dev_off == sp[i].dev_off + bytes && off[j] == off[i] + bytes) bytes += sp[j++].bytes;
+      if (h2d)
+        bl.push_back({dev + sp[i].dev_off, pin + off[i], bytes});
+      else
+        bl.push_back({pin + off[i], dev + sp[i].dev_off, bytes});
+      i = j;
+    }
+    HIP_TRY(launch_blit(bl.data(), (int)bl.size(), st));
+    return 0;
+  }
   if (dma_2d() && sp.size() >= 2) {
     for (size_t i = 0; i < sp.size();) {
       size_t j = i + 1;
@@ -1525,6 +1563,23 @@ uint64_t slime_rs_chunk_size(uint64_t size, int need) { return need > 0 ? 4 * sl
 static int pick_mapping(hipStream_t st, const uint8_t* d_bytes, uint64_t len, uint32_t* d_words,
                         uint32_t* d_scratch, uint32_t* mapping);
 
+// Data chunk j's bytes past the object (its tail): zero low bytes of the
+// object's partial last word, then splitVector's zero symbols serialised under
+// mapping m as BE(m) (map.go:28-33,103-113; multi_store.go:279-296).  They
+// depend only on m and the object's length, so the host writes them.
+static void write_data_tails(uint64_t size, int need, uint64_t chunk, uint8_t* const* chunks, uint32_t m) {
+  const uint8_t pad[4] = {(uint8_t)(m >> 24), (uint8_t)(m >> 16), (uint8_t)(m >> 8), (uint8_t)m};
+  const uint64_t word_end = 4 * ((size + 3) / 4);  // end of the object's last (possibly partial) word
+  for (int j = 0; j < need; ++j) {
+    const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk;
+    uint8_t* c = chunks[j];
+    const uint64_t body = size > lo ? std::min(size, hi) - lo : 0;
+    const uint64_t zero_end = word_end > lo ? std::min(word_end, hi) - lo : 0;
+    if (zero_end > body) memset(c + body, 0, zero_end - body);
+    for (uint64_t o = std::max(body, zero_end); o < chunk; o += 4) memcpy(c + o, pad, 4);
+  }
+}
+
 static int write_data_chunks(int dev, const uint8_t* data, uint64_t size, int need, uint8_t* const* chunks,
                              uint32_t* mapping) {
   const uint64_t L = slot_L(size, (uint32_t)need), chunk = 4 * L, nw = (size + 3) / 4;
@@ -1540,17 +1595,12 @@ static int write_data_chunks(int dev, const uint8_t* data, uint64_t size, int ne
   uint32_t m = 0;
   if (int rc = pick_mapping(ws->stream, d_bytes, size, d_words, (uint32_t*)(ws->dbuf + bbytes + wbytes), &m))
     return rc;
-  const uint8_t pad[4] = {(uint8_t)(m >> 24), (uint8_t)(m >> 16), (uint8_t)(m >> 8), (uint8_t)m};
-  const uint64_t word_end = 4 * nw;  // end of the object's last (possibly partial) word
   for (int j = 0; j < need; ++j) {
-    const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk;
-    uint8_t* c = chunks[j];
-    const uint64_t body = size > lo ? std::min(size, hi) - lo : 0;
-    if (body && c != data + lo) memcpy(c, data + lo, body);  // an aliased chunk is already the object's bytes
-    const uint64_t zero_end = word_end > lo ? std::min(word_end, hi) - lo : 0;
-    if (zero_end > body) memset(c + body, 0, zero_end - body);
-    for (uint64_t o = std::max(body, zero_end); o < chunk; o += 4) memcpy(c + o, pad, 4);
+    const uint64_t lo = (uint64_t)j * chunk;
+    const uint64_t body = size > lo ? std::min(size, lo + chunk) - lo : 0;
+    if (body && chunks[j] != data + lo) memcpy(chunks[j], data + lo, body);  // an aliased chunk is already the object's bytes
   }
+  write_data_tails(size, need, chunk, chunks, m);
   *mapping = m;
   return 0;
 }
@@ -1618,13 +1668,23 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
   const int r = total - need;
   const uint64_t cl = window_cols(L, (uint64_t)total, obj_window_bytes());
   const uint64_t nwin = (L + cl - 1) / cl;
+  // One window (objects up to about the window size): MapToGF's flags come
+  // back with the parity, so a mapping-0 object costs one host round trip
+  // in all.
+  const bool one = nwin == 1;
+  uint32_t ms[2] = {0, 0};
+  static const uint32_t kZero[2] = {0, 0};
   auto body = [&]() -> int {
-    HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
-    HIP_TRY(hipStreamSynchronize(ws->stream));
+    if (!one) {  // the flags start at zero for every window's kernel
+      HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
+      if (int rc = ws->fence_stages((int)std::min<uint64_t>(host_stages(), nwin))) return rc;
+    }
     if (int rc = run_windows(
-            "write_chunks", ws, slot, nwin, (size_t)total * round64(cl * 4),
+            "write_chunks", ws, slot, nwin, (size_t)total * round64(cl * 4) + 128,
             [&](uint64_t c, int, Window& w) {
               const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
+              if (one)  // the flags zeroed by the window's own upload, ahead of its kernel
+                w.in.push_back({(uint8_t*)kZero, (uint64_t)((uint8_t*)d_map - slot), sizeof(kZero)});
               for (int j = 0; j < need; ++j) {
                 const uint64_t lo = (uint64_t)j * chunk + 4 * c0, hi = std::min(size, lo + 4 * nc);
                 if (lo >= hi) continue;
@@ -1633,6 +1693,7 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
               }
               for (int i = 0; i < r; ++i)
                 w.out.push_back({chunks[need + i] + 4 * c0, (uint64_t)(need + i) * chunk + 4 * c0, 4 * nc});
+              if (one) w.out.push_back({(uint8_t*)ms, (uint64_t)((uint8_t*)d_map - slot), sizeof(ms)});
             },
             [&](uint64_t c, int, hipStream_t st) -> int {
               BytesLaunch a = bytes_launch(plan, slot, stride, 0, L, size, 1, 0, d_status, d_map);
@@ -1645,10 +1706,18 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
               if (dg) dg->parity_ready(4 * std::min(L, (c + 1) * cl));
             }))
       return rc;
-    HIP_TRY(launch_select_mapping(d_map, d_status, 1, ws->stream));
-    uint32_t ms[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
-    HIP_TRY(hipStreamSynchronize(ws->stream));
+    // One window: ms came back with the parity, ms[1] holding MapToGF's
+    // flags (bit 0: a word >= p).  With bit 0 clear the mapping is 0 and
+    // nothing else runs; otherwise -- and after several windows -- the
+    // device chooses (select_mapping) as the 1<<31 re-encode and the
+    // fallback expect.
+    if (!one || (ms[1] & 1u)) {  // every window has landed: the flags are complete
+      HIP_TRY(launch_select_mapping(d_map, d_status, 1, ws->stream));
+      HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
+      HIP_TRY(hipStreamSynchronize(ws->stream));
+    } else {
+      ms[0] = ms[1] = 0;
+    }
     const bool redo = ms[0] != 0 || ms[1] != 0;
     if (dg) {
       if (redo)
@@ -1664,16 +1733,14 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
     } else if (ms[0] != 0) {  // mapping 1<<31: re-encode the whole object (map.go:47-62)
       HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, stride, 0, L, size, 1, 1, d_status, d_map), ws->stream));
     }
-    // The data-chunk tail (partial word, splitVector padding), and every
-    // parity chunk again if the mapping was not 0.
-    std::vector<Span> out;
-    for (int j = 0; j < need; ++j) {
-      const uint64_t lo = (uint64_t)j * chunk, start = std::max(size, lo);
-      if (start < lo + chunk) out.push_back({chunks[j] + (start - lo), start, lo + chunk - start});
-    }
-    if (redo)
+    // The data-chunk tails (partial word, splitVector padding) on the host,
+    // and every parity chunk again from the device if the mapping was not 0.
+    write_data_tails(size, need, chunk, chunks, ms[0]);
+    if (redo) {
+      std::vector<Span> out;
       for (int i = need; i < total; ++i) out.push_back({chunks[i], (uint64_t)i * chunk, chunk});
-    if (int rc = staged_d2h(ws, slot, out.data(), out.size())) return rc;
+      if (int rc = staged_d2h(ws, slot, out.data(), out.size())) return rc;
+    }
     *mapping = ms[0];
     if (dg && redo) {
       dg->parity_ready(chunk);
@@ -1754,13 +1821,15 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
   // the object's bytes of those columns out.
   const uint64_t cl = window_cols(L, 2 * (uint64_t)need, obj_window_bytes());
   const uint64_t nwin = (L + cl - 1) / cl;
+  // The mapping goes up with every window's inputs (the same word each time:
+  // each window's kernel reads it behind its own upload).
+  const uint32_t map_word = mapping;
   auto body = [&]() -> int {
-    HIP_TRY(hipMemcpyAsync(d_map, &mapping, 4, hipMemcpyHostToDevice, ws->stream));
-    HIP_TRY(hipStreamSynchronize(ws->stream));
     return run_windows(
-        "reconstruct", ws, slot, nwin, (size_t)2 * need * round64(cl * 4),
+        "reconstruct", ws, slot, nwin, (size_t)2 * need * round64(cl * 4) + 64,
         [&](uint64_t c, int, Window& w) {
           const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
+          w.in.push_back({(uint8_t*)&map_word, (uint64_t)((uint8_t*)d_map - slot), 4});
           for (int q = 0; q < need; ++q)
             w.in.push_back({const_cast<uint8_t*>(chunks[q]) + 4 * c0, (uint64_t)q * chunk_bytes + 4 * c0, 4 * nc});
           for (int t = 0; t < need; ++t) {

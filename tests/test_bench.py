@@ -135,13 +135,13 @@ def test_committed_traffic_matches_shipped_kernel_code():
     import sys
     sys.path.insert(0, ROOT)
     from slime_amd.codeobj import kernel_code_id
-    tj = json.load(open(os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")))
+    tj = json.load(open(os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")))
     assert tj["config"] == "8/12 L=8388608 nobj=128" and tj["kernel"] == "rs_apply_queue_kernel"
     lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
     code = kernel_code_id(lib, ("rs_apply_queue_kernelILi8E",))
     assert code is not None
     assert tj["kernel_code"] == code, \
-        "apply kernel's machine code changed since its PMC passes: re-run tools/gpu_r03.sh pmc_fetch pmc_write"
+        "apply kernel's machine code changed since its PMC passes: re-run tools/gpu_r04.sh pmc_fetch pmc_write, then tools/pmc_traffic.py"
     alg = 128 * 4 * 8388608 * 12
     assert abs(tj["hbm_bytes_per_launch"] / alg - 1) < 0.01  # no wasted re-reads
 

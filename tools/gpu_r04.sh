@@ -41,9 +41,9 @@ for step in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
             python3 bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
     pmc_fetch) run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc \
-            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
     pmc_write) run pmc_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc \
-            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --host-path 0 --bytes-path 0 --alloc-probe 0 ;;
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
     # byte-path kernels (object_bytes_path leg) at C3 and C5: kernel stats + traffic passes
     bprof_c3) run bprof_c3 600 rocprofv3 --kernel-trace --stats -d "$OUT/bprof_c3" -o bench --output-format csv -- \
             python3 bench.py --steps 5 --warmup 1 $NOLEGS ;;
@@ -214,6 +214,22 @@ for step in "$@"; do
                 run hostab_${v%%:*}_$rep 300 env ${v#*:} python bench.py $HA || exit 1
               done
             done ;;
+    latprobe) run latprobe 200 python tools/latency_probe.py ;;
+    latc) run latc 200 tools/latency_c 300 ;;
+    concsmall) run conc4k 200 python tools/host_concurrency.py --kib 4 --reps 300 --delay 0 --threads 1,2,4,8,16 &&
+               run conc64k 200 python tools/host_concurrency.py --kib 64 --reps 200 --delay 0 --threads 1,2,4,8,16 ;;
+    latwin) for w in 16 4 2; do run latwin_$w 120 env SLIME_RS_OBJ_WINDOW_MIB=$w tools/latency_c 100 || exit 1; done ;;
+    latab) for rep in 1 2; do run latab_blit_$rep 120 tools/latency_c 200 && run latab_sdma_$rep 120 env SLIME_RS_BLIT_KIB=0 tools/latency_c 200 &&
+             run latab_rocblit_$rep 120 env SLIME_RS_BLIT_KIB=0 GPU_FORCE_BLIT_COPY_SIZE=4096 tools/latency_c 200 || exit 1; done ;;
+    latenv) run latenv_base 120 tools/latency_c 200 && run latenv_blit 120 env GPU_FORCE_BLIT_COPY_SIZE=4096 tools/latency_c 200 &&
+            run latenv_nosdma 120 env HSA_ENABLE_SDMA=0 tools/latency_c 200 && run latenv_base2 120 tools/latency_c 200 ;;
+    latcprof) run latcprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d "$OUT/latcprof" -o lat --output-format csv -- tools/latency_c 50 ;;
+    lattrace) run lattrace 200 env SLIME_RS_PIPE_TRACE=1 python tools/latency_probe.py ;;
+    latprof) run latprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d "$OUT/latprof" -o lat --output-format csv -- \
+            python3 tools/latency_probe.py ;;
+    hostonly) run hostonly 300 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 ;;
+    hostprof) run hostprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/hostprof" -o host --output-format csv -- \
+            python3 bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

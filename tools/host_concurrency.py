@@ -5,7 +5,7 @@ T threads, each writing (or reconstructing) its own 64 MiB 8/12 objects back
 to back; aggregate object GiB/s over the wall time, per T.  ctypes releases
 the GIL for the C calls, so the threads run the library concurrently.
 
-    python tools/host_concurrency.py [--threads 1,2,4,8,16] [--reps 6] [--mib 64]
+    python tools/host_concurrency.py [--threads 1,2,4,8,16] [--reps 6] [--mib 64 | --kib 4]
 """
 from __future__ import annotations
 
@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--threads", default="1,2,4,8,16")
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--mib", type=int, default=64)
+    ap.add_argument("--kib", type=int, default=0, help="object size in KiB (overrides --mib): small-object calls")
     ap.add_argument("--need", type=int, default=8)
     ap.add_argument("--total", type=int, default=12)
     ap.add_argument("--delay", type=float, default=15.0,
@@ -49,7 +50,7 @@ def main():
     from slime_amd import objects
     need, total = args.need, args.total
     tmax = max(int(t) for t in args.threads.split(","))
-    size = args.mib << 20
+    size = (args.kib << 10) if args.kib else (args.mib << 20)
     cb = objects.chunk_size(size, need)
     rng = np.random.default_rng(25)
     objs = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(tmax)]
@@ -95,18 +96,18 @@ def main():
             t.join()
         dt = time.perf_counter() - t0
         assert not errors, errors
-        return T * args.reps * size / GIB / dt
+        return T * args.reps * size / GIB / dt, T * args.reps / dt
 
     for kind in ("write", "write_zero_copy", "reconstruct", "write_digest"):
         for T in (int(t) for t in args.threads.split(",")):
             time.sleep(0.5)  # let the cgroup's CPU quota refill between runs
             th0 = throttled_usec()
-            g = run(kind, T)
-            results.append({"kind": kind, "threads": T, "gibs": round(g, 2),
+            g, calls = run(kind, T)
+            results.append({"kind": kind, "threads": T, "gibs": round(g, 2), "calls_per_s": round(calls),
                             "throttled_ms": round((throttled_usec() - th0) / 1e3, 1)})
             print(json.dumps(results[-1]), flush=True)
     ok = all(outs[i].tobytes() == objs[i].tobytes() for i in range(tmax))
-    print(json.dumps({"verified": ok, "object_mib": args.mib, "code": f"{need}/{total}", "reps": args.reps}))
+    print(json.dumps({"verified": ok, "object_bytes": size, "code": f"{need}/{total}", "reps": args.reps}))
 
 
 if __name__ == "__main__":
