@@ -216,6 +216,7 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    concc) for t in 1 2 4 8 16; do run concc_$t 120 tools/latency_c 400 $t || exit 1; done ;;
     concsmall) run conc4k 200 python tools/host_concurrency.py --kib 4 --reps 300 --delay 0 --threads 1,2,4,8,16 &&
                run conc64k 200 python tools/host_concurrency.py --kib 64 --reps 200 --delay 0 --threads 1,2,4,8,16 ;;
     latwin) for w in 16 4 2; do run latwin_$w 120 env SLIME_RS_OBJ_WINDOW_MIB=$w tools/latency_c 100 || exit 1; done ;;
