@@ -869,6 +869,37 @@ def test_write_chunks_and_reconstruct_vs_oracle(need, total, S, kind):
         _oracle_reconstruct([chunks[i] for i in have], have, m, need, S)
 
 
+@pytest.mark.parametrize("need,total", [(8, 12), (10, 14), (3, 5)])
+@pytest.mark.parametrize("S", [(2 << 20) + 1, (4 << 20) - 3, (4 << 20) + 5, (6 << 20) + 7])
+@pytest.mark.parametrize("kind", ["plain", "high"])
+def test_host_windows_either_side_of_the_copy_kernel_threshold(need, total, S, kind):
+    """A window moving <= 4 MiB each way crosses PCIe as one copy kernel over
+    the pinned ring (host_blit.hip), a larger one through the copy engines
+    (rs_capi.cpp dma_spans): objects on both sides of that line, odd sizes
+    (4-byte-aligned but not 16-byte-aligned chunk offsets, a partial last
+    word), one-window 1<<31 objects (the host sees the flags and the device
+    re-encodes), and the Go-API rows at L on both sides."""
+    from slime_amd import objects
+    rng = np.random.default_rng(S + need)
+    obj = _obj_bytes(rng, S, kind)
+    m, chunks = objects.write_chunks(obj, need, total)
+    m_ref, want = _oracle_chunks(obj, need, total, [])
+    assert m == m_ref == (1 << 31 if kind == "high" else m)
+    assert [c.tobytes() for c in chunks] == want
+    have = sorted(rng.choice(total, size=need, replace=False).tolist())
+    got = objects.reconstruct([chunks[i] for i in have], have, m, S)
+    assert got.tobytes() == obj
+    if kind == "plain":  # the rows path at the same L (CreateParity / RecoverData)
+        L = len(chunks[0]) // 4
+        data = [np.frombuffer(chunks[j], dtype=">u4").astype(np.uint32) for j in range(need)]
+        for idx in (need, total - 1):
+            assert np.array_equal(rs.CreateParity(data, idx), OC.create_parity(data, idx)[1])
+        code = data + [OC.create_parity(data, need + i)[1] for i in range(total - need)]
+        rec = rs.RecoverData([code[i] for i in have], have)
+        for g, d in zip(rec, data):
+            assert g.size == L and np.array_equal(g, d)
+
+
 def test_reconstruct_every_pattern_4_6():
     from slime_amd import objects
     rng = np.random.default_rng(46)

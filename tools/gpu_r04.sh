@@ -216,6 +216,7 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    tests_blit) run pytest_blit 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -k "copy_kernel_threshold or write_chunks_and_reconstruct" ;;
     concc) for t in 1 2 4 8 16; do run concc_$t 120 tools/latency_c 400 $t || exit 1; done ;;
     concsmall) run conc4k 200 python tools/host_concurrency.py --kib 4 --reps 300 --delay 0 --threads 1,2,4,8,16 &&
                run conc64k 200 python tools/host_concurrency.py --kib 64 --reps 200 --delay 0 --threads 1,2,4,8,16 ;;
