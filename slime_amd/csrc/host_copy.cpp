@@ -20,8 +20,21 @@
 namespace slime {
 namespace {
 
-constexpr size_t kPiece = 512u << 10;  // bytes per work piece
-constexpr size_t kSerialBelow = 2u << 20;  // small copies: not worth a wake-up
+// Work pieces of 64..512 KiB, about four per thread; copies below 512 KiB
+// stay on the caller (a host window's outputs of ~1 MiB were copied by the
+// caller alone at ~18 GB/s: half of a CreateParity call's host time,
+// profiles/r04/s16_cptrace).
+constexpr size_t kPieceMax = 512u << 10, kPieceMin = 64u << 10;
+// Small copies stay on the caller (not worth a wake-up); env
+// SLIME_RS_COPY_SERIAL_KIB, read once.
+size_t serial_below() {
+  static const size_t b = [] {
+    const char* e = getenv("SLIME_RS_COPY_SERIAL_KIB");
+    const long v = e ? atol(e) : 512;
+    return (size_t)(v < 0 ? 0 : v) << 10;
+  }();
+  return b;
+}
 // After a job a worker spins this long for the next one before it sleeps.
 // A host call posts one job per window (8-16 MiB, a fraction of a ms of
 // copying); a worker that went to sleep between windows can take longer to
@@ -232,18 +245,19 @@ void parallel_pieces(size_t n, void (*fn)(const void* ctx, size_t piece), const 
 void parallel_copy(const CopyItem* items, size_t n) {
   size_t total = 0;
   for (size_t i = 0; i < n; ++i) total += items[i].bytes;
-  if (total < kSerialBelow) {
+  if (total < serial_below()) {
     for (size_t i = 0; i < n; ++i)
       if (items[i].bytes) memcpy(items[i].dst, items[i].src, items[i].bytes);
     return;
   }
+  const size_t piece = std::min(kPieceMax, std::max(kPieceMin, total / (4 * (size_t)(copy_pool_threads() + 1))));
   std::vector<CopyItem> pieces;
-  pieces.reserve(total / kPiece + n);
+  pieces.reserve(total / piece + n);
   for (size_t i = 0; i < n; ++i) {
     char* d = (char*)items[i].dst;
     const char* s = (const char*)items[i].src;
-    for (size_t off = 0; off < items[i].bytes; off += kPiece)
-      pieces.push_back({d + off, s + off, std::min(kPiece, items[i].bytes - off)});
+    for (size_t off = 0; off < items[i].bytes; off += piece)
+      pieces.push_back({d + off, s + off, std::min(piece, items[i].bytes - off)});
   }
   parallel_pieces(
       pieces.size(), [](const void* ctx, size_t i) { copy_piece(((const CopyItem*)ctx)[i]); }, pieces.data());

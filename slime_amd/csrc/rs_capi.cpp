@@ -627,37 +627,58 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   std::vector<Window> win(S);
   std::vector<CopyItem> items;
   auto pin_of = [&](int s) { return ws->pin + (size_t)s * stage_bytes; };
-  auto land = [&](int s) -> int {
-    auto t0 = clk::now();
+  auto wait_stage = [&](int s) -> int {
+    const auto t0 = clk::now();
     HIP_TRY(hipEventSynchronize(ws->sev[s]));
     t_wait += ms_since(t0);
-    t0 = clk::now();
+    return 0;
+  };
+  auto add_out_items = [&](int s) {  // stage s's landed outputs -> the caller's buffers
     const Window& w = win[s];
-    items.clear();
     for (size_t i = 0; i < w.out.size(); ++i) items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
+  };
+  auto land = [&](int s) -> int {
+    if (int rc = wait_stage(s)) return rc;
+    const auto t0 = clk::now();
+    items.clear();
+    add_out_items(s);
     parallel_copy(items.data(), items.size());
     t_out += ms_since(t0);
-    landed(w.index);
+    landed(win[s].index);
     return 0;
   };
   auto body = [&]() -> int {
     for (uint64_t c = 0; c < n; ++c) {
       const int s = (int)(c % S);
-      if (c >= (uint64_t)S)
-        if (int rc = land(s)) return rc;
+      // Window c reuses stage s of window c - S: once that window's DMA is
+      // done, its outputs leave the pinned stage in the same pool job as
+      // window c's inputs arrive (two regions of the stage: c's inputs end
+      // where c - S's did or earlier, and its outputs follow its inputs).
       Window& w = win[s];
+      items.clear();
+      bool prev = false;
+      uint64_t prev_index = 0;
+      size_t prev_out_start = 0;
+      if (c >= (uint64_t)S) {
+        if (int rc = wait_stage(s)) return rc;
+        prev = true;
+        prev_index = w.index;
+        prev_out_start = w.out.empty() ? stage_bytes : w.out_off[0];
+        add_out_items(s);
+      }
+      const size_t nprev = items.size();
       w.index = c;
       w.in.clear(), w.out.clear(), w.host.clear();
       io(c, s, w);
       uint8_t* const pin = pin_of(s);
       size_t off = 0;
-      items.clear();
       w.in_off.resize(w.in.size());
       for (size_t i = 0; i < w.in.size(); ++i) {
         w.in_off[i] = off;
         items.push_back({pin + off, w.in[i].host, w.in[i].bytes});
         off = round64(off + w.in[i].bytes);
       }
+      const size_t in_end = off;
       w.out_off.resize(w.out.size());
       for (size_t i = 0; i < w.out.size(); ++i) {
         w.out_off[i] = off;
@@ -666,8 +687,14 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       if (off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
       items.insert(items.end(), w.host.begin(), w.host.end());
       auto t0 = clk::now();
-      parallel_copy(items.data(), items.size());
+      if (prev && in_end > prev_out_start) {  // the regions would overlap: outputs first, then inputs
+        parallel_copy(items.data(), nprev);
+        parallel_copy(items.data() + nprev, items.size() - nprev);
+      } else {
+        parallel_copy(items.data(), items.size());
+      }
       t_in += ms_since(t0);
+      if (prev) landed(prev_index);
       t0 = clk::now();
       hipStream_t st = ws->sst[s];
       if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;

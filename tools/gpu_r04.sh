@@ -216,6 +216,11 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    serialab) for rep in 1 2; do for v in 512 2048; do run serialab_${v}_$rep 200 env SLIME_RS_COPY_SERIAL_KIB=$v tools/latency_c 200 &&
+                run cp_serial_${v}_$rep 200 env SLIME_RS_COPY_SERIAL_KIB=$v python tools/cp_trace.py || exit 1; done; done ;;
+    cptrace) run cptrace 200 env SLIME_RS_PIPE_TRACE=1 python tools/cp_trace.py &&
+             run cptrace_st4 200 env SLIME_RS_HOST_STAGES=4 python tools/cp_trace.py &&
+             run cptrace_t0 200 env SLIME_RS_COPY_THREADS=0 python tools/cp_trace.py ;;
     tests_blit) run pytest_blit 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -k "copy_kernel_threshold or write_chunks_and_reconstruct" ;;
     concc) for t in 1 2 4 8 16; do run concc_$t 120 tools/latency_c 400 $t || exit 1; done ;;
     concsmall) run conc4k 200 python tools/host_concurrency.py --kib 4 --reps 300 --delay 0 --threads 1,2,4,8,16 &&
