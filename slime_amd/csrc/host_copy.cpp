@@ -20,17 +20,16 @@
 namespace slime {
 namespace {
 
-// Work pieces of 64..512 KiB, about four per thread; copies below 512 KiB
-// stay on the caller (a host window's outputs of ~1 MiB were copied by the
-// caller alone at ~18 GB/s: half of a CreateParity call's host time,
-// profiles/r04/s16_cptrace).
+// Work pieces of 64..512 KiB, about four per thread (a fixed 512 KiB left
+// most of the pool idle on a window's ~1 MiB of outputs).
 constexpr size_t kPieceMax = 512u << 10, kPieceMin = 64u << 10;
-// Small copies stay on the caller (not worth a wake-up); env
-// SLIME_RS_COPY_SERIAL_KIB, read once.
+// Copies below 2 MiB stay on the caller: a wake-up costs more than it saves
+// there (1 MiB host calls ran 10-20% slower with a 512 KiB threshold,
+// profiles/r04/s18_serialab).  Env SLIME_RS_COPY_SERIAL_KIB, read once.
 size_t serial_below() {
   static const size_t b = [] {
     const char* e = getenv("SLIME_RS_COPY_SERIAL_KIB");
-    const long v = e ? atol(e) : 512;
+    const long v = e ? atol(e) : 2048;
     return (size_t)(v < 0 ? 0 : v) << 10;
   }();
   return b;
