@@ -532,21 +532,29 @@ bool dma_2d() {
 
 // Windows moving at most this many bytes one way go as one copy kernel over
 // the mapped pinned ring instead of copy-engine transfers (host_blit.hip):
-// env SLIME_RS_BLIT_KIB, default 4096; 0 = always the copy engines.
-uint64_t blit_max_bytes() {
-  static const uint64_t b = [] {
-    const char* e = getenv("SLIME_RS_BLIT_KIB");
-    const long long v = e ? atoll(e) : 4096;
-    return v > 0 ? (uint64_t)v << 10 : 0ull;
-  }();
-  return b;
+// uploads up to 4 MiB (env SLIME_RS_BLIT_KIB; a kernel reading host memory
+// is latency-bound, so larger uploads keep the copy engines: a 64 MiB
+// CreateParity ran 1.88 ms instead of 1.41 with kernel uploads), downloads
+// of every window size (env SLIME_RS_BLIT_D2H_KIB, default 64 MiB: the
+// kernel's writes are posted and run beside the copy engines' uploads --
+// fused reconstruct +4-7%, write_chunks +3-10%, profiles/r04/s19-s20).  0 =
+// always the copy engines.
+uint64_t env_kib(const char* name, long long dflt) {
+  const char* e = getenv(name);
+  const long long v = e ? atoll(e) : dflt;
+  return v > 0 ? (uint64_t)v << 10 : 0ull;
+}
+uint64_t blit_max_bytes(bool h2d) {
+  static const uint64_t up = env_kib("SLIME_RS_BLIT_KIB", 4096);
+  static const uint64_t down = env_kib("SLIME_RS_BLIT_D2H_KIB", 65536);
+  return h2d ? up : down;
 }
 
 int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
               hipStream_t st) {
   uint64_t total = 0;
   for (const Span& s : sp) total += s.bytes;
-  if (total && total <= blit_max_bytes()) {
+  if (total && total <= blit_max_bytes(h2d)) {
     std::vector<BlitSpan> bl;
     bl.reserve(sp.size());
     for (size_t i = 0; i < sp.size();) {  // neighbours contiguous on both sides merge, as below
