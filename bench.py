@@ -560,9 +560,15 @@ def latency_leg(need, total, erase, sizes_kib=(4, 64, 1024, 8192), reps=25) -> d
     """Per-call latency from host memory at request-body sizes (a proxy serves
     objects of every size, main.go:107-109): median and p90 microseconds of the
     fused write_chunks / reconstruct and of the unchanged Go API's
-    CreateParity (one row) / RecoverData, caller-reused outputs."""
+    CreateParity (one row) / RecoverData, caller-reused outputs.  `c_abi`
+    calls the C entry points with their argument arrays built once, as the cgo
+    shim holds them (what a Go caller waits); `python` goes through the Python
+    mirror (slime_amd.objects / rs), whose argument marshalling adds ~15 us."""
+    import ctypes
     import numpy as np
+    from slime_amd import _native as N
     from slime_amd import gf, objects, rs
+    lib = N.lib
     have = [i for i in range(total) if i not in erase][:need]
     pc = time.perf_counter
 
@@ -576,31 +582,58 @@ def latency_leg(need, total, erase, sizes_kib=(4, 64, 1024, 8192), reps=25) -> d
         ts.sort()
         return {"p50_us": round(ts[len(ts) // 2] * 1e6, 1), "p90_us": round(ts[(9 * len(ts)) // 10] * 1e6, 1)}
 
+    def ptrs(arrs):
+        return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+    def checked(rc):
+        if rc:
+            raise RuntimeError(f"latency leg: status {rc}")
+
     rows, ok = [], True
     rng = np.random.default_rng(0x1A7)
     for kib in sizes_kib:
         data = rng.integers(0, 256, size=kib << 10, dtype=np.uint8)
-        cb = objects.chunk_size(data.size, need)
+        S = data.size
+        cb = objects.chunk_size(S, need)
         chunks = [np.zeros(cb, dtype=np.uint8) for _ in range(total)]
-        out = np.zeros(data.size, dtype=np.uint8)
+        out = np.zeros(S, dtype=np.uint8)
+        m_box = ctypes.c_uint32(0)
+        # C-ABI, arguments prepared once (a cgo caller's marshalled slices)
+        p_data, p_chunks, p_out = data.ctypes.data, ptrs(chunks), out.ctypes.data
+        surv = [chunks[i] for i in have]
+        p_surv, p_have = ptrs(surv), (ctypes.c_int * need)(*have)
+        c_w = stats(lambda: checked(lib.slime_rs_write_chunks(p_data, S, need, total, p_chunks, ctypes.byref(m_box))))
+        m = int(m_box.value)
+        c_r = stats(lambda: checked(lib.slime_rs_reconstruct(p_surv, p_have, need, cb, m, S, p_out)))
+        ok = ok and bool(np.array_equal(out, data))
+        mm, words = gf.MapToGF(data)
+        parts = objects.split_vector(words, need)
+        L = parts[0].size
+        par = np.zeros(L, dtype=np.uint32)
+        p_parts, lens = ptrs(parts), (ctypes.c_uint64 * need)(*([L] * need))
+        c_cp = stats(lambda: checked(lib.slime_rs_create_parity(p_parts, lens, need, need, par.ctypes.data)))
+        sym = [gf.MapToGFWith(chunks[i], m) for i in have]
+        rec = [np.zeros(L, dtype=np.uint32) for _ in range(need)]
+        p_sym, p_rec = ptrs(sym), ptrs(rec)
+        c_rd = stats(lambda: checked(lib.slime_rs_recover_data(p_sym, lens, need, p_have, need, p_rec)))
+        ok = ok and all(np.array_equal(rec[i], parts[i]) for i in range(need))
+        # the Python mirror, call by call
         box = {}
         w = stats(lambda: box.update(m=objects.write_chunks(data, need, total, out=chunks)[0]))
-        surv = [chunks[i] for i in have]
-        rc = stats(lambda: objects.reconstruct(surv, have, box["m"], data.size, out=out))
-        ok = ok and bool(np.array_equal(out, data))
-        m, words = gf.MapToGF(data)
-        parts = objects.split_vector(words, need)
-        par = np.zeros(parts[0].size, dtype=np.uint32)
+        rc = stats(lambda: objects.reconstruct(surv, have, box["m"], S, out=out))
+        ok = ok and bool(np.array_equal(out, data)) and mm == m == box["m"]
         cp = stats(lambda: rs.CreateParity(parts, need, par))
-        sym = [gf.MapToGFWith(chunks[i], m) for i in have]
-        rec = [np.zeros(sym[0].size, dtype=np.uint32) for _ in range(need)]
         rd = stats(lambda: rs.RecoverData(sym, have, rec))
         ok = ok and all(np.array_equal(rec[i], parts[i]) for i in range(need))
-        rows.append({"object_kib": kib, "write_chunks": w, "reconstruct": rc, "create_parity_one_row": cp,
-                     "recover_data": rd})
+        rows.append({"object_kib": kib,
+                     "c_abi": {"write_chunks": c_w, "reconstruct": c_r, "create_parity_one_row": c_cp,
+                               "recover_data": c_rd},
+                     "python": {"write_chunks": w, "reconstruct": rc, "create_parity_one_row": cp,
+                                "recover_data": rd}})
     return {"sizes": rows, "reps": reps, "erased": erase, "verified": ok,
             "what": "wall time per host call (host bytes in, host bytes out, PCIe and launch included), "
-                    "median and 90th percentile"}
+                    "median and 90th percentile; c_abi: the C entry points with argument arrays built once "
+                    "(the cgo shim's view); python: the Python mirror"}
 
 
 def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
