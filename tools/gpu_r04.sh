@@ -216,6 +216,8 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    hugeab) HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
+            for rep in 1 2; do run hugeab_on_$rep 200 python bench.py $HA && run hugeab_off_$rep 200 env SLIME_RS_CODEC_HUGEPAGE=0 python bench.py $HA || exit 1; done ;;
     blitbig) for rep in 1 2; do for v in 4096 65536; do run blitbig_${v}_$rep 200 env SLIME_RS_BLIT_D2H_KIB=$v python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 &&
                run blitcp_${v}_$rep 200 env SLIME_RS_BLIT_D2H_KIB=$v python tools/cp_trace.py || exit 1; done; done ;;
     serialab) for rep in 1 2; do for v in 512 2048; do run serialab_${v}_$rep 200 env SLIME_RS_COPY_SERIAL_KIB=$v tools/latency_c 200 &&
