@@ -521,11 +521,16 @@ size_t round64(size_t n) { return (n + 63) & ~(size_t)63; }
 
 // DMA spans one by one, merging neighbours contiguous on both sides.
 // Runs of equal-length spans at constant device and pinned strides (a
-// window's rows: one per chunk) go as one pitched copy when SLIME_RS_DMA_2D=1.
+// window's rows: one per chunk) go as one pitched copy (env SLIME_RS_DMA_2D=0:
+// a copy per span).  Per-span copies reach the copy engine as separate
+// commands ~10 us apart: a 64 MiB reconstruct's eight 1 MiB uploads per
+// window ran back to back with those gaps, and one pitched copy took the
+// fused reconstruct from 22 to 27 GiB/s and write_chunks from 32 to 36
+// (profiles/r04/s24_rctrace, s25_dma2d).
 bool dma_2d() {
   static const bool on = [] {
     const char* e = getenv("SLIME_RS_DMA_2D");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }

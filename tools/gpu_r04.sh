@@ -216,6 +216,11 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    dma2dab) sleep 20; HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
+             for rep in 1 2; do run rc2d_off_$rep 120 python tools/rc_trace.py && run rc2d_on_$rep 120 env SLIME_RS_DMA_2D=1 python tools/rc_trace.py &&
+               run host2d_off_$rep 200 python bench.py $HA && run host2d_on_$rep 200 env SLIME_RS_DMA_2D=1 python bench.py $HA || exit 1; done ;;
+    rctrace) run rctrace 200 env SLIME_RS_PIPE_TRACE=1 python tools/rc_trace.py &&
+             run rcprof 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/rcprof" -o rc --output-format csv -- python3 tools/rc_trace.py ;;
     hugeab) HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
             for rep in 1 2; do run hugeab_on_$rep 200 python bench.py $HA && run hugeab_off_$rep 200 env SLIME_RS_CODEC_HUGEPAGE=0 python bench.py $HA || exit 1; done ;;
     blitbig) for rep in 1 2; do for v in 4096 65536; do run blitbig_${v}_$rep 200 env SLIME_RS_BLIT_D2H_KIB=$v python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 &&
