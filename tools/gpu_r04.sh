@@ -216,6 +216,8 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    thrab) sleep 20; HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
+           for rep in 1 2; do for t in 8 12 15; do run thr_${t}_$rep 200 env SLIME_RS_COPY_THREADS=$t python bench.py $HA || exit 1; done; done ;;
     dma2dab) sleep 20; HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
              for rep in 1 2; do run rc2d_off_$rep 120 python tools/rc_trace.py && run rc2d_on_$rep 120 env SLIME_RS_DMA_2D=1 python tools/rc_trace.py &&
                run host2d_off_$rep 200 python bench.py $HA && run host2d_on_$rep 200 env SLIME_RS_DMA_2D=1 python bench.py $HA || exit 1; done ;;
