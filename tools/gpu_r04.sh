@@ -239,7 +239,7 @@ for step in "$@"; do
     concc) for t in 1 2 4 8 16; do run concc_$t 120 tools/latency_c 400 $t || exit 1; done ;;
     concsmall) run conc4k 200 python tools/host_concurrency.py --kib 4 --reps 300 --delay 0 --threads 1,2,4,8,16 &&
                run conc64k 200 python tools/host_concurrency.py --kib 64 --reps 200 --delay 0 --threads 1,2,4,8,16 ;;
-    latwin) for w in 16 4 2; do run latwin_$w 120 env SLIME_RS_OBJ_WINDOW_MIB=$w tools/latency_c 100 || exit 1; done ;;
+    latwin) for rep in 1 2; do for w in 16 4 2; do run latwin_${w}_$rep 120 env SLIME_RS_OBJ_WINDOW_MIB=$w tools/latency_c 100 || exit 1; done; done ;;
     latab) for rep in 1 2; do run latab_blit_$rep 120 tools/latency_c 200 && run latab_sdma_$rep 120 env SLIME_RS_BLIT_KIB=0 tools/latency_c 200 &&
              run latab_rocblit_$rep 120 env SLIME_RS_BLIT_KIB=0 GPU_FORCE_BLIT_COPY_SIZE=4096 tools/latency_c 200 || exit 1; done ;;
     latenv) run latenv_base 120 tools/latency_c 200 && run latenv_blit 120 env GPU_FORCE_BLIT_COPY_SIZE=4096 tools/latency_c 200 &&
