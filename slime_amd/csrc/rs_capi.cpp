@@ -508,7 +508,8 @@ void drain_stages(Workspace* ws) {
 // caller when stage s is needed again (or at the end), so the host copies of
 // one window overlap the DMA and kernels of the others, and the H2D of one
 // window overlaps the D2H of another.  Windows may also carry host-to-host
-// copies (write_chunks' data-chunk bodies), done with the window's inputs.
+// copies (write_chunks' data-chunk bodies), done once the window is queued,
+// while its upload and kernel run.
 
 struct Window {
   uint64_t index = 0;  // window number c
@@ -698,7 +699,6 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
         off = round64(off + w.out[i].bytes);
       }
       if (off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
-      items.insert(items.end(), w.host.begin(), w.host.end());
       auto t0 = clk::now();
       if (prev && in_end > prev_out_start) {  // the regions would overlap: outputs first, then inputs
         parallel_copy(items.data(), nprev);
@@ -719,6 +719,13 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       t_enq += ms_since(t0);
       t_h2d += a;
       t_launch += b - a;
+      // Host-to-host copies (write_chunks' data-chunk bodies) are not needed
+      // on the device: they run while the window's upload and kernel do.
+      if (!w.host.empty()) {
+        t0 = clk::now();
+        parallel_copy(w.host.data(), w.host.size());
+        t_in += ms_since(t0);
+      }
     }
     for (uint64_t c = n > (uint64_t)S ? n - S : 0; c < n; ++c)
       if (int rc = land((int)(c % S))) return rc;

@@ -216,6 +216,7 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    latc2) for rep in 1 2; do run latc2_$rep 200 tools/latency_c 200 || exit 1; done ;;
     c2seg) for rep in 1 2; do for sg in 0 4 8 16; do
              if [ $sg = 0 ]; then run c2seg_${sg}_$rep 200 python bench.py --preset c2 --steps 20 --warmup 3 --bytes-path 0 $NOLEGS || exit 1;
              else run c2seg_${sg}_$rep 200 env SLIME_RS_SEGMENTS=$sg python bench.py --preset c2 --steps 20 --warmup 3 --bytes-path 0 $NOLEGS || exit 1; fi; done; done ;;
