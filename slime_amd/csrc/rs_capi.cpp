@@ -308,6 +308,8 @@ struct Workspace {
   size_t dcap = 0;
   hipStream_t sst[kMaxStages] = {};  // one stream per pipeline stage
   hipEvent_t sev[kMaxStages] = {};   // stage's D2H done
+  static constexpr int kParts = 4;
+  hipEvent_t pev[kMaxStages][kParts] = {};  // a part of the stage's D2H done (run_windows)
   hipEvent_t cev = nullptr;          // compute stream reached a point (staged_d2h)
   uint8_t* pin = nullptr;            // pinned staging, host_stages() x (in rows | out rows)
   size_t pcap = 0;
@@ -353,6 +355,7 @@ struct Workspace {
     for (int i = 0; i < kMaxStages; ++i) {
       HIP_TRY(hipStreamCreateWithFlags(&sst[i], hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming));
+      for (int p = 0; p < kParts; ++p) HIP_TRY(hipEventCreateWithFlags(&pev[i][p], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&cev, hipEventDisableTiming));
     return 0;
@@ -516,7 +519,23 @@ struct Window {
   std::vector<Span> in, out;
   std::vector<CopyItem> host;
   std::vector<size_t> in_off, out_off;  // offsets in the stage's pinned buffer
+  std::vector<size_t> part_end;         // out spans [part_end[p-1], part_end[p]) are D2H part p
 };
+
+// A one-window call's download of at least this many bytes goes as up to
+// Workspace::kParts parts, each with its own event, so the host copies part
+// p out of the ring while part p+1 still crosses PCIe (8 MiB reconstruct
+// 496-522 -> 453-486 us, profiles/r04/s34_parts; env SLIME_RS_D2H_PARTS:
+// parts, 1 = one download).
+int d2h_parts() {
+  static const int p = [] {
+    const char* e = getenv("SLIME_RS_D2H_PARTS");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : v > 4 ? 4 : v;
+  }();
+  return p;
+}
+constexpr uint64_t kPartedD2H = 8u << 20;
 
 size_t round64(size_t n) { return (n + 63) & ~(size_t)63; }
 
@@ -652,13 +671,32 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
     for (size_t i = 0; i < w.out.size(); ++i) items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
   };
   auto land = [&](int s) -> int {
+    const Window& w = win[s];
+    if (w.part_end.size() > 1) {  // part by part, as each part's download completes
+      size_t i0 = 0;
+      for (size_t p = 0; p < w.part_end.size(); ++p) {
+        auto t0 = clk::now();
+        HIP_TRY(hipEventSynchronize(ws->pev[s][p]));
+        t_wait += ms_since(t0);
+        t0 = clk::now();
+        items.clear();
+        for (size_t i = i0; i < w.part_end[p]; ++i)
+          items.push_back({w.out[i].host, pin_of(s) + w.out_off[i], w.out[i].bytes});
+        parallel_copy(items.data(), items.size());
+        t_out += ms_since(t0);
+        i0 = w.part_end[p];
+      }
+      if (int rc = wait_stage(s)) return rc;  // the stage's own event, recorded after the last part
+      landed(w.index);
+      return 0;
+    }
     if (int rc = wait_stage(s)) return rc;
     const auto t0 = clk::now();
     items.clear();
     add_out_items(s);
     parallel_copy(items.data(), items.size());
     t_out += ms_since(t0);
-    landed(win[s].index);
+    landed(w.index);
     return 0;
   };
   auto body = [&]() -> int {
@@ -714,7 +752,27 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       const double a = ms_since(t0);
       if (int rc = launch(c, s, st)) return rc;
       const double b = ms_since(t0);
-      if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) return rc;
+      uint64_t out_bytes = 0;
+      for (const Span& o : w.out) out_bytes += o.bytes;
+      // Only a call of one window lands every window alone; in longer calls
+      // the parts measured no better (64 MiB reconstruct 26.2 vs 27.8 GiB/s).
+      const size_t parts = n == 1 && out_bytes >= kPartedD2H ? std::min<size_t>(d2h_parts(), w.out.size()) : 1;
+      w.part_end.clear();
+      if (parts > 1) {
+        std::vector<Span> psp;
+        std::vector<size_t> poff;
+        for (size_t p = 0, r0 = 0; p < parts; ++p) {
+          const size_t r1 = w.out.size() * (p + 1) / parts;
+          psp.assign(w.out.begin() + r0, w.out.begin() + r1);
+          poff.assign(w.out_off.begin() + r0, w.out_off.begin() + r1);
+          if (int rc = dma_spans(dev, pin, psp, poff, false, st)) return rc;
+          HIP_TRY(hipEventRecord(ws->pev[s][p], st));
+          w.part_end.push_back(r1);
+          r0 = r1;
+        }
+      } else if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) {
+        return rc;
+      }
       HIP_TRY(hipEventRecord(ws->sev[s], st));
       t_enq += ms_since(t0);
       t_h2d += a;

@@ -216,6 +216,9 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    partsab) HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
+             for rep in 1 2; do for v in 4 1; do run parts_lat_${v}_$rep 200 env SLIME_RS_D2H_PARTS=$v tools/latency_c 200 &&
+               run parts_host_${v}_$rep 200 env SLIME_RS_D2H_PARTS=$v python bench.py $HA || exit 1; done; done ;;
     latc2) for rep in 1 2; do run latc2_$rep 200 tools/latency_c 200 || exit 1; done ;;
     c2seg) for rep in 1 2; do for sg in 0 4 8 16; do
              if [ $sg = 0 ]; then run c2seg_${sg}_$rep 200 python bench.py --preset c2 --steps 20 --warmup 3 --bytes-path 0 $NOLEGS || exit 1;
