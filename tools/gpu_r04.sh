@@ -216,6 +216,8 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    spinab) for rep in 1 2; do for v in 200 0; do run spin_lat_${v}_$rep 200 env SLIME_RS_SPIN_US=$v tools/latency_c 200 &&
+              run spin_conc_${v}_$rep 200 env SLIME_RS_SPIN_US=$v tools/latency_c 300 8 || exit 1; done; done ;;
     upgab) HA="--objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0"
            for rep in 1 2; do for v in 1 0; do run upg_lat_${v}_$rep 200 env SLIME_RS_UP_GROUPS=$v tools/latency_c 200 &&
              run upg_host_${v}_$rep 200 env SLIME_RS_UP_GROUPS=$v python bench.py $HA || exit 1; done; done ;;
