@@ -323,10 +323,30 @@ def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[in
     allc = _cpu_leg(OC, sample, need, total, have, ncores, seconds * 0.6)
     allc.pop("_first")
     mib = sample.shape[1] * need * 4 / (1 << 20)
+    # Small objects (a proxy's small requests): the same per-object path on one
+    # thread, per call, on the first columns of the sample (the shards of an
+    # S-byte object), beside host_path.latency's GPU calls.
+    small = []
+    for kib in (4, 64, 1024):
+        Ls = -(-(kib << 10) // 4 // need)
+        o = np.ascontiguousarray(sample[:, :Ls])
+        OC.object_reps(o, need, total, have, 1)  # warm
+        reps = max(1, int(0.2 / max(1e-6, Ls * need * (total - need + need) * 2e-9)))
+        t0 = time.perf_counter()
+        rec = OC.object_reps(o, need, total, have, reps)
+        dt = time.perf_counter() - t0
+        ok = ok and all(np.array_equal(rec[t], sample[t, :Ls]) for t in range(need))
+        small.append({"object_kib": kib, "encode_plus_recover_us": round(dt / reps * 1e6, 2), "calls": reps})
     return {"value": allc["value"], "unit": "GiB/s", "cores": ncores, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": affinity,
             "cgroup_cpu_quota": quota, "verified": ok,
             "single_thread": one, "all_cores": allc,
+            "small_objects_one_thread": {"sizes": small,
+                                         "what": "per object, in C with the reference's matrix cache: r "
+                                                 "one-row CreateParity calls + RecoverData (inverse per call), "
+                                                 "1 thread -- the RS math only (the reference also runs MapToGF / "
+                                                 "MapFromGF byte passes); compare host_path.latency (GPU, bytes "
+                                                 "in and out)"},
             "sample": f"{sample_name} ({mib:.0f} MiB of data shards, copied from HBM after the timed steps), "
                       f"need={need} total={total}: per object, r CreateParity passes (multi_store.go:528-531) + "
                       f"RecoverData(erase {erase}) recomputing all need rows (vector.go:80-85); 1 thread "

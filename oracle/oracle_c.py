@@ -36,6 +36,7 @@ def _load():
         "oracle_map_from_gf": (None, [ctypes.c_uint32, V, ctypes.c_uint64, V]),
         "oracle_split_vector": (ctypes.c_uint64, [V, ctypes.c_uint64, ctypes.c_int, V]),
         "oracle_encode_object": (ctypes.c_int, [V, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]),
+        "oracle_object_reps": (ctypes.c_int, [V, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, V, V, ctypes.c_int]),
         "oracle_fnv1a64": (ctypes.c_uint64, [ctypes.c_uint64, V, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
@@ -137,6 +138,19 @@ def encode_object(shards: np.ndarray, need: int, total: int) -> None:
     assert shards.flags.c_contiguous and shards.dtype == np.uint32
     rc = lib.oracle_encode_object(shards.ctypes.data, need, total, shards.shape[1])
     assert rc == 0, rc
+
+
+def object_reps(shards: np.ndarray, need: int, total: int, have, reps: int) -> list[np.ndarray]:
+    """`reps` times the reference's per-object path with its matrix cache
+    (r one-row CreateParity calls + one RecoverData), in C: the CPU baseline's
+    per-call timing.  Returns the last RecoverData's rows."""
+    assert shards.flags.c_contiguous and shards.dtype == np.uint32
+    L = shards.shape[1]
+    scratch = np.zeros((need, L), dtype=np.uint32)
+    hv = (ctypes.c_int * need)(*have)
+    rc = lib.oracle_object_reps(shards.ctypes.data, need, total, L, hv, scratch.ctypes.data, reps)
+    assert rc == 0, rc
+    return [scratch[t] for t in range(need)]
 
 
 FNV64_OFFSET = 14695981039346656037

@@ -261,6 +261,44 @@ int oracle_encode_object(uint32_t *shards, int need, int total, uint64_t L) {
     return OR_OK;
 }
 
+/*
+ * Per-object timing loop for the CPU baseline's small objects (bench.py):
+ * `reps` times the reference's per-object path with its matrix cache
+ * (ParityMatrixCached, matrixcache.go:7-29, built once here): r CreateParity
+ * calls of one row each (vector.go:18-41) and one RecoverData over the
+ * survivors `have` (vector.go:50-88: the inverse built per call, all k rows
+ * recomputed).  shards [total][L]; the recovered rows go to scratch [need][L].
+ */
+int oracle_object_reps(uint32_t *shards, int need, int total, uint64_t L, const int *have, uint32_t *scratch,
+                       int reps) {
+    const int r = total - need;
+    if (need > 128 || total > 256) return -1;
+    uint32_t *m = (uint32_t *)malloc((size_t)total * need * sizeof(uint32_t));
+    uint32_t *hv = (uint32_t *)malloc((size_t)need * need * sizeof(uint32_t));
+    uint32_t *inv = (uint32_t *)malloc((size_t)need * need * sizeof(uint32_t));
+    int st = (m && hv && inv) ? oracle_parity_matrix(need, r, m) : -1;
+    const uint32_t *data[128], *surv[128];
+    uint32_t *out[128];
+    for (int j = 0; j < need; j++) {
+        data[j] = shards + (uint64_t)j * L;
+        surv[j] = shards + (uint64_t)have[j] * L;
+        out[j] = scratch + (uint64_t)j * L;
+    }
+    for (int rep = 0; st == OR_OK && rep < reps; rep++) {
+        for (int i = need; i < total; i++) {
+            uint32_t *o = shards + (uint64_t)i * L;
+            oracle_apply_matrix(m + (size_t)i * need, 1, need, data, &o, L);
+        }
+        for (int q = 0; q < need; q++) memcpy(hv + (size_t)q * need, m + (size_t)have[q] * need, need * sizeof(uint32_t));
+        st = oracle_invert_matrix(hv, need, inv);
+        if (st == OR_OK) oracle_apply_matrix(inv, need, need, surv, out, L);
+    }
+    free(m);
+    free(hv);
+    free(inv);
+    return st;
+}
+
 /* Chunk-file header hash of storedir (internal/store/storedir/directory.go:25-28,548-553):
  * fnv.New64a() over SHA-256 ‖ data.  Go's hash/fnv is the published FNV-1a:
  * offset basis 14695981039346656037, prime 1099511628211, h ^= byte then

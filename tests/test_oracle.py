@@ -151,3 +151,21 @@ def test_split_vector_padding():
     data = np.arange(1, 6, dtype=np.uint32)
     parts = OP.split_vector(data, 4)  # multi_store.go:271-299: perVector 2, zero-padded tail
     assert [p.tolist() for p in parts] == [[1, 2], [3, 4], [5, 0], [0, 0]]
+
+
+def test_object_reps_matches_the_per_call_path():
+    """oracle_object_reps (the CPU baseline's small-object timing loop, with the
+    reference's matrix cache) computes what create_parity + recover_data do."""
+    rng = np.random.default_rng(77)
+    need, total, L = 8, 12, 129
+    shards = np.zeros((total, L), dtype=np.uint32)
+    shards[:need] = rng.integers(0, 2**32, size=(need, L), dtype=np.uint64).astype(np.uint32)
+    want = shards.copy()
+    OC.encode_object(want, need, total)
+    have = [1, 4, 5, 6, 8, 9, 10, 11]
+    rec = OC.object_reps(shards, need, total, have, 3)
+    assert np.array_equal(shards[need:], want[need:])
+    rc, ref = OC.recover_data([want[i] for i in have], have)
+    assert rc == 0
+    for a, b in zip(rec, ref):
+        assert np.array_equal(a, b)
