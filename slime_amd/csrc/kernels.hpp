@@ -112,13 +112,6 @@ void schedule_counts(int device, uint64_t* dynamic, uint64_t* fallback);
 // contiguous segments scheduled like separate objects).
 uint32_t object_segments(uint32_t nobj, uint64_t ncols);
 
-// Segments per object of a dynamic-schedule launch (TicketWalk `spread`,
-// rs_apply_kernel.hpp): about 64 segments over the batch, ceil(64 / nobj),
-// capped at the object's groups of 4*C tiles of U 16-byte vectors per lane
-// (in-process sweeps, profiles/r02/s61_spread/, s62_spread2/: best S = 1 at
-// 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
-// Env SLIME_RS_SEGMENTS forces a count (tuning).  0 when the launch has too
-// many units for 32-bit tickets (the caller takes the static kernel).
 // Walk units of a queue launch over nobj objects of ncols columns (4 columns
 // a lane, 64 U lanes a tile, C tiles a unit, `spread` segments an object:
 // TicketWalk's numbering, empty units included).
@@ -140,6 +133,14 @@ inline uint64_t queue_blocks(uint64_t full, uint64_t units) {
   return want < 1 ? 1 : want < full ? want : full;
 }
 
+// Segments per object of a dynamic-schedule launch (TicketWalk `spread`,
+// rs_apply_kernel.hpp): about 64 segments over the batch, ceil(64 / nobj),
+// capped at the object's groups of 4*C tiles of U 16-byte vectors per lane
+// (in-process sweeps, profiles/r02/s61_spread/, s62_spread2/: best S = 1 at
+// 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
+// Env SLIME_RS_SEGMENTS forces a count (tuning).  0 when the launch has too
+// many units for 32-bit tickets, or at most one block's (below): the caller
+// takes the static kernel.
 inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
   const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
   const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
@@ -151,7 +152,18 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
   uint64_t S = forced ? forced : (64 + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
   if (S > groups) S = groups ? groups : 1;
   const uint64_t B = (groups + S - 1) / S;
-  if ((uint64_t)nobj * S * B * 4 >= (1ull << 32)) return 0;
+  const uint64_t units = (uint64_t)nobj * S * B * 4;
+  if (units >= (1ull << 32)) return 0;
+  // A launch of at most one block's units (a host call on a small object)
+  // takes the static kernels: the dynamic schedule has nothing to balance
+  // there, and its set hand-out and ticket atomics are most of such a launch
+  // (env SLIME_RS_TINY_UNITS, default 4; 0 = every launch on the queue).
+  static const uint64_t tiny = [] {
+    const char* e = getenv("SLIME_RS_TINY_UNITS");
+    const long long v = e ? atoll(e) : 4;
+    return v > 0 ? (uint64_t)v : 0ull;
+  }();
+  if (units <= tiny) return 0;
   return (uint32_t)S;
 }
 

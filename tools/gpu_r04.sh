@@ -216,6 +216,7 @@ for step in "$@"; do
             done ;;
     latprobe) run latprobe 200 python tools/latency_probe.py ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    tinyab) for rep in 1 2; do for v in 4 0; do run tiny_lat_${v}_$rep 200 env SLIME_RS_TINY_UNITS=$v tools/latency_c 200 || exit 1; done; done ;;
     altpaths) run alt_copyengines 400 env SLIME_RS_BLIT_KIB=0 SLIME_RS_BLIT_D2H_KIB=0 SLIME_RS_DMA_2D=0 SLIME_RS_D2H_PARTS=1 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct or write_chunks or copy_kernel_threshold" &&
               run alt_allblit 400 env SLIME_RS_BLIT_KIB=65536 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "host or reconstruct or write_chunks or copy_kernel_threshold" ;;
     spinab) for rep in 1 2; do for v in 200 0; do run spin_lat_${v}_$rep 200 env SLIME_RS_SPIN_US=$v tools/latency_c 200 &&
