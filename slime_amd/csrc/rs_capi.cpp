@@ -634,6 +634,20 @@ int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std
   return 0;
 }
 
+// A one-window call whose inputs total at most this many bytes runs its
+// kernel on the mapped pinned stage itself ("direct"): the stage holds the
+// window in the device layout, the kernel reads its inputs and writes its
+// outputs across PCIe, and the two copy kernels around it -- each a dispatch
+// and a PCIe round trip, most of a 4 KiB call -- do not run (env
+// SLIME_RS_DIRECT_KIB, default 256; 0 = never).
+uint64_t direct_max_bytes() {
+  static const uint64_t v = env_kib("SLIME_RS_DIRECT_KIB", 256);
+  return v;
+}
+// Pinned stage of a direct call: at least this much, as the device buffer
+// (Workspace::reserve), so the kernel finds the same room past the layout.
+constexpr size_t kDirectPinned = 1u << 20;
+
 // Process-wide split of host-pipeline time (slime_rs_host_stats): where the
 // host entry points spend their wall time, in microseconds.
 struct HostStats {
@@ -641,13 +655,16 @@ struct HostStats {
 };
 HostStats g_host_stats;
 
-// io(c, s, Window&) fills window c's spans; launch(c, s, stream) enqueues its
-// kernels; landed(c) runs once window c's outputs are in the caller's buffers
-// (windows land in order).  SLIME_RS_PIPE_TRACE=1 prints each call's split of
-// host time to stderr.
+// io(c, s, Window&) fills window c's spans; launch(c, s, stream, base)
+// enqueues its kernels over the window's device layout at `base` (dev, or
+// the pinned stage in a direct call); landed(c) runs once window c's outputs
+// are in the caller's buffers (windows land in order).  direct_bytes: the
+// size of one window's device layout when the caller's kernels may run on
+// the pinned stage (direct_max_bytes), else 0.  SLIME_RS_PIPE_TRACE=1 prints
+// each call's split of host time to stderr.
 template <class Io, class Launch, class Landed>
 int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&& io,
-                Launch&& launch, Landed&& landed) {
+                Launch&& launch, Landed&& landed, size_t direct_bytes = 0) {
   if (n == 0) return 0;
   static const bool trace = getenv("SLIME_RS_PIPE_TRACE") != nullptr;
   using clk = std::chrono::steady_clock;
@@ -655,7 +672,10 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
   const auto t_start = clk::now();
   double t_in = 0, t_wait = 0, t_out = 0, t_enq = 0, t_h2d = 0, t_launch = 0;
   const int S = (int)std::min<uint64_t>(host_stages(), n);
-  if (int rc = ws->reserve_pinned(stage_bytes * S)) return rc;
+  const bool may_direct = n == 1 && direct_bytes && direct_bytes <= 8 * direct_max_bytes();
+  if (int rc = ws->reserve_pinned(may_direct ? std::max(std::max(stage_bytes, direct_bytes), kDirectPinned)
+                                             : stage_bytes * S))
+    return rc;
   if (int rc = ws->ensure_stages()) return rc;
   std::vector<Window> win(S);
   std::vector<CopyItem> items;
@@ -723,20 +743,29 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       w.in.clear(), w.out.clear(), w.host.clear();
       io(c, s, w);
       uint8_t* const pin = pin_of(s);
+      // Direct: every span inside the layout, inputs within the limit; the
+      // stage then holds each span at its device offset.
+      bool direct = may_direct;
+      if (direct) {
+        uint64_t in_bytes = 0;
+        for (const Span& x : w.in) in_bytes += x.bytes, direct &= x.dev_off + x.bytes <= direct_bytes;
+        for (const Span& x : w.out) direct &= x.dev_off + x.bytes <= direct_bytes;
+        direct &= in_bytes <= direct_max_bytes();
+      }
       size_t off = 0;
       w.in_off.resize(w.in.size());
       for (size_t i = 0; i < w.in.size(); ++i) {
-        w.in_off[i] = off;
-        items.push_back({pin + off, w.in[i].host, w.in[i].bytes});
+        w.in_off[i] = direct ? w.in[i].dev_off : off;
+        items.push_back({pin + w.in_off[i], w.in[i].host, w.in[i].bytes});
         off = round64(off + w.in[i].bytes);
       }
       const size_t in_end = off;
       w.out_off.resize(w.out.size());
       for (size_t i = 0; i < w.out.size(); ++i) {
-        w.out_off[i] = off;
+        w.out_off[i] = direct ? w.out[i].dev_off : off;
         off = round64(off + w.out[i].bytes);
       }
-      if (off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
+      if (!direct && off > stage_bytes) return fail(Status::InvalidArg, "window larger than its pinned stage");
       auto t0 = clk::now();
       if (prev && in_end > prev_out_start) {  // the regions would overlap: outputs first, then inputs
         parallel_copy(items.data(), nprev);
@@ -748,9 +777,23 @@ int run_windows(const char* what, Workspace* ws, uint8_t* dev, uint64_t n, size_
       if (prev) landed(prev_index);
       t0 = clk::now();
       hipStream_t st = ws->sst[s];
+      if (direct) {  // the kernel on the stage: no copies across PCIe besides its own accesses
+        if (int rc = launch(c, s, st, pin)) return rc;
+        HIP_TRY(hipEventRecord(ws->sev[s], st));
+        w.part_end.clear();
+        const double e = ms_since(t0);
+        t_enq += e;
+        t_launch += e;
+        if (!w.host.empty()) {
+          t0 = clk::now();
+          parallel_copy(w.host.data(), w.host.size());
+          t_in += ms_since(t0);
+        }
+        continue;
+      }
       if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;
       const double a = ms_since(t0);
-      if (int rc = launch(c, s, st)) return rc;
+      if (int rc = launch(c, s, st, dev)) return rc;
       const double b = ms_since(t0);
       uint64_t out_bytes = 0;
       for (const Span& o : w.out) out_bytes += o.bytes;
@@ -840,11 +883,12 @@ int host_apply_staged(Workspace* ws, const slime_rs_plan* plan, const uint32_t* 
         for (uint64_t j = 0; j < nin; ++j) w.in.push_back({(uint8_t*)(in[j] + c0), base + j * rs * 4, nc * 4});
         for (uint64_t i = 0; i < nout; ++i) w.out.push_back({(uint8_t*)(out[i] + c0), base + (nin + i) * rs * 4, nc * 4});
       },
-      [&](uint64_t c, int s, hipStream_t st) -> int {
+      [&](uint64_t c, int s, hipStream_t st, uint8_t* base) -> int {
         const uint64_t nc = std::min(cl, L - c * cl);
-        const uint32_t* di = (const uint32_t*)(dev + (size_t)s * stage_dev);
+        const uint32_t* di = (const uint32_t*)(base + (size_t)s * stage_dev);
         return execute(plan, di, 0, rs, (uint32_t*)di + nin * rs, 0, rs, nc, 1, st);
-      });
+      },
+      [](uint64_t) {}, stage_dev);
 }
 
 // Register mode: page-lock the caller's rows for the duration of the call
@@ -1779,12 +1823,10 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
   const bool one = nwin == 1;
   uint32_t ms[2] = {0, 0};
   static const uint32_t kZero[2] = {0, 0};
-  auto body = [&]() -> int {
-    if (!one) {  // the flags start at zero for every window's kernel
-      HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
-      if (int rc = ws->fence_stages((int)std::min<uint64_t>(host_stages(), nwin))) return rc;
-    }
-    if (int rc = run_windows(
+  bool ran_direct = false;
+  auto rebase = [&](uint8_t* base, uint32_t* p) { return (uint32_t*)(base + ((uint8_t*)p - slot)); };
+  auto pass = [&](size_t direct_bytes) -> int {
+    return run_windows(
             "write_chunks", ws, slot, nwin, (size_t)total * round64(cl * 4) + 128,
             [&](uint64_t c, int, Window& w) {
               const uint64_t c0 = c * cl, nc = std::min(cl, L - c0);
@@ -1800,17 +1842,34 @@ static int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int t
                 w.out.push_back({chunks[need + i] + 4 * c0, (uint64_t)(need + i) * chunk + 4 * c0, 4 * nc});
               if (one) w.out.push_back({(uint8_t*)ms, (uint64_t)((uint8_t*)d_map - slot), sizeof(ms)});
             },
-            [&](uint64_t c, int, hipStream_t st) -> int {
-              BytesLaunch a = bytes_launch(plan, slot, stride, 0, L, size, 1, 0, d_status, d_map);
+            [&](uint64_t c, int, hipStream_t st, uint8_t* base) -> int {
+              ran_direct = base != slot;
+              BytesLaunch a =
+                  bytes_launch(plan, base, stride, 0, L, size, 1, 0, rebase(base, d_status), rebase(base, d_map));
               a.col0 = c * cl;
               a.ncols = std::min(cl, L - a.col0);
               HIP_TRY(launch_encode_bytes(a, st));
               return 0;
             },
             [&](uint64_t c) {
-              if (dg) dg->parity_ready(4 * std::min(L, (c + 1) * cl));
-            }))
-      return rc;
+              if (dg && !(ran_direct && (ms[1] & 1u))) dg->parity_ready(4 * std::min(L, (c + 1) * cl));
+            },
+            direct_bytes);
+  };
+  auto body = [&]() -> int {
+    if (!one) {  // the flags start at zero for every window's kernel
+      HIP_TRY(hipMemsetAsync(d_map, 0, 8, ws->stream));
+      if (int rc = ws->fence_stages((int)std::min<uint64_t>(host_stages(), nwin))) return rc;
+    }
+    if (int rc = pass(one ? round16(stride) + 8 : 0)) return rc;
+    // A direct pass (the kernel on the pinned stage) left nothing on the
+    // device; an object that is not mapping 0 -- a word >= p, odds ~5 in 2^32
+    // a word -- runs the window again through the device buffer, which the
+    // choice of mapping and the re-encode below read.
+    if (ran_direct && (ms[1] & 1u)) {
+      ran_direct = false;
+      if (int rc = pass(0)) return rc;
+    }
     // One window: ms came back with the parity, ms[1] holding MapToGF's
     // flags (bit 0: a word >= p).  With bit 0 clear the mapping is 0 and
     // nothing else runs; otherwise -- and after several windows -- the
@@ -1942,13 +2001,15 @@ int slime_rs_reconstruct(const uint8_t* const* chunks, const int* indices, int n
             if (o < got) w.out.push_back({out + o, body_bytes + o, std::min(4 * nc, got - o)});
           }
         },
-        [&](uint64_t c, int, hipStream_t st) -> int {
-          BytesLaunch a = bytes_launch(plan, slot, stride, 0, L, 0, 1, 0, nullptr, d_map);
+        [&](uint64_t c, int, hipStream_t st, uint8_t* base) -> int {
+          BytesLaunch a =
+              bytes_launch(plan, base, stride, 0, L, 0, 1, 0, nullptr, (uint32_t*)(base + ((uint8_t*)d_map - slot)));
           a.col0 = c * cl;
           a.ncols = std::min(cl, L - a.col0);
           HIP_TRY(launch_decode_bytes(a, st));
           return 0;
-        });
+        },
+        [](uint64_t) {}, round16(stride) + 4);
   };
   const int rc = body();
   if (rc) drain_stages(ws);
@@ -2021,7 +2082,7 @@ static int pack_windows(Workspace* ws, const uint8_t* in, uint64_t len, uint32_t
         w.in.push_back({const_cast<uint8_t*>(in) + b0, (uint64_t)(d_bytes - base) + b0, nb});
         w.out.push_back({(uint8_t*)out + b0, (uint64_t)((uint8_t*)d_words - base) + b0, 4 * ((nb + 3) / 4)});
       },
-      [&](uint64_t c, int, hipStream_t st) -> int {
+      [&](uint64_t c, int, hipStream_t st, uint8_t*) -> int {
         const uint64_t b0 = c * W, nb = std::min(W, len - b0);
         HIP_TRY(launch_map_pack(d_bytes + b0, nb, n, d_words + b0 / 4, d_flags, st));
         return 0;
@@ -2188,7 +2249,7 @@ static int map_from_gf_device(uint32_t n, const uint32_t* in, uint64_t count, ui
         w.in.push_back({(uint8_t*)(in + w0), 4 * w0, 4 * nwd});
         w.out.push_back({out + 4 * w0, wbytes + 4 * w0, 4 * nwd});
       },
-      [&](uint64_t c, int, hipStream_t st) -> int {
+      [&](uint64_t c, int, hipStream_t st, uint8_t*) -> int {
         const uint64_t w0 = c * W, nwd = std::min(W, count - w0);
         HIP_TRY(launch_map_unpack(d_words + w0, nwd, n, d_bytes + 4 * w0, st));
         return 0;
