@@ -1269,3 +1269,65 @@ def test_on_device_restores_the_threads_previous_selection():
     with N.on_device(0):
         pass
     assert N.lib.slime_rs_selected_device() == N.ANY_DEVICE
+
+
+_SMALL_CALLS = r'''
+import hashlib, json, sys
+import numpy as np
+from slime_amd import objects, rs
+out = []
+for need, total, S, kind in json.loads(sys.argv[1]):
+    rng = np.random.default_rng(S * 13 + need)
+    b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+    if kind == "high" and S >= 4:
+        b[0:4] = b"\xff\xff\xff\xff"
+    if kind == "fallback" and S >= 8:
+        b[0:8] = b"\xff\xff\xff\xff\x7f\xff\xff\xff"
+    m, chunks = objects.write_chunks(bytes(b), need, total)
+    have = list(range(total - need, total))
+    back = objects.reconstruct([chunks[i] for i in have], have, m, S).tobytes() == bytes(b)
+    rows = [np.frombuffer(chunks[j], dtype=np.uint32).copy() for j in range(need)]
+    par = rs.CreateParity(rows, total - 1)
+    out.append([m, [hashlib.sha256(c.tobytes()).hexdigest() for c in chunks], back,
+                hashlib.sha256(np.ascontiguousarray(par).tobytes()).hexdigest()])
+print(json.dumps(out))
+'''
+
+
+def test_small_calls_same_with_direct_and_tiny_rules_off():
+    """The small-call rules (rs_capi.cpp run_windows "direct": a one-window
+    call's kernel on the mapped pinned stage; kernels.hpp queue_spread: one
+    block's units on the static kernels) change no byte: a child process with
+    both off (SLIME_RS_DIRECT_KIB=0, SLIME_RS_TINY_UNITS=0: copy kernels and the
+    dynamic schedule) gives the same mappings, chunks, round trips and parity
+    rows as this process, and this process matches the oracle.  "fallback"
+    objects draw their mapping at random, so only plain and 1<<31 objects are
+    compared across processes."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+    cases = [[need, total, S, kind] for need, total in ((4, 6), (8, 12), (10, 14))
+             for S in (1, 5, 4096, 65536 + 3, 200003) for kind in ("plain", "high")]
+    env = dict(os.environ, SLIME_RS_DIRECT_KIB="0", SLIME_RS_TINY_UNITS="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", _SMALL_CALLS, json.dumps(cases)], env=env, cwd=root,
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    child = json.loads(res.stdout.strip().splitlines()[-1])
+    from slime_amd import objects
+    for (need, total, S, kind), (cm, chashes, cback, cpar) in zip(cases, child):
+        rng = np.random.default_rng(S * 13 + need)
+        obj = _obj_bytes(rng, S, kind)
+        m, chunks = objects.write_chunks(obj, need, total)
+        m_ref, want = _oracle_chunks(obj, need, total, [])
+        assert m == m_ref == cm, (need, S, kind)
+        assert [c.tobytes() for c in chunks] == want
+        assert [hashlib.sha256(w).hexdigest() for w in want] == chashes, (need, S, kind)
+        assert cback, (need, S, kind)
+        rows = [np.frombuffer(chunks[j], dtype=np.uint32).copy() for j in range(need)]
+        par = rs.CreateParity(rows, total - 1)
+        _, par_ref = OC.create_parity(rows, total - 1)
+        assert np.array_equal(np.asarray(par, dtype=np.uint32), np.asarray(par_ref, dtype=np.uint32))
+        assert hashlib.sha256(np.ascontiguousarray(par).tobytes()).hexdigest() == cpar, (need, S, kind)

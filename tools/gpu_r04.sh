@@ -219,6 +219,7 @@ for step in "$@"; do
     tinyab) for rep in 1 2; do for v in 4 0; do run tiny_lat_${v}_$rep 200 env SLIME_RS_TINY_UNITS=$v tools/latency_c 200 || exit 1; done; done ;;
     directab) for rep in 1 2; do for v in 256 1024 4096 0; do run direct_lat_${v}_$rep 200 env SLIME_RS_DIRECT_KIB=$v tools/latency_c 200 || exit 1; done; done ;;
     tests_direct0) run pytest_host_direct0 400 env SLIME_RS_DIRECT_KIB=0 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct" ;;
+    tests_small) run pytest_small 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 280 --timeout-method thread -k small_calls_same ;;
     altpaths) run alt_copyengines 400 env SLIME_RS_BLIT_KIB=0 SLIME_RS_BLIT_D2H_KIB=0 SLIME_RS_DMA_2D=0 SLIME_RS_D2H_PARTS=1 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct or write_chunks or copy_kernel_threshold" &&
               run alt_allblit 400 env SLIME_RS_BLIT_KIB=65536 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "host or reconstruct or write_chunks or copy_kernel_threshold" ;;
     spinab) for rep in 1 2; do for v in 200 0; do run spin_lat_${v}_$rep 200 env SLIME_RS_SPIN_US=$v tools/latency_c 200 &&
