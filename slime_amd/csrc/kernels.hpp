@@ -154,16 +154,28 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
   const uint64_t B = (groups + S - 1) / S;
   const uint64_t units = (uint64_t)nobj * S * B * 4;
   if (units >= (1ull << 32)) return 0;
-  // A launch of at most one block's units (a host call on a small object)
-  // takes the static kernels: the dynamic schedule has nothing to balance
-  // there, and its set hand-out and ticket atomics are most of such a launch
-  // (env SLIME_RS_TINY_UNITS, default 4; 0 = every launch on the queue).
+  // A launch of at most one block's units takes the static kernels: the
+  // dynamic schedule has nothing to balance there, and its set hand-out and
+  // ticket atomics are most of such a launch (env SLIME_RS_TINY_UNITS,
+  // default 4; 0 = off).  So does a launch over ONE object of at most 1024
+  // units -- a host call's window, up to about 16 MiB: one block or less per
+  // CU, and the static grid's waves load their tiles at once where the
+  // queue's fewer waves walk them (1 MiB write_chunks 94-113 -> 82-92 us,
+  // reconstruct 122-150 -> 110-125, 8 MiB 3-5% faster, 64 MiB fused write and
+  // reconstruct equal or better: profiles/r04/s50_tinyab2, s51_tinyab3; env
+  // SLIME_RS_ONE_OBJECT_UNITS, default 1024; 0 = off).  Batches of several
+  // objects keep the queue from 5 units up.
   static const uint64_t tiny = [] {
     const char* e = getenv("SLIME_RS_TINY_UNITS");
     const long long v = e ? atoll(e) : 4;
     return v > 0 ? (uint64_t)v : 0ull;
   }();
-  if (units <= tiny) return 0;
+  static const uint64_t one_object = [] {
+    const char* e = getenv("SLIME_RS_ONE_OBJECT_UNITS");
+    const long long v = e ? atoll(e) : 1024;
+    return v > 0 ? (uint64_t)v : 0ull;
+  }();
+  if (units <= tiny || (nobj == 1 && units <= one_object)) return 0;
   return (uint32_t)S;
 }
 
