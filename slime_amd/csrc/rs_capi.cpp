@@ -638,10 +638,15 @@ int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std
 // kernel on the mapped pinned stage itself ("direct"): the stage holds the
 // window in the device layout, the kernel reads its inputs and writes its
 // outputs across PCIe, and the two copy kernels around it -- each a dispatch
-// and a PCIe round trip, most of a 4 KiB call -- do not run (env
-// SLIME_RS_DIRECT_KIB, default 256; 0 = never).
+// and a PCIe round trip, most of a 4 KiB call -- do not run.  One window has
+// no upload/compute overlap to lose, and the static grid of a one-object
+// launch (queue_spread) keeps enough loads in flight across the link: 4 KiB
+// write_chunks 23 -> 20 us, 1 MiB 80 -> 67-80, 8 MiB 392-402 -> 363-366
+// (profiles/r04/s44-s45, s52_directab2, s53_directab3; the 1 MiB gain varies
+// by box).  Env SLIME_RS_DIRECT_KIB, default 16384 (every one-window call);
+// 0 = never.
 uint64_t direct_max_bytes() {
-  static const uint64_t v = env_kib("SLIME_RS_DIRECT_KIB", 256);
+  static const uint64_t v = env_kib("SLIME_RS_DIRECT_KIB", 16384);
   return v;
 }
 // Pinned stage of a direct call: at least this much, as the device buffer
