@@ -1300,7 +1300,8 @@ def test_small_calls_same_with_direct_and_tiny_rules_off():
     block's units, or one object's up to 1024, on the static kernels) change no
     byte: a child process with them off (SLIME_RS_DIRECT_KIB=0,
     SLIME_RS_TINY_UNITS=0, SLIME_RS_ONE_OBJECT_UNITS=0: copy kernels and the
-    dynamic schedule) gives the same mappings, chunks, round trips and parity
+    dynamic schedule; one-window objects of 4-6 MiB take the copy kernel or the
+    copy engines) gives the same mappings, chunks, round trips and parity
     rows as this process, and this process matches the oracle.  "fallback"
     objects draw their mapping at random, so only plain and 1<<31 objects are
     compared across processes."""
@@ -1311,6 +1312,8 @@ def test_small_calls_same_with_direct_and_tiny_rules_off():
     import sys
     cases = [[need, total, S, kind] for need, total in ((4, 6), (8, 12), (10, 14))
              for S in (1, 5, 4096, 65536 + 3, 200003, (3 << 20) + 1) for kind in ("plain", "high")]
+    # one-window objects either side of the copy kernel's 4 MiB upload limit (direct off in the child)
+    cases += [[8, 12, S, kind] for S in ((4 << 20) - 3, (6 << 20) + 7) for kind in ("plain", "high")]
     env = dict(os.environ, SLIME_RS_DIRECT_KIB="0", SLIME_RS_TINY_UNITS="0", SLIME_RS_ONE_OBJECT_UNITS="0")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = subprocess.run([sys.executable, "-c", _SMALL_CALLS, json.dumps(cases)], env=env, cwd=root,
