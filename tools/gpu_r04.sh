@@ -220,6 +220,7 @@ for step in "$@"; do
     directab2) for rep in 1 2; do for v in 16384 256; do run direct2_lat_${v}_$rep 200 env SLIME_RS_DIRECT_KIB=$v tools/latency_c 200 || exit 1; done; done ;;
     bigdirect) for rep in 1 2; do run bd_host_def_$rep 300 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 && run bd_host_64_$rep 300 env SLIME_RS_OBJ_WINDOW_MIB=64 SLIME_RS_DIRECT_KIB=131072 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 || exit 1; done ;;
     tests_knobsoff) run pytest_knobsoff 1100 env SLIME_RS_DIRECT_KIB=0 SLIME_RS_ONE_OBJECT_UNITS=0 SLIME_RS_TINY_UNITS=0 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    ssab) for rep in 1 2 3; do for v in 0 1; do run ss_lat_${v}_$rep 200 env SLIME_RS_DIRECT_STREAM_SYNC=$v tools/latency_c 300 || exit 1; done; done ;;
     winab) for rep in 1 2; do for v in 16 4 2; do run win_lat_${v}_$rep 200 env SLIME_RS_OBJ_WINDOW_MIB=$v tools/latency_c 200 || exit 1; done; done ;;
     cohab) for rep in 1 2; do for v in d 1 0; do run coh_lat_${v}_$rep 200 env SLIME_RS_PIN_COHERENT=$v tools/latency_c 200 || exit 1; done; done &&
            for v in d 1; do run coh_host_$v 300 env SLIME_RS_PIN_COHERENT=$v python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 || exit 1; done ;;
