@@ -363,3 +363,19 @@ def test_slot_geometry_chunk_strides():
     for bad in (4096, 4102):  # below 4L, not a multiple of 4
         with pytest.raises(ValueError):
             D._chunk_stride(1025, bad)
+
+
+def test_every_env_knob_is_documented():
+    """Every SLIME_RS_* environment variable the native library reads is in
+    INTEGRATION.md's table of knobs (a maintainer tuning a box finds them all)."""
+    import pathlib
+    import re
+    root = pathlib.Path(__file__).resolve().parent.parent
+    names = set()
+    for f in (root / "slime_amd" / "csrc").iterdir():
+        if f.suffix in (".cpp", ".hpp", ".hip", ".h"):
+            names |= set(re.findall(r'"(SLIME_RS_[A-Z0-9_]+)"', f.read_text()))
+    assert len(names) > 20
+    doc = (root / "INTEGRATION.md").read_text()
+    missing = sorted(n for n in names if n not in doc)
+    assert not missing, missing
