@@ -16,8 +16,14 @@ CACHETEST := tests/cpp/plan_cache_test
 COPYTEST := tests/cpp/copy_pool_test
 POOLTEST := tests/cpp/device_pool_test
 MFMATEST := tests/cpp/mfma_table_test
+PROXYLOAD := tools/libproxy_load.so
 
-all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST) $(PROXYLOAD)
+
+# Proxy-level load generator over the C-ABI (bench.py host_path.pooled): C++ threads, no GIL.
+$(PROXYLOAD): tools/proxy_load.cpp include/slime_rs.h $(LIB)
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -fPIC -shared -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
+	  -Wl,-rpath,'$$ORIGIN/../slime_amd/lib'
 
 # The matrix-core kernel's int8-limb arithmetic emulated on its table (mfma_table.hpp), CPU only.
 $(MFMATEST): tests/cpp/mfma_table_test.cpp $(SRC)/mfma_table.hpp $(SRC)/gfp.hpp $(SRC)/gfp_host.hpp
@@ -57,7 +63,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
+	rm -rf build $(LIB) $(PROXYLOAD) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

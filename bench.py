@@ -103,9 +103,15 @@ def parse(argv=None):
     ap.add_argument("--shard-align", type=int, default=64,
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
-    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py over rocprofv3 --pmc passes; "
-                         "used only when its config and the kernel's machine code match this build)")
+    ap.add_argument("--traffic", type=str,
+                    default=",".join(os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r05", "r04")),
+                    help="PMC-derived HBM bytes per launch, comma-separated files (tools/pmc_traffic.py over "
+                         "rocprofv3 --pmc passes; an entry is used only when its config and the kernel's machine "
+                         "code match this build)")
+    ap.add_argument("--shape-legs", type=str, default="c2,ns64",
+                    help="after the timed region, also time these BASELINE shapes per GPU (weak), each in the "
+                         "main batch's buffer re-laid (no allocation): c2 (4/6, 32 x 64 MiB), ns64 (8/12, "
+                         "64 x 512 MiB, the north star's 64 MiB shards); '' for none")
     args = ap.parse_args(argv)
     if args.preset:
         given = {a.split("=")[0] for a in (argv if argv is not None else sys.argv[1:]) if a.startswith("--")}
@@ -888,7 +894,7 @@ class SymbolBatch:
     separate).  One step = one encode launch + one decode launch."""
 
     def __init__(self, args, dev: int, seed: int, need: int, total: int, S: int, nobj: int, erase: list[int],
-                 decode_dst: str = "inplace"):
+                 decode_dst: str = "inplace", reuse: torch.Tensor | None = None):
         self.need, self.total, self.S, self.nobj, self.erase = need, total, S, nobj, erase
         self.have = [i for i in range(total) if i not in erase][:need]
         self.L = L = ceil_div(ceil_div(S, 4), need)  # perVector = ceil(ceil(S/4)/need) (multi_store.go:272)
@@ -898,8 +904,13 @@ class SymbolBatch:
         # never read or written; the algorithmic bytes are L's.
         self.SS = SS = ceil_div(L, max(1, args.shard_align)) * max(1, args.shard_align)
         self.lay = D.layout_of(total, L, SS)
-        self.buf = batch_empty(args, max(1, nobj) * total * SS, torch.int32, dev)
-        self.placement = D.placement(self.buf) if args.allocator == "vmm" else None
+        numel = max(1, nobj) * total * SS
+        # `reuse`: re-lay another batch's buffer (its placement is that batch's)
+        # instead of allocating -- the legs after the timed C3 region.
+        self.owned = reuse is None or reuse.numel() < numel
+        self.buf = batch_empty(args, numel, torch.int32, dev) if self.owned else reuse[:numel]
+        self.placement = (D.placement(self.buf) if self.owned else dict(D.placement(reuse), relaid=True)) \
+            if args.allocator == "vmm" else None
         D.fill_symbols(self.buf, seed)
         self.enc = D.Plan.encode(need, total, dev)
         self.dec = D.Plan.reconstruct(need, total, self.have, erase, dev)
@@ -971,6 +982,29 @@ class SymbolBatch:
     def free(self):
         del self.buf, self.rec
         torch.cuda.empty_cache()
+        D.release_deferred()
+
+
+def symbol_traffic(args, need: int, total: int, L: int, nobj: int, kname: str) -> tuple:
+    """HBM bytes per launch of the symbol path's apply kernel at this shape.
+    PMC counters cannot be read inside this process (they need rocprofv3 --pmc
+    passes of their own), so the bytes are replayed from the committed
+    summaries of such passes (--traffic: tools/pmc_traffic.py output, one
+    entry or a list) only when one was taken on this config AND this kernel's
+    machine code; the second value says where they came from."""
+    code_id = kernel_code_id(D.N.LIB_PATH, (f"{kname}ILi{need}E",))
+    config = f"{need}/{total} L={L} nobj={nobj}"
+    for path in (p for p in args.traffic.split(",") if p):
+        try:
+            tj = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for e in tj if isinstance(tj, list) else [tj]:
+            if code_id and e.get("config") == config and e.get("kernel") == kname and e.get("kernel_code") == code_id:
+                return e.get("hbm_bytes_per_launch"), (
+                    f"replayed: {os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                    f"session {e.get('session', '?')}, kernel code {code_id})")
+    return None, "not measured for this kernel's machine code/config"
 
 
 def apply_kernel_name(need: int, rows: int, L: int, shard_bytes_span: int) -> str:
@@ -1020,6 +1054,53 @@ def c5_leg(args, dev: int, rank: int, world: int) -> dict:
             "verified": all(p["verified"] for p in per_rank)}
 
 
+def shape_leg(args, name: str, dev: int, rank: int, world: int, reuse: torch.Tensor | None) -> dict:
+    """A BASELINE shape beside the headline C3+C4 (PRESETS[name]: c2 = config
+    2, 4/6 x 32 x 64 MiB; ns64 = the north star's "8/12 on 64 MiB shards", 64 x
+    512 MiB), timed like the main region (W untimed steps, K timed ones of one
+    encode + one decode launch, barrier + synchronize on both sides, HIP
+    events on the launch stream) in `reuse` -- the main batch's buffer re-laid,
+    so the leg allocates nothing.  Per GPU ("weak"): every rank runs its own
+    batch of this shape.  The reference's loop is the same per-object
+    multi_store.go:528-531 at that shape."""
+    need, total, mib, per_gpu, _, erase_s = PRESETS[name]
+    erase = [int(x) for x in erase_s.split(",")]
+    S = mib << 20
+    sb = SymbolBatch(args, dev, 0x5113E + 0x1000 * (1 + sorted(PRESETS).index(name)) + 7919 * rank,
+                     need, total, S, per_gpu, erase, reuse=reuse)
+    res = sb.run(args.steps, args.warmup)
+    enc_ms = sum(res["enc_all"]) / len(res["enc_all"])
+    dec_ms = sum(res["dec_all"]) / len(res["dec_all"])
+    enc_alg, dec_alg = sb.alg_bytes()
+    r = total - need
+    kname = apply_kernel_name(need, r, sb.L, total * sb.SS * 4)
+    traffic, source = symbol_traffic(args, need, total, sb.L, per_gpu, kname)
+    ach = (enc_alg + dec_alg) / 2 / ((enc_ms + dec_ms) / 2 * 1e-3) / 1e9
+    placement, L, SS = sb.placement, sb.L, sb.SS
+    if sb.owned:
+        sb.free()
+    del sb
+    elapsed, bad = batch.max_over_ranks([res["elapsed"], 0.0 if res["ok"] else 1.0])
+    return {"value": round(2 * per_gpu * world * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
+            "scaling": "weak", "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "config": f"{shape_label(need, total, mib)}need={need} total={total}, {mib} MiB objects x {per_gpu} per "
+                      f"GPU; encode all parity + decode erased {erase}",
+            "symbols_per_shard": L, "shard_stride_symbols": SS,
+            "encode_gibs": round(per_gpu * S / GIB / (enc_ms * 1e-3), 2),
+            "decode_gibs": round(per_gpu * S / GIB / (dec_ms * 1e-3), 2),
+            "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4),
+                          "encode_min_max": [round(min(res["enc_all"]), 4), round(max(res["enc_all"]), 4)],
+                          "decode_min_max": [round(min(res["dec_all"]), 4), round(max(res["dec_all"]), 4)]},
+            "roofline": {"bound": "hbm", "kernel": f"{kname}<{need},vec>", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "encode_frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "decode_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_over_alg":
+                             round(traffic / ((enc_alg + dec_alg) / 2), 4) if traffic else None,
+                         "traffic_source": source, "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg}},
+            "placement": placement, "verified": bad == 0.0}
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -1055,7 +1136,11 @@ def main():
                               "partitions": [json.loads(p) for p in parts],
                               "c5_partitioned": None if not args.c5_leg else
                               {"need": 10, "total": 14, "object_mib": 1024, "objects": PRESETS["c5"][4],
-                               "partitions": [json.loads(p) for p in c5parts]}}), flush=True)
+                               "partitions": [json.loads(p) for p in c5parts]},
+                              "shapes": {n: {"need": PRESETS[n][0], "total": PRESETS[n][1], "object_mib": PRESETS[n][2],
+                                             "objects_per_rank": PRESETS[n][3], "scaling": "weak"}
+                                         for n in args.shape_legs.split(",") if n and
+                                         PRESETS[n][:3] != (args.need, args.total, args.object_mib)}}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -1090,22 +1175,7 @@ def main():
     launch_ms = (enc_ms + dec_ms) / 2
     achieved = (enc_alg + dec_alg) / 2 / (launch_ms * 1e-3) / 1e9
     kname = apply_kernel_name(need, r, L, total * SS * 4)
-    # HBM traffic cannot be counted inside this process (PMC needs rocprofv3
-    # --pmc passes of their own).  It is replayed from the summary of such
-    # passes only when they were taken on this config AND this kernel source,
-    # and the line says where it came from.
-    traffic, traffic_source = None, "not measured for this kernel's machine code/config"
-    code_id = kernel_code_id(D.N.LIB_PATH, (f"{kname}ILi{need}E",))
-    if os.path.exists(args.traffic) and code_id:
-        try:
-            tj = json.load(open(args.traffic))
-            if tj.get("config") == f"{need}/{total} L={L} nobj={nobj}" and tj.get("kernel") == kname \
-                    and tj.get("kernel_code") == code_id:
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_source = (f"replayed: {os.path.relpath(args.traffic, ROOT)} (rocprofv3 --pmc FETCH_SIZE / "
-                                  f"WRITE_SIZE passes, session {tj.get('session', '?')}, kernel code {code_id})")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_source = symbol_traffic(args, need, total, L, nobj, kname)
     # Distinct devices across ranks (n_gpus), by PCI address.
     bdfs = batch.gather_strings(board_info(dev)["bdf"])
     # The CPU baseline's input: object 0 of this batch as the GPU left it
@@ -1162,6 +1232,13 @@ def main():
                        "threshold_gbs": float(D.lib.slime_rs_placement_threshold()),
                        "what": "slime_rs_probe_placement over the fresh hipMalloc buffer before it was filled, "
                                "beside the probe of the library buffer that was kept"}
+    # The other BASELINE shapes, in the main buffer re-laid (after the
+    # allocator probe, which reads the main batch's contents no more).
+    shapes = {}
+    for name in (x for x in args.shape_legs.split(",") if x):
+        pn, pt, pm, ppg, _, _ = PRESETS[name]
+        if (pn, pt, pm) != (need, total, args.object_mib):
+            shapes[name] = shape_leg(args, name, dev, rank, world, sb.buf)
     sb.free()
     bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj) if args.bytes_path else None
     if want_host and args.host_order == "after-free":
@@ -1217,6 +1294,7 @@ def main():
             "rehearsal": (f"{world} ranks sharing {len(set(bdfs))} GPU(s) (SLIME_BENCH_SHARE_GPU=1): "
                           "a test of the multi-rank path, not a scaling number") if shared_gpu_rehearsal() else None,
             "c5_partitioned": c5,
+            "shapes": shapes,
             "object_bytes_path": bytes_path,
             "allocator_probe": alloc_probe,
         }
@@ -1229,7 +1307,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if bad or (c5 is not None and not c5["verified"]):
+    if bad or (c5 is not None and not c5["verified"]) or not all(v["verified"] for v in shapes.values()):
         sys.exit(3)
 
 

@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kBlock) void redo_list_kernel(const uint8_t* __rest
     if (!mask) continue;
     uint32_t at = 0;
     if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
-    at = __builtin_amdgcn_readfirstlane(at);
+    at = __builtin_amdgcn_readlane(at, 0);  // lane 0 drew it, whatever the exec mask
     if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
   }
 }

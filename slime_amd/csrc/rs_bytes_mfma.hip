@@ -96,7 +96,8 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
   uint32_t f = flags_now(fobj);
   while (t < ntiles) {
     const uint32_t tn = t + nwaves;
-    const uint32_t m = (__builtin_amdgcn_readfirstlane(f) & 1u) ? 0x80000000u : 0u;
+    // lane 0's load: the lane that records the mapping this tile used
+    const uint32_t m = (__builtin_amdgcn_readlane(f, 0) & 1u) ? 0x80000000u : 0u;
     if (lane == 0) rec[t] = m ? 1 : 0;
     if (tn < ntiles) f = flags_now(fobj);  // tile tn's mapping, in flight during tile t
     const MfmaIO io{0x80808080u ^ be(m), m};
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
     if (!mask) continue;
     uint32_t at = 0;
     if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
-    at = __builtin_amdgcn_readfirstlane(at);
+    at = __builtin_amdgcn_readlane(at, 0);  // lane 0 drew it, whatever the exec mask
     if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
   }
 }

@@ -199,3 +199,22 @@ def test_matrix_core_labels_follow_the_library_rule():
     no = [(8, 4), (10, 4), (16, 16), (20, 4), (17, 7), (64, 33), (113, 4), (40, 0)]
     assert all(bench._matrix_cores(k, r) for k, r in yes)
     assert not any(bench._matrix_cores(k, r) for k, r in no)
+
+
+def test_dry_run_plans_the_c2_and_north_star_shape_legs():
+    """Every line carries BASELINE config 2 (4/6, 32 x 64 MiB) and the north
+    star's 64 MiB-shard shape (8/12, 64 x 512 MiB) per GPU beside C3+C4; a
+    run whose main shape is one of them does not repeat it."""
+    r = _bench(["--gpus", "2", "--dry-run"], SLIME_BENCH_DEVICE_COUNT="2")
+    assert r.returncode == 0, r.stdout + r.stderr
+    sh = json.loads(r.stdout.strip().splitlines()[-1])["shapes"]
+    assert sh["c2"] == {"need": 4, "total": 6, "object_mib": 64, "objects_per_rank": 32, "scaling": "weak"}
+    assert sh["ns64"] == {"need": 8, "total": 12, "object_mib": 512, "objects_per_rank": 64, "scaling": "weak"}
+    r = _bench(["--dry-run", "--preset", "c2"], SLIME_BENCH_DEVICE_COUNT="1")
+    sh = json.loads(r.stdout.strip().splitlines()[-1])["shapes"]
+    assert set(sh) == {"ns64"}
+    # ns64 re-lays the C3 batch's buffer: exactly the same number of words
+    bench = _load("bench.py", "bench_mod_ns64")
+    c3 = 128 * 12 * bench.ceil_div(bench.ceil_div(256 << 20, 4), 8)
+    ns = 64 * 12 * bench.ceil_div(bench.ceil_div(512 << 20, 4), 8)
+    assert c3 == ns
