@@ -8,7 +8,7 @@ SRC      := slime_amd/csrc
 OBJ      := build/obj
 LIB      := slime_amd/lib/libslime_rs.so
 
-OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_apply_mfma.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/rs_bytes_mfma.o $(OBJ)/gf_codec.o $(OBJ)/host_blit.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/host_codec.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/rs_capi.o
+OBJS := $(OBJ)/rs_apply.o $(OBJ)/rs_apply_k32.o $(OBJ)/rs_apply_mfma.o $(OBJ)/rs_bytes.o $(OBJ)/rs_bytes_k32.o $(OBJ)/rs_bytes_mfma.o $(OBJ)/gf_codec.o $(OBJ)/host_blit.o $(OBJ)/rs_matrix.o $(OBJ)/host_copy.o $(OBJ)/host_codec.o $(OBJ)/digest.o $(OBJ)/device_alloc.o $(OBJ)/host_pipeline.o $(OBJ)/go_api.o $(OBJ)/object_calls.o $(OBJ)/rs_capi.o
 HDRS := $(wildcard $(SRC)/*.hpp) include/slime_rs.h
 
 CXXTEST  := tests/cpp/rs_host_test

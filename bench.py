@@ -90,6 +90,13 @@ def parse(argv=None):
                          "freed them: the driver then wipes the freed VRAM with the same DMA engines the host "
                          "path uses, which slows its transfers for seconds (DESIGN.md, End-to-end)")
     ap.add_argument("--host-delay", type=float, default=0.0, help="seconds to wait before the host leg")
+    ap.add_argument("--pooled", type=int, default=1,
+                    help="at every N: rank 0 drives the host entry points as one proxy does (--pool-threads "
+                         "concurrent PUT + GET requests, SLIME_RS_ANY_DEVICE) over the GPUs of all N ranks, the "
+                         "other ranks parked at a barrier; reported as host_path.pooled (never `value`)")
+    ap.add_argument("--pool-threads", type=int, default=25,
+                    help="concurrent requests of the pooled leg (slime's --parallel-requests default, main.go:107-109)")
+    ap.add_argument("--pool-seconds", type=float, default=2.0, help="timed seconds per pooled workload")
     ap.add_argument("--allocator", choices=["vmm", "torch"], default="vmm",
                     help="batch buffers from slime_rs_device_alloc (physical chunks mapped into one range: the "
                          "placement the kernels stream well from, DESIGN.md 'Placement modes') or torch.empty "
@@ -243,6 +250,17 @@ def _cgroup_cpus() -> float | None:
         return None
 
 
+def _mem_available() -> int:
+    """MemAvailable of this host in bytes (16 GiB if unreadable)."""
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) << 10
+    except (OSError, ValueError, IndexError):
+        pass
+    return 16 << 30
+
+
 def _cpu_leg(OC, sample, need: int, total: int, have: list[int], threads: int, seconds: float) -> dict:
     """`threads` host threads, each on its own copy of the sample object, each
     running the reference's per-object path until ~`seconds` of wall time: r
@@ -283,7 +301,7 @@ def _cpu_leg(OC, sample, need: int, total: int, have: list[int], threads: int, s
     for t in ts:
         t.join()
     dt = time.perf_counter() - t0
-    nbytes = 2 * sum(reps) * need * L * 4  # encode + decode of each object pass
+    nbytes = 2 * sum(reps) * need * L * 4  # encode + decode of each object pass (L columns)
     return {"value": round(nbytes / GIB / dt, 4), "unit": "GiB/s", "cores": threads,
             "object_passes": sum(reps), "seconds": round(dt, 2), "_first": first}
 
@@ -295,9 +313,6 @@ def _matrix_cores(k: int, rows: int) -> bool:
     from slime_amd import _native as N
     if N.lib.slime_rs_kernel_matrix_cores(-1) != 1 or rows > 32 or k > 112 or rows < 1:
         return False
-    forced = int(os.environ.get("SLIME_RS_MFMA_MINK", "0") or 0)
-    if forced > 0:
-        return k >= forced and k >= 17
     return k >= 33 or (k >= 17 and k * rows >= 128)
 
 
@@ -326,8 +341,18 @@ def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[in
     first = one.pop("_first")
     ok = bool(np.array_equal(first["parity"], sample[need:])) and \
         all(np.array_equal(first["data"][t], sample[t]) for t in range(need))
-    allc = _cpu_leg(OC, sample, need, total, have, ncores, seconds * 0.6)
+    # The all-core leg gives every thread its own copy of the object and of
+    # RecoverData's outputs ((total + need) x 4 bytes per column): on a host
+    # with many cores and no quota that is far more memory than the sample.
+    # Threads take a column slice of the sample instead (the rate is per byte),
+    # sized so that all copies fit in min(8 GiB, a quarter of MemAvailable).
+    L = sample.shape[1]
+    budget = min(8 << 30, _mem_available() // 4)
+    cols = max(4096, min(L, budget // (ncores * (total + need) * 4))) & ~63
+    cols = min(cols, L)
+    allc = _cpu_leg(OC, np.ascontiguousarray(sample[:, :cols]), need, total, have, ncores, seconds * 0.6)
     allc.pop("_first")
+    allc["columns_per_thread"] = int(cols)
     mib = sample.shape[1] * need * 4 / (1 << 20)
     # Small objects (a proxy's small requests): the same per-object path on one
     # thread, per call, on the first columns of the sample (the shards of an
@@ -357,7 +382,8 @@ def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[in
                       f"need={need} total={total}: per object, r CreateParity passes (multi_store.go:528-531) + "
                       f"RecoverData(erase {erase}) recomputing all need rows (vector.go:80-85); 1 thread "
                       f"({one['object_passes']} passes in {one['seconds']} s) and {ncores} threads on copies of it "
-                      f"({allc['object_passes']} passes in {allc['seconds']} s); oracle/rs_oracle.c, gcc -O2; "
+                      f"({allc['object_passes']} passes over the first {allc['columns_per_thread']} columns in "
+                      f"{allc['seconds']} s); oracle/rs_oracle.c, gcc -O2; "
                       "verified = the CPU's parity equals the GPU's for this object and RecoverData returns its data"}
 
 
@@ -441,7 +467,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
     kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
-    if _matrix_cores(need, total - need) and (need >= 25 or os.environ.get("SLIME_RS_MFMA_MINK")):
+    if _matrix_cores(need, total - need) and need >= 25:
         kernels["encode"] = ["encode_bytes_mfma_kernel"]
     if _matrix_cores(need, len(erase)):
         kernels["decode"] = ["decode_bytes_mfma_kernel"]
@@ -553,13 +579,14 @@ def host_leg(need, total, erase, obj_mib=64, reps=5):
     sym = [gf.MapToGFWith(chunks[i], m) for i in have]
     rec = [np.zeros(sym[0].size, dtype=np.uint32) for _ in range(need)]
     t_rd = med(lambda: rs.RecoverData(sym, have, rec))
-    unchanged = unchanged_caller(data, need, total, have, chunks, m, box["m"], reps)
+    unchanged = unchanged_caller(data, need, total, have, chunks, m, box["m"], max(7, reps))
     with_device_codec = None
     prev = gf.codec_placement(1)
     try:  # the same caller with the codec through the GPU (round 3's form), for comparison
         u = unchanged_caller(data, need, total, have, chunks, m, box["m"], 3)
         with_device_codec = {"write_gibs": u["write_gibs"], "read_gibs": u["read_gibs"],
-                             "split_ms": {"write": u["split_ms"]["write"], "read": u["split_ms"]["read"]}}
+                             "split_ms": {"write": u["write"]["split_ms"], "read": u["read"]["split_ms"]},
+                             "verified": u["verified"]}
     finally:
         gf.codec_placement(prev)
     par2 = [np.zeros(parts[0].size, dtype=np.uint32) for _ in range(r)]
@@ -664,21 +691,34 @@ def latency_leg(need, total, erase, sizes_kib=(4, 64, 1024, 8192), reps=25) -> d
 
 def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
     """multi_store.go as it is, call by call through the Go-API mirrors, on
-    fresh outputs (Go's make): writeChunks = MapToGF (:526) + splitVector
-    (:527) + r CreateParity (:528-531) + a MapFromGF per chunk (:554);
-    reconstruct's slow path = MapToGFWith per survivor (:224) + RecoverData
-    (:237) + MapFromGF per data row appended to make([]byte, 0, Size+16)
-    (:204,238-241).  Each phase is timed; the split is the median call's.
-    alloc_alone: the same fresh output buffers allocated (as the mirrors
-    allocate them) and first touched by one thread (page faults), alone --
-    the part of the phases that is Go's make()."""
+    fresh outputs (Go's make).  writeChunks = MapToGF (:526) + splitVector
+    (:527) + r CreateParity (:528-531) + a MapFromGF per chunk, each on its
+    own goroutine (:552-554: here one thread per part, all concurrent).
+    reconstruct's slow path = make([]byte, 0, Size+16) (:204) + MapToGFWith
+    per survivor (:224) + RecoverData (:237) + MapFromGF per data row
+    appended in order (:238-241).  `reps` timed calls of each after a warm
+    one: total min / median / max, every phase of every rep, and the median
+    call's split with `other` = total - the phases (Python between the
+    calls).  fresh_alloc_alone_ms: the same fresh outputs allocated and first
+    touched by one thread, timed on their own -- NOT part of the total; it
+    says how much of the phases is Go's make() (page faults).  Each rep also
+    records the process's page faults during the call and the time to drop
+    its intermediate buffers afterwards (deferred_free_ms, off the clock)."""
+    import concurrent.futures as cf
+    import resource
+
     import numpy as np
     from slime_amd import _native as N
     from slime_amd import gf, objects, rs
     r = total - need
     pc = time.perf_counter
+    goroutines = cf.ThreadPoolExecutor(max_workers=total)  # one per part, as writeChunks' go statements
 
-    def write():
+    # Every phase's intermediate buffers are handed back in `garbage` and
+    # dropped after the call's clock stops: Go's collector frees them off the
+    # request path, while CPython would munmap them (several ms per 64 MiB)
+    # inside the call.  The drop is timed on its own (deferred_free_ms).
+    def write(garbage):
         t0 = pc()
         mm, w = gf.MapToGF(data)
         t1 = pc()
@@ -686,71 +726,105 @@ def unchanged_caller(data, need, total, have, chunks, m, m_fused, reps) -> dict:
         t2 = pc()
         pv = [rs.CreateParity(ps, need + i) for i in range(r)]
         t3 = pc()
-        out = [gf.MapFromGF(mm, p) for p in ps + pv]
+        out = list(goroutines.map(lambda p: gf.MapFromGF(mm, p), ps + pv))
         t4 = pc()
-        return (mm, out), [t1 - t0, t2 - t1, t3 - t2, t4 - t3]
+        garbage.extend([w, ps, pv])
+        return (mm, out), [("map_to_gf", t1 - t0), ("split_vector", t2 - t1), (f"create_parity_x{r}", t3 - t2),
+                           (f"map_from_gf_x{total}_concurrent", t4 - t3)]
 
-    def read():
+    def read(garbage):
         t0 = pc()
-        cs = [gf.MapToGFWith(chunks[i], m) for i in have]
+        buf = np.empty(data.size + 16, dtype=np.uint8)  # make([]byte, 0, Size+16) (:204)
         t1 = pc()
-        vs = rs.RecoverData(cs, have)
+        cs = [gf.MapToGFWith(chunks[i], m) for i in have]
         t2 = pc()
-        buf = np.empty(data.size + 16, dtype=np.uint8)  # make([]byte, 0, Size+16)
+        vs = rs.RecoverData(cs, have)
+        t3 = pc()
         o = 0
         for v in vs:
             b = gf.MapFromGF(m, v)
             n = min(len(b), buf.size - o)
             buf[o:o + n] = np.frombuffer(b, dtype=np.uint8, count=n)
             o += n
-        t3 = pc()
-        return buf[:data.size], [t1 - t0, t2 - t1, t3 - t2]
+            garbage.append(b)
+        t4 = pc()
+        garbage.extend([cs, vs])
+        return buf[:data.size], [("make_output", t1 - t0), (f"map_to_gf_with_x{need}", t2 - t1),
+                                 ("recover_data", t3 - t2), (f"map_from_gf_append_x{need}", t4 - t3)]
 
-    def median_run(fn):
-        fn()
+    def faults():
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        return ru.ru_minflt + ru.ru_majflt
+
+    def runs_of(fn):
+        fn([])
         runs = []
         for _ in range(reps):
+            garbage = []
+            f0 = faults()
             t0 = pc()
-            res, split = fn()
-            runs.append((pc() - t0, split, res))
-        runs.sort(key=lambda x: x[0])
-        return runs[len(runs) // 2]
+            res, split = fn(garbage)
+            t = pc() - t0
+            f1 = faults()
+            del garbage[:]
+            t_free = pc() - t0 - t
+            runs.append((t, dict(split), res, f1 - f0, t_free))
+        return runs
 
-    t_w, sw, (mm, wc) = median_run(write)
-    t_r, sr, got = median_run(read)
+    ms = lambda x: round(x * 1e3, 3)  # noqa: E731
+
+    def summary(runs):
+        ts = sorted(r_[0] for r_ in runs)
+        med = sorted(runs, key=lambda x: x[0])[len(runs) // 2]
+        split = {k: ms(v) for k, v in med[1].items()}
+        split["other"] = round(ms(med[0]) - sum(split.values()), 3)
+        split["total"] = ms(med[0])
+        return {"total_ms": {"min": ms(ts[0]), "median": ms(med[0]), "max": ms(ts[-1])},
+                "split_ms": split,
+                "reps_ms": [dict({k: ms(v) for k, v in r_[1].items()}, total=ms(r_[0]), page_faults=r_[3],
+                                 deferred_free_ms=ms(r_[4])) for r_ in runs]}, med
+    try:
+        wruns = runs_of(write)
+        rruns = runs_of(read)
+    finally:
+        goroutines.shutdown()
+    wsum, wmed = summary(wruns)
+    rsum, rmed = summary(rruns)
+    mm, wc = wmed[2]
     ok_w = mm == m_fused and all(bytes(c) == bytes(x) for c, x in zip(wc, chunks))
-    ok_r = bytes(got) == data.tobytes()
+    ok_r = all(bytes(x[2]) == data.tobytes() for x in rruns[:1] + [rmed])
     L = chunks[0].size // 4
 
-    def alloc_write():
+    def alloc_write(garbage):
         bufs = [np.empty((data.size + 3) // 4, dtype=np.uint32)] + \
                [np.zeros(L, dtype=np.uint32) for _ in range(r)] + [gf._new_bytearray(None, 4 * L) for _ in range(total)]
         for b in bufs:
             np.frombuffer(b, dtype=np.uint8)[::4096] = 1
+        garbage.extend(bufs)
         return None, []
 
-    def alloc_read():
+    def alloc_read(garbage):
         bufs = [np.empty(L, dtype=np.uint32) for _ in range(2 * need)] + [gf._new_bytearray(None, 4 * L) for _ in range(need)] + \
                [np.empty(data.size + 16, dtype=np.uint8)]
         for b in bufs:
             np.frombuffer(b, dtype=np.uint8)[::4096] = 1
+        garbage.extend(bufs)
         return None, []
 
-    a_w = median_run(alloc_write)[0]
-    a_r = median_run(alloc_read)[0]
-    ms = lambda x: round(x * 1e3, 3)  # noqa: E731
-    return {"write_gibs": round(data.size / GIB / t_w, 2), "read_gibs": round(data.size / GIB / t_r, 2),
-            "split_ms": {"write": {"total": ms(t_w), "map_to_gf": ms(sw[0]), "split_vector": ms(sw[1]),
-                                   f"create_parity_x{r}": ms(sw[2]), f"map_from_gf_x{total}": ms(sw[3]),
-                                   "alloc_alone": ms(a_w)},
-                         "read": {"total": ms(t_r), f"map_to_gf_with_x{need}": ms(sr[0]), "recover_data": ms(sr[1]),
-                                  f"map_from_gf_append_x{need}": ms(sr[2]), "alloc_alone": ms(a_r)}},
+    a_w = sorted(x[0] for x in runs_of(alloc_write))[reps // 2]
+    a_r = sorted(x[0] for x in runs_of(alloc_read))[reps // 2]
+    return {"write_gibs": round(data.size / GIB / wmed[0], 2), "read_gibs": round(data.size / GIB / rmed[0], 2),
+            "write": wsum, "read": rsum, "reps": reps,
+            "fresh_alloc_alone_ms": {"write": ms(a_w), "read": ms(a_r),
+                                     "what": "the phases' fresh outputs allocated and first touched by one thread, "
+                                             "timed alone (median); not part of total"},
             "codec": dict(N.codec_info(), placement="device" if gf.codec_placement() else "host"),
             "verified": bool(ok_w and ok_r),
-            "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF "
-                    f"(write); {need} x MapToGFWith + RecoverData + {need} x MapFromGF appended (read); fresh "
-                    "outputs per call as Go's make(); CreateParity/RecoverData host->GPU->host; the codec on the "
-                    "host cores (placement host) or through the GPU (with_device_codec)"}
+            "what": f"multi_store.go unchanged: MapToGF + splitVector + {r} x CreateParity + {total} x MapFromGF on "
+                    f"{total} concurrent threads (write); make + {need} x MapToGFWith + RecoverData + {need} x "
+                    "MapFromGF appended (read); fresh outputs per call as Go's make(); CreateParity/RecoverData "
+                    "host->GPU->host; the codec on the host cores (placement host) or through the GPU "
+                    "(with_device_codec); split = the median call's phases, other = total - phases"}
 
 
 def digest_leg(data, need, total, chunks, have, out, med, g) -> dict:
@@ -1014,8 +1088,7 @@ def apply_kernel_name(need: int, rows: int, L: int, shard_bytes_span: int) -> st
     unless switched off; wide codes on the matrix cores, rs_apply_mfma.hip)."""
     kname = "rs_apply_kernel"
     if L < (1 << 30) and D.lib.slime_rs_kernel_pipeline(-1) == 1:
-        queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1 and \
-            (need <= 16 or os.environ.get("SLIME_RS_K32", "1")[:1] != "0")
+        queue = need <= 32 and D.lib.slime_rs_kernel_schedule(-1) == 1
         kname = "rs_apply_queue_kernel" if queue else "rs_apply_pipe_kernel"
     if _matrix_cores(need, rows) and shard_bytes_span < (1 << 32):
         kname = "rs_apply_mfma_kernel"  # wide codes (rs_apply_mfma.hip)
@@ -1052,6 +1125,75 @@ def c5_leg(args, dev: int, rank: int, world: int) -> dict:
             "kernel": f"{kname}<{need},vec>", "per_rank": per_rank,
             "frac_min": min((p["frac"] for p in per_rank if p["frac"]), default=None),
             "verified": all(p["verified"] for p in per_rank)}
+
+
+POOL_WORKLOADS = (  # (label, object MiB, pattern: 0 fused entry points, 1 the unchanged Go caller)
+    ("fused_64mib", 64, 0), ("fused_1mib", 1, 0), ("unchanged_caller_64mib", 64, 1))
+
+
+def pool_devices(world: int, ndev: int) -> list[int]:
+    """The GPUs of this job's ranks (one per rank, rank r on GPU r % ndev):
+    the device pool of the pooled leg may use exactly these."""
+    return sorted({r % max(1, ndev) for r in range(world)})
+
+
+def pooled_leg(args, rank: int, world: int, devices: list[int]) -> dict | None:
+    """The deployment shape of the Go library on a node: ONE proxy process
+    serving --pool-threads concurrent requests (main.go:107-109: 25), each a
+    PUT (Multi.writeChunks, multi_store.go:516-557) then a GET of the same
+    object (Multi.reconstruct's slow path, :185-252), every call through the
+    *_ex forms with SLIME_RS_ANY_DEVICE, so the library's device pool spreads
+    them over the GPUs of all N ranks (SLIME_RS_DEVICES = those GPUs).  Rank 0
+    drives it from C++ threads (tools/proxy_load.cpp: no GIL between calls, as
+    goroutines); the other ranks wait at a barrier.  Workloads: the fused
+    entry points at 64 MiB (the proxy's request-body bound) and 1 MiB, and
+    the unchanged caller (MapToGF + 4 x CreateParity + 12 x MapFromGF; 8 x
+    MapToGFWith + RecoverData + 8 x MapFromGF) at 64 MiB.  Per-device call
+    counts come from slime_rs_pool_calls.  PCIe-inclusive host memory in and
+    out: never `value`."""
+    batch.barrier()
+    out = None
+    if rank == 0:
+        import ctypes
+
+        from slime_amd import _native as N
+        path = os.path.join(ROOT, "tools", "libproxy_load.so")
+        lib = ctypes.CDLL(path)
+        lib.proxy_load.restype = ctypes.c_int
+        lib.proxy_load.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_double, ctypes.c_uint64,
+                                   ctypes.POINTER(ctypes.c_double)]
+        need, total, erase = 8, 12, [0, 1, 2, 3]
+        have = [i for i in range(total) if i not in erase][:need]
+        c_have = (ctypes.c_int * need)(*have)
+        legs, ok = {}, True
+        for label, mib, pattern in POOL_WORKLOADS:
+            before = [N.pool_calls(d)[0] for d in devices]
+            res = (ctypes.c_double * 10)()
+            rc = lib.proxy_load(args.pool_threads, mib << 20, need, total, c_have, pattern, args.pool_seconds,
+                                0x9001 + mib, res)
+            after = [N.pool_calls(d)[0] for d in devices]
+            reqs, wall = res[0], res[1]
+            good = rc == 0 and res[2] == 1.0
+            ok = ok and good
+            legs[label] = {
+                "object_mib": mib, "requests": int(reqs), "seconds": round(wall, 3),
+                "gibs": round(2 * reqs * (mib << 20) / GIB / wall, 2) if wall else None,
+                "requests_per_s": round(reqs / wall, 1) if wall else None,
+                "calls_per_s": round(res[3] / wall, 1) if wall else None,
+                "put_ms": {"p50": round(res[4], 3), "p99": round(res[5], 3)},
+                "get_ms": {"p50": round(res[6], 3), "p99": round(res[7], 3)},
+                "per_device_calls": {str(d): a - b for d, a, b in zip(devices, after, before)},
+                "failed_calls": int(res[8]), "status": rc, "setup_s": round(res[9], 2), "verified": good}
+        out = {"threads": args.pool_threads, "devices": devices, "need": need, "total": total, "erased": erase,
+               "workloads": legs, "verified": ok,
+               "what": "one process, --pool-threads concurrent PUT (writeChunks) + GET (reconstruct) requests per "
+                       "thread loop, every call through the cgo shim's *_ex forms with SLIME_RS_ANY_DEVICE over the "
+                       "GPUs of all N ranks (tools/proxy_load.cpp); gibs = object bytes written + read per second; "
+                       "per-request p50/p99 ms; verified = each thread's first and last GET returned its object, "
+                       "its chunks were stable, and the unchanged caller's chunks equal the fused path's"}
+    batch.barrier()
+    return out
 
 
 def shape_leg(args, name: str, dev: int, rank: int, world: int, reuse: torch.Tensor | None) -> dict:
@@ -1124,6 +1266,10 @@ def main():
         print(f"bench.py: {world} ranks (local rank {local}) but {ndev} visible GPU(s); one rank per GPU",
               file=sys.stderr, flush=True)
         sys.exit(2)
+    devices = pool_devices(world, ndev)
+    if args.pooled and "SLIME_RS_DEVICES" not in os.environ:
+        # The library reads it once, at its first host call (none yet).
+        os.environ["SLIME_RS_DEVICES"] = ",".join(map(str, devices))
     if args.dry_run:
         first, count = batch.partition(args.global_objects, world, rank) if args.global_objects else \
             (rank * args.objects, args.objects)
@@ -1140,7 +1286,11 @@ def main():
                               "shapes": {n: {"need": PRESETS[n][0], "total": PRESETS[n][1], "object_mib": PRESETS[n][2],
                                              "objects_per_rank": PRESETS[n][3], "scaling": "weak"}
                                          for n in args.shape_legs.split(",") if n and
-                                         PRESETS[n][:3] != (args.need, args.total, args.object_mib)}}), flush=True)
+                                         PRESETS[n][:3] != (args.need, args.total, args.object_mib)},
+                              "host_path.pooled": None if not args.pooled else
+                              {"driver_rank": 0, "threads": args.pool_threads, "devices": devices,
+                               "pool_env": os.environ.get("SLIME_RS_DEVICES"),
+                               "workloads": [w[0] for w in POOL_WORKLOADS]}}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -1199,6 +1349,9 @@ def main():
 
     if want_host and args.host_order == "before-free":
         host = run_host_leg()
+    # The proxy's shape, at every N, while the batch buffers are still held
+    # (freed VRAM is wiped by the same DMA engines the host path uses).
+    pooled = pooled_leg(args, rank, world, devices) if args.pooled else None
     # After the host leg: the probe's buffers go back to the driver, whose
     # wipe of freed VRAM would slow the host leg's DMA (DESIGN.md End-to-end).
     ceilings = stream_ceilings(dev, sb.stream) if args.ceilings else None
@@ -1301,13 +1454,16 @@ def main():
         line["device"] = board_info(dev)
         if host is not None:
             line["host_path"] = host
+        if pooled is not None:  # at every N (the N = 1 host legs above run only at N = 1)
+            line.setdefault("host_path", {})["pooled"] = pooled
         if cpu_sample is not None:
             line["cpu_baseline"] = cpu_baseline(cpu_sample, f"object 0 of this run's batch ({args.object_mib} MiB)",
                                                 need, total, erase, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if bad or (c5 is not None and not c5["verified"]) or not all(v["verified"] for v in shapes.values()):
+    if bad or (c5 is not None and not c5["verified"]) or not all(v["verified"] for v in shapes.values()) or \
+            (pooled is not None and not pooled["verified"]):
         sys.exit(3)
 
 

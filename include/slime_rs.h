@@ -84,26 +84,13 @@ typedef struct slime_rs_call {
   char *detail;      /* optional: receives this call's failure detail, NUL-terminated ("" on success) */
   size_t detail_cap; /* bytes at detail (0: no detail wanted) */
 } slime_rs_call_t;
-/* How the Go-API entry points (CreateParity/CreateParities/RecoverData) move
- * host rows to the GPU and back (process-wide; env SLIME_RS_HOST_PIPE sets
- * the initial value):
- *   0 staged   - column-chunked 3-stage ring through pinned staging buffers,
- *                H2D / kernel / D2H of one chunk overlapping the host copies
- *                of the others (default);
- *   1 register - page-lock the caller's rows for the call and DMA directly
- *                (falls back to staged when registration is refused);
- *   2 direct   - one-shot pageable hipMemcpy (measurement reference).
- * mode < 0 queries: returns the current mode.  Otherwise returns 0, or
- * SLIME_RS_ERR_INVALID_ARG for an unknown mode.  No reference counterpart:
- * the Go implementation computes in place on host memory. */
-int slime_rs_host_pipeline(int mode);
-/* Kernel form for shards/chunks under 4 GiB (process-wide; env SLIME_RS_PIPE=0
- * sets the initial value): 1 = software-pipelined kernels (default), 0 = the
- * non-pipelined forms that larger shards always take.  mode < 0 queries.
- * Results are identical; the parity tests run both. */
+/* Kernel form for shards/chunks under 4 GiB (process-wide): 1 =
+ * software-pipelined kernels (default), 0 = the non-pipelined forms that
+ * larger shards always take.  mode < 0 queries.  Results are identical; the
+ * parity tests run both. */
 int slime_rs_kernel_pipeline(int mode);
-/* Work schedule of the pipelined kernels for k <= 32 (process-wide; env
- * SLIME_RS_QUEUE=0/1/2 sets the initial value): 1 = dynamic, waves take units
+/* Work schedule of the pipelined kernels for k <= 32 (process-wide): 1 =
+ * dynamic, waves take units
  * of work from ticket counters, except inside a graph capture, where the
  * static kernels are captured (default); 2 = dynamic inside captures too --
  * the captured launch keeps a counter set for the graph's life (returned to
@@ -113,8 +100,7 @@ int slime_rs_kernel_pipeline(int mode);
  * every mode. */
 int slime_rs_kernel_schedule(int mode);
 /* Wide codes (k >= 33, or 17 <= k <= 32 with k x rows >= 128; up to 32 output
- * rows and k <= 112) on the matrix cores
- * (process-wide; env SLIME_RS_MFMA=0 sets the initial value): 1 = the exact
+ * rows and k <= 112) on the matrix cores (process-wide): 1 = the exact
  * int8-limb kernel on v_mfma_i32_16x16x64_i8 (default), 0 = the VALU kernels.
  * mode < 0 queries.  Results are identical; the parity tests run both. */
 int slime_rs_kernel_matrix_cores(int mode);
@@ -139,8 +125,8 @@ int slime_gf_map_to_gf(const uint8_t *in, uint64_t len, uint32_t *mapping, uint3
 int slime_gf_map_to_gf_with(const uint8_t *in, uint64_t len, uint32_t n, uint32_t *out);
 /* gf.MapFromGF (internal/rs/gf/map.go:103). out holds 4*count bytes. */
 int slime_gf_map_from_gf(uint32_t n, const uint32_t *in, uint64_t count, uint8_t *out);
-/* Where the three host-memory codec calls above run (process-wide; env
- * SLIME_RS_CODEC=device sets the initial value): 0 = on the host cores, in
+/* Where the three host-memory codec calls above run (process-wide): 0 = on
+ * the host cores, in
  * place on the caller's buffers (AVX2 passes split over the library's copy
  * pool; default -- the codec is a byte swap, an XOR and a compare, and the
  * bytes are in host memory); 1 = through the GPU codec kernels and the pinned
@@ -185,7 +171,9 @@ int slime_rs_create_parities(const uint32_t *const *data, const uint64_t *lens, 
  * code-row index indices[i]; out[0..nchunks-1] each receive lens[0] words of
  * data rows 0..nchunks-1.  Only the erased data rows (those not among
  * indices) are computed on the GPU; a surviving data row's inverse row is a
- * unit row, so its output is that chunk mod p, written on the host. */
+ * unit row, so its output is that chunk mod p, written on the host.  Output
+ * rows may overlap the chunks (an in-place repair): survivors an output
+ * overlaps are read from copies taken first. */
 int slime_rs_recover_data(const uint32_t *const *chunks, const uint64_t *lens, int nchunks, const int *indices,
                           int nindices, uint32_t *const *out);
 

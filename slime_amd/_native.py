@@ -73,7 +73,6 @@ SIGNATURES = [
     ("slime_rs_device_count", ctypes.c_int, []),
     ("slime_rs_select_device", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_selected_device", ctypes.c_int, []),
-    ("slime_rs_host_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_matrix_cores", ctypes.c_int, [ctypes.c_int]),

@@ -128,8 +128,11 @@ double placement_probe(int device, uint8_t* va, uint64_t bytes) {
   hipStream_t s = nullptr;
   hipEvent_t ev[3] = {};
   double best = 0;
-  bool ok = hipMemcpy(d, table.data(), table.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-            hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  // Everything on a private non-blocking stream, waited for there only: no
+  // other stream (torch's, or a capture in progress on another thread) is
+  // synchronised.
+  bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+            hipMemcpyAsync(d, table.data(), table.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess;
   for (auto& e : ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   if (ok) {
     ApplyLaunch a;
@@ -271,8 +274,7 @@ int slime_rs_probe_placement(void* ptr, uint64_t bytes, int device, double* gbs)
     if (p0 < (uintptr_t)base || p1 > (uintptr_t)base + size)
       return fail(Status::InvalidArg, "probe_placement: range exceeds its allocation");
   }
-  *gbs = placement_probe(device, (uint8_t*)ptr, bytes);
-  if (hipError_t e = hipDeviceSynchronize()) return fail_hip(e, "probe_placement");
+  *gbs = placement_probe(device, (uint8_t*)ptr, bytes);  // synchronises its own stream only
   return 0;
 }
 

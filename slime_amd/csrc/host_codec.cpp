@@ -153,14 +153,16 @@ __attribute__((target("avx2"))) void mod_avx2(const uint32_t* in, uint64_t count
 
 // Output buffers of the Go API are fresh (Go's make, a Python bytearray or
 // numpy array): their first touch is this pass, one 4 KiB page fault at a
-// time.  Ranges of at least 4 MiB are advised to fault as 2 MiB pages
-// (transparent huge pages in "madvise" mode) before the pass writes them --
-// a hint on the 2 MiB-aligned interior only, ignored where it does not apply
-// (env SLIME_RS_CODEC_HUGEPAGE=0 turns it off).
+// time.  With env SLIME_RS_CODEC_HUGEPAGE=1, ranges of at least 4 MiB are
+// advised to fault as 2 MiB pages (transparent huge pages in "madvise" mode)
+// before the pass writes them -- a hint on the 2 MiB-aligned interior only.
+// Off by default: the buffers belong to the caller (under cgo, the Go heap,
+// whose huge-page advice the Go runtime manages itself) and the advice would
+// outlive the call.
 void advise_huge(void* p, uint64_t bytes) {
   static const bool on = [] {
     const char* e = getenv("SLIME_RS_CODEC_HUGEPAGE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   constexpr uintptr_t kHuge = 2u << 20;
   if (!on || bytes < (4u << 20)) return;

@@ -25,15 +25,9 @@ namespace {
 constexpr size_t kPieceMax = 512u << 10, kPieceMin = 64u << 10;
 // Copies below 2 MiB stay on the caller: a wake-up costs more than it saves
 // there (1 MiB host calls ran 10-20% slower with a 512 KiB threshold,
-// profiles/r04/s18_serialab).  Env SLIME_RS_COPY_SERIAL_KIB, read once.
-size_t serial_below() {
-  static const size_t b = [] {
-    const char* e = getenv("SLIME_RS_COPY_SERIAL_KIB");
-    const long v = e ? atol(e) : 2048;
-    return (size_t)(v < 0 ? 0 : v) << 10;
-  }();
-  return b;
-}
+// profiles/r04/s18_serialab).
+constexpr size_t kSerialBelow = 2u << 20;
+size_t serial_below() { return kSerialBelow; }
 // After a job a worker spins this long for the next one before it sleeps.
 // A host call posts one job per window (8-16 MiB, a fraction of a ms of
 // copying); a worker that went to sleep between windows can take longer to
@@ -80,20 +74,7 @@ void stream_copy(void* dst, const void* src, size_t n) {
   _mm_sfence();
 }
 
-bool use_nt() {
-  static const bool on = [] {
-    const char* e = getenv("SLIME_RS_COPY_NT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-void copy_piece(const CopyItem& it) {
-  if (use_nt())
-    stream_copy(it.dst, it.src, it.bytes);
-  else
-    memcpy(it.dst, it.src, it.bytes);
-}
+void copy_piece(const CopyItem& it) { stream_copy(it.dst, it.src, it.bytes); }
 
 size_t drain(Job* j) {
   size_t did = 0;

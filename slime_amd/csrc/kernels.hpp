@@ -38,21 +38,14 @@ struct ApplyLaunch {
 };
 
 // Matrix-core apply kernel: whether this launch can take it (table present,
-// mode on, k at or above the tuning threshold, shape and spans supported),
-// and the launch.  Process-wide mode: env SLIME_RS_MFMA=0 sets it off;
-// slime_rs_kernel_matrix_cores() switches it.
+// mode on, mfma_wanted, shape and spans supported), and the launch.
+// Process-wide mode, on by default: slime_rs_kernel_matrix_cores() switches it.
 bool mfma_eligible(const ApplyLaunch& a);
 hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream);
 int matrix_core_mode();
 void set_matrix_core_mode(int m);
-// Smallest k whose byte-path launches take the matrix cores (env
-// SLIME_RS_MFMA_MINK, tuning; default 33: the symbol path also takes them for
-// 17 <= k <= 32 when k * rows >= 128, rs_apply_mfma.hip) and the kernel form (env SLIME_RS_MFMA_MODE: 2 K-step refill,
-// the product; 1 two tile buffers; 0 no prefetch).
-uint32_t mfma_min_k();
-int mfma_kernel_form();
 // The product rule (rs_apply_mfma.hip): k >= 33, or 17 <= k <= 32 with
-// k * rows >= 128 multiply-accumulates per column; SLIME_RS_MFMA_MINK forces k >= n.
+// k * rows >= 128 multiply-accumulates per column.
 bool mfma_wanted(uint32_t k, uint32_t rows);
 
 // Row stride (words) of a device coefficient table: k rounded up to 16 words,
@@ -61,20 +54,9 @@ inline uint32_t coeff_stride(uint32_t k) { return (k + 15u) & ~15u; }
 
 hipError_t launch_apply(const ApplyLaunch& a, hipStream_t stream);
 
-// Launch geometry of the apply kernels (rs_apply.hip): resident 256-lane
-// blocks per launch (0 = per-k default) and object segments in flight; env
-// overrides for the tuning harness only.
-struct ApplyGeometry {
-  uint64_t target, inflight;
-};
-const ApplyGeometry& apply_geometry();
-
 // 17 <= k <= 32, 16-byte-aligned-capable layouts, shards under 4 GiB: the
 // pipelined k-template kernel instantiated for wide k (rs_apply_k32.hip).
 hipError_t launch_pipe_k32(const ApplyLaunch& a, hipStream_t stream);
-// Whether 17 <= k <= 32 take the k-template kernels (default) or the wide
-// 16-shard chunk kernels (env SLIME_RS_K32=0, read once: tuning A/B).
-bool k32_kernels();
 
 // Kernel form for shards/chunks under 4 GiB: software-pipelined (default) or
 // not (the form larger ones always take).  Process-wide; see rs_apply.hip.
@@ -138,18 +120,12 @@ inline uint64_t queue_blocks(uint64_t full, uint64_t units) {
 // capped at the object's groups of 4*C tiles of U 16-byte vectors per lane
 // (in-process sweeps, profiles/r02/s61_spread/, s62_spread2/: best S = 1 at
 // 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
-// Env SLIME_RS_SEGMENTS forces a count (tuning).  0 when the launch has too
-// many units for 32-bit tickets, or at most one block's (below): the caller
-// takes the static kernel.
+// 0 when the launch has too many units for 32-bit tickets, or at most one
+// block's (below): the caller takes the static kernel.
 inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C) {
   const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
   const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
-  static const uint64_t forced = [] {
-    const char* e = getenv("SLIME_RS_SEGMENTS");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? (uint64_t)v : 0ull;
-  }();
-  uint64_t S = forced ? forced : (64 + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
+  uint64_t S = (64 + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
   if (S > groups) S = groups ? groups : 1;
   const uint64_t B = (groups + S - 1) / S;
   const uint64_t units = (uint64_t)nobj * S * B * 4;

@@ -35,14 +35,9 @@ namespace slime {
 // about 256 independent object segments in flight -- 128 x 256 MiB objects
 // reach 6.1 TB/s unsegmented, 32 x 64 MiB objects need 8 segments each to get
 // from 5.08 to 5.54 TB/s (profiles/r01/segs/) -- and at least 1024 vectors
-// (4 U=4 tiles) per segment.  Env SLIME_RS_SEGMENTS forces a count (tuning).
+// (4 U=4 tiles) per segment.
 uint32_t object_segments(uint32_t nobj, uint64_t ncols) {
-  static const uint64_t forced = [] {
-    const char* e = getenv("SLIME_RS_SEGMENTS");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? (uint64_t)v : 0ull;
-  }();
-  const uint64_t want = forced ? forced : (256 + nobj - 1) / nobj;
+  const uint64_t want = (256 + nobj - 1) / nobj;
   const uint64_t max_s = (ncols >> 2) / 1024 ? (ncols >> 2) / 1024 : 1;
   return (uint32_t)(want < max_s ? want : max_s);
 }
@@ -52,7 +47,7 @@ using apply::kBlock;
 using apply::rs_apply_kernel;
 
 // Non-pipelined vectorised kernel (the fallback for shards >= 4 GiB and
-// SLIME_RS_PIPE=0; tools/apply_variants.py sweep, DESIGN.md "Tuning"): each wave streams U KiB of every shard per step with
+// slime_rs_kernel_pipeline(0); tools/apply_variants.py sweep, DESIGN.md "Tuning"): each wave streams U KiB of every shard per step with
 // non-temporal loads and stores (read-once/write-once streams).  U = 4 up to
 // k = 10 (<= 192 VGPRs, 2 waves/SIMD at the 512-block grid), U = 2 beyond so
 // the k x U x 16 B of symbols stay in registers without dropping below that.
@@ -65,35 +60,13 @@ constexpr bool kNtStores = true;
 
 }  // namespace
 
-static uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* e = getenv(name);
-  const long long v = e ? atoll(e) : 0;
-  return v > 0 ? (uint64_t)v : dflt;
-}
-
-bool k32_kernels() {
-  static const bool on = [] {
-    const char* e = getenv("SLIME_RS_K32");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-const ApplyGeometry& apply_geometry() {
-  static const ApplyGeometry g{env_u64("SLIME_RS_GRID_TARGET", 0), env_u64("SLIME_RS_OBJ_INFLIGHT", 65535)};
-  return g;
-}
-
 namespace {
 
-// Launch geometry: `target` resident 256-lane blocks (8 per CU at 2048 on 256
-// CUs), spread over at most `inflight` objects at a time.  The default block
-// budget is 512, and 256 for 9 <= k <= 12 (U = 4 at k = 9, 10 holds 36-40 KiB
-// of symbols per wave; fewer, fatter waves measured +5..18% at 10/14 and
-// +2% at 12/16 on 1 GiB objects, profiles/r01/gridk/).  Environment
-// overrides exist for the tuning harness only.
-using Geometry = ApplyGeometry;
-const Geometry& geometry() { return apply_geometry(); }
+// Launch geometry: `target` resident 256-lane blocks over the batch's object
+// segments (grid.y, at most 65535 at a time).  The block budget is 512, and
+// 256 for 9 <= k <= 12 (U = 4 at k = 9, 10 holds 36-40 KiB of symbols per
+// wave; fewer, fatter waves measured +5..18% at 10/14 and +2% at 12/16 on
+// 1 GiB objects, profiles/r01/gridk/).
 template <int K>
 constexpr uint64_t default_blocks() {
   return K >= 9 && K <= 12 ? 256 : 512;
@@ -103,12 +76,10 @@ template <int K, bool VEC>
 hipError_t launch_k(const ApplyLaunch& a, hipStream_t stream) {
   constexpr int U = unroll_for<K>();
   const uint64_t per_block = VEC && K > 0 ? 4ull * kBlock * U : (uint64_t)kBlock;
-  const Geometry& geo = geometry();
   const uint32_t nseg = VEC && K > 0 ? object_segments(a.nobj, a.ncols) : 1u;
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : default_blocks<K>();
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  const uint64_t target = default_blocks<K>();
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
@@ -141,12 +112,10 @@ template <int K>
 hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
   constexpr int U = pipe_unroll<K>();
   const uint64_t per_block = 4ull * kBlock * U;
-  const Geometry& geo = geometry();
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : pipe_blocks<K>();
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  const uint64_t target = pipe_blocks<K>();
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
@@ -184,8 +153,7 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
   *launched = false;
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
-  const Geometry& geo = geometry();
-  const uint64_t blocks = queue_blocks(geo.target ? geo.target : kQueueBlocks, queue_units(a.nobj, a.ncols, U, C, spread));
+  const uint64_t blocks = queue_blocks(kQueueBlocks, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(
       stream,
       [&](uint32_t* set) {
@@ -451,23 +419,15 @@ hipError_t with_tickets(hipStream_t stream, const std::function<hipError_t(uint3
 }
 
 // Kernel form (process-wide): the software-pipelined kernels (default) or
-// the non-pipelined forms that shards/chunks of 4 GiB and more always take.
-// Env SLIME_RS_PIPE=0 sets the initial value (read once, not per launch);
+// the non-pipelined forms that shards/chunks of 4 GiB and more always take;
 // slime_rs_kernel_pipeline() switches it (the parity tests cover both forms
 // in one process).
-static std::atomic<int> g_pipelined{[] {
-  const char* e = getenv("SLIME_RS_PIPE");
-  return e && e[0] == '0' ? 0 : 1;
-}()};
+static std::atomic<int> g_pipelined{1};
 bool pipelined_kernels() { return g_pipelined.load(std::memory_order_relaxed) != 0; }
 // Work schedule of the pipelined kernels (process-wide): 1 = dynamic outside
 // graph captures, static inside (default); 2 = dynamic in captures too; 0 =
-// static shares.  Env SLIME_RS_QUEUE=0/1/2 sets the initial value;
-// slime_rs_kernel_schedule() switches it.
-static std::atomic<int> g_queue_mode{[] {
-  const char* e = getenv("SLIME_RS_QUEUE");
-  return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
-}()};
+// static shares.  slime_rs_kernel_schedule() switches it.
+static std::atomic<int> g_queue_mode{1};
 int queue_mode() { return g_queue_mode.load(std::memory_order_relaxed); }
 bool queue_allowed(hipStream_t s) {
   const int m = queue_mode();
@@ -501,10 +461,8 @@ hipError_t launch_wide_k(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t per_block = 4ull * kBlock;
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  const Geometry& geo = geometry();
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : 512;
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  const uint64_t target = 512;
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
@@ -525,10 +483,8 @@ hipError_t launch_wide_pipe(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t per_block = 4ull * kBlock;
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  const Geometry& geo = geometry();
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : (a.k <= 32 ? 256 : 1024);
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  const uint64_t target = a.k <= 32 ? 256 : 1024;
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
@@ -540,7 +496,7 @@ hipError_t launch_wide_pipe(const ApplyLaunch& a, hipStream_t stream) {
 }
 
 hipError_t launch_wide(const ApplyLaunch& a, hipStream_t stream) {
-  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_pipe_k32(a, stream);
+  if (pipe_ok(a) && a.k <= 32) return launch_pipe_k32(a, stream);
   if (pipe_ok(a)) return a.rows <= 8 ? launch_wide_pipe<8>(a, stream) : launch_wide_pipe<16>(a, stream);
   return a.k <= 32 ? launch_wide_k<32, 8>(a, stream) : launch_wide_k<16, 16>(a, stream);
 }

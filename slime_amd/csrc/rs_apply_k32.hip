@@ -28,8 +28,7 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
   *launched = false;
   const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
   if (!spread) return hipSuccess;
-  const ApplyGeometry& geo = apply_geometry();
-  const uint64_t blocks = queue_blocks(geo.target ? geo.target : 256, queue_units(a.nobj, a.ncols, U, C, spread));
+  const uint64_t blocks = queue_blocks(256, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(
       stream,
       [&](uint32_t* set) {
@@ -52,13 +51,10 @@ hipError_t launch_k32(const ApplyLaunch& a, hipStream_t stream) {
   constexpr int U = K <= 24 ? 2 : 1;
   constexpr uint64_t kBlocks = 256;
   const uint64_t per_block = 4ull * apply::kBlock * U;
-  const ApplyGeometry& geo = apply_geometry();
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const uint64_t target = geo.target ? geo.target : kBlocks;
-  uint64_t gx = (target + gy - 1) / gy;
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  uint64_t gx = (kBlocks + gy - 1) / gy;
   const uint64_t need = (a.ncols / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;

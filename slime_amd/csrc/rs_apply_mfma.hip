@@ -3,9 +3,6 @@
 // product on v_mfma_i32_16x16x64_i8, for plans whose table carries the digit
 // fragments (built for k >= 17 with rows <= 32, k <= 112: mfma_table.hpp).
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
-#include <string.h>
-
 #include <atomic>
 
 #include "kernels.hpp"
@@ -13,36 +10,18 @@
 
 namespace slime {
 
-// Process-wide switch (env SLIME_RS_MFMA=0 sets the initial value;
-// slime_rs_kernel_matrix_cores() switches it).  Which shapes take the matrix
-// cores is mfma_wanted() below; env SLIME_RS_MFMA_MINK=n replaces that rule
-// by k >= n (tuning A/B only).
-static std::atomic<int> g_mfma{[] {
-  const char* e = getenv("SLIME_RS_MFMA");
-  return e && e[0] == '0' ? 0 : 1;
-}()};
+// Process-wide switch (slime_rs_kernel_matrix_cores()); on by default.
+// Which shapes take the matrix cores is mfma_wanted() below.
+static std::atomic<int> g_mfma{1};
 int matrix_core_mode() { return g_mfma.load(std::memory_order_relaxed); }
 void set_matrix_core_mode(int m) { g_mfma.store(m, std::memory_order_relaxed); }
-// SLIME_RS_MFMA_MINK, or 0 when unset (the product rule below).
-static uint32_t forced_min_k() {
-  static const uint32_t v = [] {
-    const char* e = getenv("SLIME_RS_MFMA_MINK");
-    const long long x = e ? atoll(e) : 0;
-    return x > 0 ? (uint32_t)x : 0u;
-  }();
-  return v;
-}
-uint32_t mfma_min_k() { return forced_min_k() ? forced_min_k() : 33u; }
 
 // Which launches take the matrix cores (product rule, measured on one box,
 // profiles/r03/s37_mfma_k32/): every k >= 33, and 17 <= k <= 32 when the
 // column's k x rows multiply-accumulates reach 128 -- 24/32 0.646 -> 0.739,
 // 32/40 0.676 -> 0.738, while 20/24 (80 per column) ties and 17/20 (51)
 // loses 4% (0.739 -> 0.709).
-bool mfma_wanted(uint32_t k, uint32_t rows) {
-  if (forced_min_k()) return k >= forced_min_k();
-  return k >= 33 || (k >= 17 && k * rows >= 128);
-}
+bool mfma_wanted(uint32_t k, uint32_t rows) { return k >= 33 || (k >= 17 && k * rows >= 128); }
 
 bool mfma_eligible(const ApplyLaunch& a) {
   if (!a.mfma || !a.vec_ok || !matrix_core_mode() || !mfma_wanted(a.k, a.rows)) return false;
@@ -56,44 +35,10 @@ bool mfma_eligible(const ApplyLaunch& a) {
 
 namespace {
 
-constexpr bool kNtLoads = true;
-constexpr bool kNtStores = true;
-
-// Kernel form (tuning A/B; env SLIME_RS_MFMA_MODE): 2 = one tile of data
-// registers refilled K step by K step behind the math (default), 1 = two
-// tile buffers, 0 = no prefetch.
-}  // namespace
-int mfma_kernel_form() {
-  static const int m = [] {
-    const char* e = getenv("SLIME_RS_MFMA_MODE");
-    const int v = e ? atoi(e) : 2;
-    return v >= 0 && v <= 2 ? v : 2;
-  }();
-  return m;
-}
-namespace {
-
-// Cache policy A/B of the refill form (env SLIME_RS_MFMA_NT, two digits: loads,
-// stores; 1 = non-temporal, the product "11").
-int mfma_nt() {
-  static const int v = [] {
-    const char* e = getenv("SLIME_RS_MFMA_NT");
-    if (!e || strlen(e) != 2) return 3;
-    return (e[0] == '1' ? 2 : 0) | (e[1] == '1' ? 1 : 0);
-  }();
-  return v;
-}
-
-template <int KS, int MODE, bool NTL = kNtLoads, bool NTS = kNtStores>
-void launch_mode(const ApplyLaunch& a, hipStream_t stream, dim3 grid, uint32_t lds, uint32_t nseg) {
-  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, NTL, NTS, MODE>), grid, dim3(apply::kBlock), lds,
-                     stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride, a.out_shard_stride,
-                     a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, nseg);
-}
-
 // Static tile walk only: a dynamic-schedule form (TicketWalk units of 4 KiB
 // per shard, the refill streaming across objects) measured 0-6% slower than
 // this walk at 40/48, 48/64, 64/80 and 80/100 (profiles/r03/s33_mfma_queue_bytes/).
+// Non-temporal loads and stores (read-once / write-once streams).
 template <int KS>
 hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint32_t mt = mfma::mtiles(a.rows);
@@ -101,28 +46,16 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint64_t per_block = 4ull * 16 * 4;  // 4 waves x 16 vectors
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
-  const ApplyGeometry& geo = apply_geometry();
-  uint64_t gy = nwork < geo.inflight ? nwork : geo.inflight;
-  if (gy > 65535) gy = 65535;
-  const int mode = mfma_kernel_form();
-  const uint64_t target = geo.target ? geo.target : 256ull * apply::mfma_waves(KS, mode);  // resident blocks
+  const uint64_t gy = nwork < 65535 ? nwork : 65535;
+  const uint64_t target = 256ull * apply::kMfmaWaves;  // resident blocks
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  const dim3 grid((uint32_t)gx, (uint32_t)gy);
-  switch (mode) {
-    case 0: launch_mode<KS, 0>(a, stream, grid, lds, nseg); break;
-    case 1: launch_mode<KS, 1>(a, stream, grid, lds, nseg); break;
-    default:
-      switch (mfma_nt()) {
-        case 0: launch_mode<KS, 2, false, false>(a, stream, grid, lds, nseg); break;
-        case 1: launch_mode<KS, 2, false, true>(a, stream, grid, lds, nseg); break;
-        case 2: launch_mode<KS, 2, true, false>(a, stream, grid, lds, nseg); break;
-        default: launch_mode<KS, 2>(a, stream, grid, lds, nseg); break;
-      }
-      break;
-  }
+  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, true, true>), dim3((uint32_t)gx, (uint32_t)gy),
+                     dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
+                     a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
+                     a.rows, a.k, nseg);
   return hipGetLastError();
 }
 

@@ -90,18 +90,14 @@ __device__ void mfma_recombine4(const i32x4&, const i32x4&, const i32x4&, const 
 #endif
 __host__ __device__ constexpr int mfma_w4_max_ks() { return SLIME_MFMA_W4_MAX_KS; }
 
-// Waves per SIMD the kernel is compiled for (registers permitting): two for
-// the no-prefetch and refill forms (W = 4 up to k = 64, W = 2 above: at most
-// 64 data VGPRs, the accumulators in VGPRs), two for the two-buffer form up
-// to two K steps, else one; form 3 is the refill form at one wave per SIMD
-// (for kernels whose extra state does not fit two).
+// Columns per lane of a tile: 4 up to k = 64, 2 above (at most 64 data VGPRs,
+// the accumulators in VGPRs), so the refill walk runs at two waves per SIMD.
 __host__ __device__ constexpr int mfma_width(int ks) { return ks <= mfma_w4_max_ks() ? 4 : 2; }
 // Column passes per K loop (mfma_rows): 2 where four-column tiles need their
 // accumulators halved to fit two waves per SIMD.
 __host__ __device__ constexpr int mfma_halves(int ks) { return ks > 4 && ks <= mfma_w4_max_ks() ? 2 : 1; }
-__host__ __device__ constexpr int mfma_waves(int ks, int mode) {
-  return mode == 3 ? 1 : (mode != 1 || ks <= 2 ? 2 : 1);
-}
+// Waves per SIMD the matrix-core kernels are compiled for.
+constexpr int kMfmaWaves = 2;
 
 template <int W>
 using vec_t = uint32_t __attribute__((ext_vector_type(W)));
@@ -251,11 +247,11 @@ __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __re
 }
 
 // The tile walk of one wave over columns [c0, c1) of one object (c0, c1
-// multiples of W): tiles t = wave, wave + nwaves, ...  MODE 0: load a tile,
-// compute it; 1: two tile buffers, the next tile's loads issued before the
-// current tile's math; 2: one tile buffer refilled K step by K step behind
-// the math (mfma_rows).
-template <int KS, int W, bool NTL, bool NTS, int MODE, bool BSWAP, class Pre>
+// multiples of W): tiles t = wave, wave + nwaves, ..., one tile buffer
+// refilled K step by K step behind the math (mfma_rows).  The refill beat two
+// tile buffers and no prefetch at every K step count (profiles/r03/
+// s33_mfma_queue_bytes/, s35_mfma_bytes/), which were removed.
+template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class Pre>
 __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob,
                                           const uint32_t (&soff)[KS][4], const i32x4* __restrict__ lfrag,
                                           const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
@@ -269,44 +265,18 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
     const uint32_t c = col_of(tile);
     return (c < c1 ? c : c1 - W) << 2;
   };
-  if constexpr (MODE == 1) {
-    vec_t<W> xa[KS][4], xb[KS][4];
-    uint32_t t = wave;
-    if (t < ntiles) mfma_load_tile<KS, W, NTL>(xa, ib, soff, colb_of(t));
-    while (t < ntiles) {
-      const uint32_t t1 = t + nwaves;
-      mfma_load_tile<KS, W, NTL>(xb, ib, soff, colb_of(t1 < ntiles ? t1 : t));
-      mfma_tile<KS, W, NTL, NTS, false, BSWAP>(xa, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io, pre);
-      t = t1;
-      if (t >= ntiles) break;
-      const uint32_t t2 = t + nwaves;
-      mfma_load_tile<KS, W, NTL>(xa, ib, soff, colb_of(t2 < ntiles ? t2 : t));
-      mfma_tile<KS, W, NTL, NTS, false, BSWAP>(xb, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io, pre);
-      t = t2;
-    }
-  } else if constexpr (MODE == 2 || MODE == 3) {
-    vec_t<W> x[KS][4];
-    uint32_t t = wave;
-    if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));
-    while (t < ntiles) {
-      const uint32_t tn = t + nwaves;
-      if (tn < ntiles)
-        mfma_tile<KS, W, NTL, NTS, true, BSWAP>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
-                                                colb_of(t), col_of(t) < c1, io, pre);
-      else
-        mfma_tile<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                                 col_of(t) < c1, io, pre);
-      t = tn;
-    }
-  } else {
-    for (uint32_t t = wave; t < ntiles; t += nwaves) {
-      vec_t<W> x[KS][4];
-      mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));
+  vec_t<W> x[KS][4];
+  uint32_t t = wave;
+  if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));
+  while (t < ntiles) {
+    const uint32_t tn = t + nwaves;
+    if (tn < ntiles)
+      mfma_tile<KS, W, NTL, NTS, true, BSWAP>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
+                                              colb_of(t), col_of(t) < c1, io, pre);
+    else
       mfma_tile<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
                                                col_of(t) < c1, io, pre);
-    }
+    t = tn;
   }
 }
 
@@ -343,8 +313,8 @@ __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restr
 
 // table: the plan's mfma table (mfma_table.hpp layout); coeff: the plan's
 // coefficient rows (column tails).
-template <int KS, bool NTL, bool NTS, int MODE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, MODE)))) void rs_apply_mfma_kernel(
+template <int KS, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMfmaWaves))) void rs_apply_mfma_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
@@ -373,8 +343,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_wav
     const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
     const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
     if (v1 > v0)
-      mfma_walk<KS, W, NTL, NTS, MODE, false>(ib, ob, soff, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1,
-                                              wave, nwaves, MfmaIO{0x80808080u, 0u}, nopre);
+      mfma_walk<KS, W, NTL, NTS, false>(ib, ob, soff, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1, wave,
+                                        nwaves, MfmaIO{0x80808080u, 0u}, nopre);
     if (seg == nseg - 1)
       for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)
         apply_column<0>(reinterpret_cast<const uint32_t*>(ib), reinterpret_cast<uint32_t*>(ob), coeff, in_idx,

@@ -237,13 +237,13 @@ hipError_t dec_wide_k(const BytesLaunch& a, hipStream_t s) {
 
 hipError_t enc_wide(const BytesLaunch& a, hipStream_t s) {
   if (bytes_mfma_eligible(a, true)) return launch_encode_bytes_mfma(a, s);
-  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_encode_bytes_k32(a, s);
+  if (pipe_ok(a) && a.k <= 32) return launch_encode_bytes_k32(a, s);
   if (pipe_ok(a)) return a.rows <= 8 ? enc_wide_pipe<8>(a, s) : enc_wide_pipe<16>(a, s);
   return a.k <= 32 ? enc_wide_k<32>(a, s) : enc_wide_k<16>(a, s);
 }
 hipError_t dec_wide(const BytesLaunch& a, hipStream_t s) {
   if (bytes_mfma_eligible(a, false)) return launch_decode_bytes_mfma(a, s);
-  if (pipe_ok(a) && a.k <= 32 && k32_kernels()) return launch_decode_bytes_k32(a, s);
+  if (pipe_ok(a) && a.k <= 32) return launch_decode_bytes_k32(a, s);
   if (pipe_ok(a)) return a.rows <= 8 ? dec_wide_pipe<8>(a, s) : dec_wide_pipe<16>(a, s);
   return a.k <= 32 ? dec_wide_k<32>(a, s) : dec_wide_k<16>(a, s);
 }
@@ -292,7 +292,7 @@ uint64_t encode_switch_bytes(const BytesLaunch& a, hipStream_t s) {
     case 16: return enc_switch_bytes<16>(a, s);
     default:
       if (bytes_mfma_eligible(a, true)) return encode_switch_bytes_mfma(a);
-      return a.k <= 32 && pipe_ok(a) && k32_kernels() ? encode_switch_bytes_k32(a, s) : 0;
+      return a.k <= 32 && pipe_ok(a) ? encode_switch_bytes_k32(a, s) : 0;
   }
 }
 

@@ -135,9 +135,8 @@ __device__ __forceinline__ uint32_t encode_edges(uint8_t* slot, uint8_t* par, ui
 
 // MODE 0: speculative pass (mapping 0, MapToGF flags into flags[obj]);
 // MODE 1: re-encode of the objects select_mapping gave mapping != 0 (status 0).
-// FORM: the apply kernel's walk form (rs_apply_mfma_kernel.hpp mfma_walk).
-template <int KS, int MODE, int FORM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, FORM)))) void
+template <int KS, int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
 encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
                          const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
@@ -255,28 +254,22 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     if (nint) {
       if constexpr (F) {
         FlagPre pre;
-        bool walked = false;
-        if constexpr (FORM == 2) {
-          if (record) {  // the mid-object switch (mfma_switch_walk)
-            uint32_t sent = 0;
-            mfma_switch_walk<KS, W>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), soff, lds,
-                                    lrowc, loff, MT, rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves,
-                                    flags + obj, record + (uint64_t)obj * units + v0 / TCV, pre, sent);
-            walked = true;
-          }
+        if (record) {  // the mid-object switch (mfma_switch_walk)
+          uint32_t sent = 0;
+          mfma_switch_walk<KS, W>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), soff, lds, lrowc,
+                                  loff, MT, rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves,
+                                  flags + obj, record + (uint64_t)obj * units + v0 / TCV, pre, sent);
+        } else {
+          apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par),
+                                                    soff, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
+                                                    4 * (v0 + nint * TCV), wave, nwaves, io, pre);
         }
-        if (!walked)
-          apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
-                                                          reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT,
-                                                          rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave,
-                                                          nwaves, io, pre);
         fbits = pre.bits();
       } else {
         apply::NoPre pre;
-        apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot),
-                                                        reinterpret_cast<char*>(par), soff, lds, lrowc, loff, MT, rows,
-                                                        lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io,
-                                                        pre);
+        apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par),
+                                                  soff, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
+                                                  4 * (v0 + nint * TCV), wave, nwaves, io, pre);
       }
     }
     // Edge tiles and tail columns (VALU step, with the data-chunk tail fix).
@@ -327,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
 // objects), then every edge range of the objects mapped with 1<<31, segment
 // by segment as phase 0 cut them (phase 0 writes edges with mapping 0).
 template <int KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, 2)))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
 encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk,
                               uint64_t col0, uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
                               const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
@@ -432,8 +425,8 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
 }
 
 // Decode: survivors in_idx -> rebuilt chunks out_idx of the same slot.
-template <int KS, int FORM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, FORM)))) void
+template <int KS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
 decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, const uint8_t* __restrict__ table,
                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
@@ -457,10 +450,9 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     const uint32_t m = mapping[sg.obj];
     uint8_t* const slot = slots + (uint64_t)sg.obj * slot_stride + 4 * col0;  // window base
     if (sg.v1 > sg.v0)
-      apply::mfma_walk<KS, W, true, true, FORM, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot),
-                                                      soff, lds, lrowc, loff, MT, rows, lane, lg, ln,
-                                                      4 * (uint32_t)sg.v0, 4 * (uint32_t)sg.v1, wave, nwaves,
-                                                      MfmaIO{0x80808080u ^ be(m), m}, pre);
+      apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot), soff,
+                                                lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * (uint32_t)sg.v0,
+                                                4 * (uint32_t)sg.v1, wave, nwaves, MfmaIO{0x80808080u ^ be(m), m}, pre);
     // Columns past the last whole vector of the window, one per lane.
     for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
       for (uint32_t i = 0; i < rows; ++i) {
@@ -489,25 +481,25 @@ uint32_t switch_units(const BytesLaunch& a) {
   return (uint32_t)((nvec + TCV - 1) / TCV);
 }
 
-template <int KS, int FORM>
-hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
+template <int KS>
+hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
-  const uint64_t blocks = 256ull * apply::mfma_waves(KS, FORM);
+  const uint64_t blocks = 256ull * apply::kMfmaWaves;
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
-    // The mid-object switch runs on the refill form when the caller handed
-    // scratch for its record (never inside a graph capture).
+    // The mid-object switch runs when the caller handed scratch for its
+    // record (never inside a graph capture).
     uint8_t* record = nullptr;
     uint32_t units = 0;
-    if (FORM == 2 && a.scratch && a.sw) {
+    if (a.scratch && a.sw) {
       units = switch_units<KS>(a);
       bytes::SwitchLayout l;
       l.units = units;
       record = l.record(a.scratch, a.nobj);
       if (hipError_t e = hipMemsetAsync(record, 2, (uint64_t)a.nobj * units, s)) return e;
     }
-    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0, FORM>),
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0>),
                        bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
                        a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma, a.coeff,
                        a.out_idx, a.flags, a.mapping, nseg, record, units);
@@ -519,7 +511,7 @@ hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
     }
     return hipSuccess;
   }
-  if (FORM == 2 && a.scratch && a.sw && a.sw->switched && a.sw->units) {
+  if (a.scratch && a.sw && a.sw->switched && a.sw->units) {
     // Phase 1 after the switch: the list of tiles to redo, then the redo.
     bytes::SwitchLayout l;
     l.units = a.sw->units;
@@ -530,89 +522,44 @@ hipError_t enc_form(const BytesLaunch& a, hipStream_t s) {
     hipLaunchKernelGGL(bytes::mfma_redo_list_kernel, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(kBlock), 0, s,
                        l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.list(a.scratch), count);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((bytes::encode_bytes_mfma_redo_kernel<KS>), dim3((uint32_t)(256ull * apply::mfma_waves(KS, 2))),
-                       dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S,
-                       a.nobj, a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, a.sw->nseg,
-                       l.list(a.scratch), count, l.units);
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_redo_kernel<KS>), dim3((uint32_t)blocks), dim3(kBlock), lds, s,
+                       a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma,
+                       a.coeff, a.out_idx, a.flags, a.mapping, a.sw->nseg, l.list(a.scratch), count, l.units);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1, FORM>), bytes_grid(ncols, 1, 1, blocks, 1),
-                     dim3(kBlock), lds, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj,
-                     a.rows, a.k, a.mfma, a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u);
+  hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1>), bytes_grid(ncols, 1, 1, blocks, 1), dim3(kBlock), lds,
+                     s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma,
+                     a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u);
   return hipGetLastError();
 }
 
-template <int KS, int FORM>
-hipError_t dec_form(const BytesLaunch& a, hipStream_t s) {
+template <int KS>
+hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
-  const uint64_t blocks = 256ull * apply::mfma_waves(KS, FORM);
+  const uint64_t blocks = 256ull * apply::kMfmaWaves;
   const uint32_t nseg = object_segments(a.nobj, ncols);
-  hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS, FORM>),
+  hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS>),
                      bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
                      a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.mfma, a.coeff,
                      a.in_idx, a.out_idx, a.mapping, nseg);
   return hipGetLastError();
 }
 
-// The refill form (2) is the product for the decode, the re-encode and the
-// speculative encode.  Round 3's speculative encode could not take it at two
-// waves per SIMD (MapToGF's flags, written in C, spilled at four K steps) and
-// ran form 3 (refill at one wave per SIMD) up to four K steps, form 0 above
-// (profiles/r03/s35_mfma_bytes/, s36_mfma_geo/); the flags' asm chain
-// (FlagPre) removed the spill.  Env SLIME_RS_MFMA_ENC_FORM=0|2|3 forces one
-// form for the speculative pass (A/B); SLIME_RS_MFMA_MODE=0/1 forces a form
-// elsewhere.
-template <int KS>
-int enc_form0() {
-  static const int f = [] {
-    const char* e = getenv("SLIME_RS_MFMA_ENC_FORM");
-    if (e && e[0] == '3') return 3;
-    if (e && e[0] == '0') return 0;
-    return 2;
-  }();
-  return f;
-}
-template <int KS>
-hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
-  if (a.phase == 0) {
-    switch (enc_form0<KS>()) {
-      case 0: return enc_form<KS, 0>(a, s);
-      case 3: return enc_form<KS, 3>(a, s);
-      default: return enc_form<KS, 2>(a, s);
-    }
-  }
-  if (a.scratch && a.sw && a.sw->switched) return enc_form<KS, 2>(a, s);  // the switch's redo
-  switch (mfma_kernel_form()) {
-    case 0: return enc_form<KS, 0>(a, s);
-    case 1: return enc_form<KS, 1>(a, s);
-    default: return enc_form<KS, 2>(a, s);
-  }
-}
-template <int KS>
-hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
-  switch (mfma_kernel_form()) {
-    case 0: return dec_form<KS, 0>(a, s);
-    case 1: return dec_form<KS, 1>(a, s);
-    default: return dec_form<KS, 2>(a, s);
-  }
-}
-
 }  // namespace
 
 // Scratch of the matrix-core mid-object switch (bytes::SwitchLayout: count,
-// redo list, one record byte per interior tile), or 0 when phase 0 will not
-// run the switching walk (another speculative form forced).
+// redo list, one record byte per interior tile).
 uint64_t encode_switch_bytes_mfma(const BytesLaunch& a) {
   if (a.phase != 0 || a.nobj == 0) return 0;
   uint32_t units = 0;
   switch (mfma::ksteps(a.k)) {
-    case 2: units = enc_form0<2>() == 2 ? switch_units<2>(a) : 0; break;
-    case 3: units = enc_form0<3>() == 2 ? switch_units<3>(a) : 0; break;
-    case 4: units = enc_form0<4>() == 2 ? switch_units<4>(a) : 0; break;
-    case 5: units = enc_form0<5>() == 2 ? switch_units<5>(a) : 0; break;
-    case 6: units = enc_form0<6>() == 2 ? switch_units<6>(a) : 0; break;
-    case 7: units = enc_form0<7>() == 2 ? switch_units<7>(a) : 0; break;
+    case 2: units = switch_units<2>(a); break;
+    case 3: units = switch_units<3>(a); break;
+    case 4: units = switch_units<4>(a); break;
+    case 5: units = switch_units<5>(a); break;
+    case 6: units = switch_units<6>(a); break;
+    case 7: units = switch_units<7>(a); break;
     default: return 0;
   }
   return units ? 256 + 5ull * a.nobj * units : 0;
@@ -622,9 +569,9 @@ bool bytes_mfma_eligible(const BytesLaunch& a, bool encode) {
   if (!a.mfma || !matrix_core_mode() || a.k < 17 || !mfma_wanted(a.k, a.rows) || !mfma::supported(a.rows, a.k))
     return false;
   // need 17..24 encodes on the VALU queue kernel, whose mid-object switch
-  // redoes only part of a 1<<31 object (SLIME_RS_MFMA_MINK below 25 forces).
-  if (encode && a.k < 25 && mfma_min_k() >= 25) return false;
-  if (!pipelined_kernels()) return false;  // SLIME_RS_PIPE=0 / kernel_pipeline(0): the non-pipelined VALU forms
+  // redoes only part of a 1<<31 object.
+  if (encode && a.k < 25) return false;
+  if (!pipelined_kernels()) return false;  // kernel_pipeline(0): the non-pipelined VALU forms
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   // 32-bit byte offsets from the window base: every chunk the launch reads
   // or writes, plus the window's columns.

@@ -192,8 +192,6 @@ def test_matrix_core_labels_follow_the_library_rule():
     """bench.py labels a wide-code line with the matrix-core kernels exactly
     where the library routes it there (rs_apply_mfma.hip mfma_wanted: k >= 33,
     or 17 <= k <= 32 with k x rows >= 128; at most 32 rows, k <= 112)."""
-    if os.environ.get("SLIME_RS_MFMA_MINK") or os.environ.get("SLIME_RS_MFMA", "1")[:1] == "0":
-        return  # the process was started with the rule overridden
     bench = _load("bench.py", "bench_mod_mfma")
     yes = [(64, 16), (33, 1), (99, 1), (112, 32), (24, 8), (32, 4), (17, 8)]
     no = [(8, 4), (10, 4), (16, 16), (20, 4), (17, 7), (64, 33), (113, 4), (40, 0)]
@@ -218,3 +216,51 @@ def test_dry_run_plans_the_c2_and_north_star_shape_legs():
     c3 = 128 * 12 * bench.ceil_div(bench.ceil_div(256 << 20, 4), 8)
     ns = 64 * 12 * bench.ceil_div(bench.ceil_div(512 << 20, 4), 8)
     assert c3 == ns
+
+
+def test_dry_run_plans_the_pooled_proxy_leg_at_every_n():
+    """At every N, rank 0 drives the host entry points as one proxy does (25
+    concurrent PUT + GET requests, SLIME_RS_ANY_DEVICE) over the GPUs of all
+    N ranks: the device pool is restricted to exactly those GPUs."""
+    for n in (1, 2, 8):
+        args = ["--gpus", str(n), "--dry-run"] if n > 1 else ["--dry-run"]
+        r = _bench(args, SLIME_BENCH_DEVICE_COUNT=str(n))
+        assert r.returncode == 0, r.stdout + r.stderr
+        pooled = json.loads(r.stdout.strip().splitlines()[-1])["host_path.pooled"]
+        assert pooled["driver_rank"] == 0 and pooled["threads"] == 25
+        assert pooled["devices"] == list(range(n))
+        assert pooled["pool_env"] == ",".join(str(d) for d in range(n))
+        assert pooled["workloads"] == ["fused_64mib", "fused_1mib", "unchanged_caller_64mib"]
+
+
+def test_proxy_load_library_exports_its_entry_point():
+    """tools/libproxy_load.so (built by make) links the C-ABI and exports
+    proxy_load; argument errors return SLIME_RS_ERR_INVALID_ARG without
+    touching a GPU."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libproxy_load.so"))
+    f = lib.proxy_load
+    f.restype = ctypes.c_int
+    out = (ctypes.c_double * 10)()
+    have = (ctypes.c_int * 8)(*range(4, 12))
+    assert f(0, ctypes.c_uint64(1 << 20), 8, 12, have, 0, ctypes.c_double(1.0), ctypes.c_uint64(1), out) == 9
+    assert f(4, ctypes.c_uint64(1 << 20), 8, 12, have, 2, ctypes.c_double(1.0), ctypes.c_uint64(1), out) == 9
+
+
+def test_proxy_load_fails_loudly_without_a_gpu():
+    """No GPU: every request's device calls return SLIME_RS_ERR_NO_DEVICE (10)
+    and the run is not verified -- there is no CPU fallback to hide behind."""
+    import ctypes
+    import torch
+    if torch.cuda.device_count() > 0:
+        return
+    sys.path.insert(0, ROOT)
+    import slime_amd  # noqa: F401  (loads libslime_rs.so first, as bench.py does)
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libproxy_load.so"))
+    lib.proxy_load.restype = ctypes.c_int
+    out = (ctypes.c_double * 10)()
+    have = (ctypes.c_int * 8)(*range(4, 12))
+    for pattern in (0, 1):
+        rc = lib.proxy_load(2, ctypes.c_uint64(4096), 8, 12, have, pattern, ctypes.c_double(0.05),
+                            ctypes.c_uint64(1), out)
+        assert rc == 10 and out[2] == 0.0 and out[8] > 0

@@ -1,0 +1,81 @@
+"""GPU tests of bench.py's host-memory legs at small sizes: the proxy-level
+pooled driver (tools/proxy_load.cpp, host_path.pooled) and the unchanged Go
+caller's split.  Both run the product through the C-ABI; the round trips and
+the chunk comparisons are their checks (the parity itself is pinned against
+the oracle in test_gpu_parity.py)."""
+import ctypes
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+from slime_amd import _native as N
+from slime_amd import objects
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_gpu_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _proxy():
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libproxy_load.so"))
+    lib.proxy_load.restype = ctypes.c_int
+    lib.proxy_load.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_double, ctypes.c_uint64,
+                               ctypes.POINTER(ctypes.c_double)]
+    return lib
+
+
+@pytest.mark.parametrize("pattern", [0, 1])
+@pytest.mark.parametrize("size,need,total,have", [
+    (256 << 10, 8, 12, [4, 5, 6, 7, 8, 9, 10, 11]),
+    ((1 << 20) + 13, 4, 6, [1, 2, 4, 5]),
+    (4099, 10, 14, [0, 2, 4, 6, 8, 9, 10, 11, 12, 13]),
+])
+def test_proxy_load_round_trips_under_concurrency(pattern, size, need, total, have):
+    """8 concurrent requests, PUT + GET each, through the *_ex forms with
+    SLIME_RS_ANY_DEVICE: every GET returns its object, chunks are stable, the
+    unchanged caller's chunks equal the fused entry point's, and the device
+    pool counted every call on a GPU."""
+    lib = _proxy()
+    n = N.lib.slime_rs_device_count()
+    before = [N.pool_calls(d)[0] for d in range(n)]
+    out = (ctypes.c_double * 10)()
+    c_have = (ctypes.c_int * need)(*have)
+    rc = lib.proxy_load(8, size, need, total, c_have, pattern, 0.3, 77 + pattern, out)
+    after = [N.pool_calls(d)[0] for d in range(n)]
+    assert rc == 0 and out[8] == 0, (rc, list(out))
+    assert out[2] == 1.0, "a GET did not return its object or the chunks changed"
+    assert out[0] >= 8 and out[1] > 0
+    # device-routed calls: fused 2 per request; unchanged r CreateParity + 1 RecoverData
+    # per request (the codec calls run on the host cores and take no device)
+    assert sum(a - b for a, b in zip(after, before)) >= out[0] * (2 if pattern == 0 else 1)
+
+
+def test_unchanged_caller_split_adds_up():
+    """The unchanged caller's line: phases + other = total for the median call,
+    total min <= median <= max over >= 7 reps, and both directions verified
+    (the write's chunks equal the fused entry point's)."""
+    bench = _bench()
+    need, total, erase = 8, 12, [0, 1, 2, 3]
+    have = [i for i in range(total) if i not in erase][:need]
+    data = np.random.default_rng(5).integers(0, 256, size=(2 << 20) + 7, dtype=np.uint8)
+    chunks = [np.zeros(objects.chunk_size(data.size, need), dtype=np.uint8) for _ in range(total)]
+    m, _ = objects.write_chunks(data, need, total, out=chunks)
+    u = bench.unchanged_caller(data, need, total, have, chunks, m, m, 7)
+    assert u["verified"]
+    for side in ("write", "read"):
+        s = u[side]["split_ms"]
+        parts = sum(v for k, v in s.items() if k != "total")
+        assert abs(parts - s["total"]) < 0.01, s
+        t = u[side]["total_ms"]
+        assert t["min"] <= t["median"] <= t["max"] and len(u[side]["reps_ms"]) == 7
+    assert "map_from_gf_x12_concurrent" in u["write"]["split_ms"]

@@ -128,16 +128,8 @@ def test_recover_data_ragged_longer_chunks():
     assert all(g.size == 8 for g in got)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["staged", "register", "direct"])
-def host_mode(request):
-    prev = N.lib.slime_rs_host_pipeline(-1)
-    N.check(N.lib.slime_rs_host_pipeline(request.param))
-    yield request.param
-    N.check(N.lib.slime_rs_host_pipeline(prev))
-
-
 @pytest.mark.parametrize("need,total,L", [(8, 12, 700001), (4, 6, 3 * 262144 + 5), (16, 20, 500003), (8, 12, 4099)])
-def test_host_pipeline_multi_chunk(host_mode, need, total, L):
+def test_host_pipeline_multi_chunk(need, total, L):
     # The Go-API entry points stream host buffers through a 3-deep ring of
     # ~8 MiB stages: these sizes span >3 chunks with a ragged last chunk.
     rng = np.random.default_rng(L)
@@ -154,9 +146,9 @@ def test_host_pipeline_multi_chunk(host_mode, need, total, L):
         assert np.array_equal(g, w)
 
 
-def test_host_pipeline_read_only_and_shared_inputs(host_mode):
-    # Read-only rows (np.frombuffer of bytes) and one row passed twice: page
-    # registration may be refused; the result must not change.
+def test_host_pipeline_read_only_and_shared_inputs():
+    # Read-only rows (np.frombuffer of bytes) and one row passed twice: the
+    # staged pipeline only reads them.
     need, total, L = 4, 7, 300007
     rng = np.random.default_rng(5)
     base = rand_vecs(rng, need, L)
@@ -167,15 +159,7 @@ def test_host_pipeline_read_only_and_shared_inputs(host_mode):
         assert np.array_equal(row, OC.create_parity([np.array(d) for d in data], need + i)[1])
 
 
-def test_host_pipeline_mode_knob():
-    prev = N.lib.slime_rs_host_pipeline(-1)
-    assert prev in (0, 1, 2)
-    with pytest.raises(N.NativeError):
-        N.check(N.lib.slime_rs_host_pipeline(3))
-    assert N.lib.slime_rs_host_pipeline(-1) == prev
-
-
-def test_host_pipeline_concurrent_callers(host_mode):
+def test_host_pipeline_concurrent_callers():
     # Several host threads share the workspace pool and the copy pool.
     import concurrent.futures as cf
     need, total, L = 8, 12, 400009
@@ -989,7 +973,7 @@ def test_fuzz_random_shapes_and_layouts(torch_dev):
 @pytest.mark.gpu
 @pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20), (20, 24), (17, 30), (40, 56)])
 def test_fallback_kernel_vs_oracle(torch_dev, need, total):
-    """The non-pipelined apply kernel (shards >= 4 GiB; SLIME_RS_PIPE=0) at
+    """The non-pipelined apply kernel (shards >= 4 GiB; kernel_pipeline(0)) at
     small sizes: encode in place, misaligned bases, reconstruct into a
     separate buffer -- and the pipelined product form on the same inputs."""
     torch = torch_dev
