@@ -221,6 +221,68 @@ def test_map_to_gf_high_bit_mapping(codec_place):
     assert rc == 0 and n == n2 == 1 << 31 and np.array_equal(v, v2)
 
 
+def test_map_to_gf_seeded_fallbacks_agree_across_placements():
+    """Objects that need MapToGF's random fallback (map.go:64-66: a word in
+    [p, 2^32) and one in [p ^ 1<<31, 2^31)) draw from the library's seeded
+    candidate stream in batches of the same size on the host and on the
+    device, first fit wins: after slime_gf_seed, a SEQUENCE of fallback
+    objects gets the same mappings on both placements, and every mapping
+    fits (every word < p)."""
+    rng = np.random.default_rng(31)
+    objs = []
+    for i in range(4):
+        w = rng.integers(0, 2**32, size=5000 + 997 * i, dtype=np.uint64).astype(np.uint32)
+        w[7] = 0xFFFFFFFF
+        w[11] = 0x7FFFFFFE
+        objs.append(w.byteswap().tobytes() + bytes(i))  # big-endian words, ragged tail
+    got = {}
+    prev = N.lib.slime_gf_codec_placement(-1)
+    try:
+        for place in (0, 1):
+            N.check(N.lib.slime_gf_codec_placement(place))
+            gf.Seed(2024)
+            got[place] = [gf.MapToGF(o) for o in objs]
+    finally:
+        N.check(N.lib.slime_gf_codec_placement(prev))
+    for (m0, v0), (m1, v1), o in zip(got[0], got[1], objs):
+        assert m0 == m1 and m0 not in (0, 1 << 31)
+        assert np.array_equal(v0, v1) and int(v0.max()) < P
+        assert gf.MapFromGF(m0, v0)[: len(o)] == o
+
+
+@pytest.mark.parametrize("alias", ["inplace_parity_slots", "shifted_overlap"])
+def test_recover_data_outputs_overlapping_chunks(alias):
+    """RecoverData whose output rows overlap survivor chunks (a C caller's
+    in-place repair): the erased rows are computed before anything the unit
+    rows read is overwritten -- identical to the oracle on fresh buffers."""
+    need, total, L = 6, 9, 70001
+    rng = np.random.default_rng(17)
+    data = rand_vecs(rng, need, L, canonical=True)
+    code = [OC.create_parity(data, t)[1] for t in range(total)]
+    have = [2, 3, 4, 6, 7, 8]  # data rows 0, 1, 5 erased
+    want = OC.recover_data([code[i] for i in have], have)[1]
+    if alias == "inplace_parity_slots":
+        # erased data rows 0, 1, 5 are written over the parity survivors' own buffers
+        chunks = [np.array(code[i]) for i in have]
+        out = [None] * need
+        out[0], out[1], out[5] = chunks[3], chunks[4], chunks[5]
+        for t in (2, 3, 4):
+            out[t] = chunks[have.index(t)]  # unit rows in place
+    else:
+        # one arena: each output row starts half a row into a survivor chunk
+        arena = np.zeros((need + 1) * L, dtype=np.uint32)
+        for q, i in enumerate(have):
+            arena[q * L:(q + 1) * L] = code[i]
+        chunks = [arena[q * L:(q + 1) * L] for q in range(need)]
+        out = [arena[t * L + L // 2:(t + 1) * L + L // 2] for t in range(need)]
+    ptr = lambda arrs: (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])  # noqa: E731
+    lens = (ctypes.c_uint64 * need)(*([L] * need))
+    idx = (ctypes.c_int * need)(*have)
+    N.check(N.lib.slime_rs_recover_data(ptr(chunks), lens, need, idx, need, ptr(out)))
+    for t in range(need):
+        assert np.array_equal(out[t], want[t]), t
+
+
 # ------------------------------------------------------- device-resident batch API
 
 def _objects(torch, nobj, n, L, seed):

@@ -40,6 +40,15 @@ for step in "$@"; do
     tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct or pool" ;;
     tests_bench) run pytest_bench 400 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 200 --timeout-method thread ;;
     hostrep) for i in 1 2 3; do run hostrep_$i 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= --pooled 0 || exit 1; done ;;
+    proxysweep) run proxy_sweep 300 python tools/proxy_sweep.py --threads 1,4,8,16,25 --mib 64,1 --seconds 1.5 &&
+                run proxy_sweep_c0 300 env SLIME_RS_COPY_THREADS=0 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 &&
+                run proxy_sweep_c4 300 env SLIME_RS_COPY_THREADS=4 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 ;;
+    # C2 gap: the same 4/6 kernel on 32 (C2), 64 and 128 objects of 64 MiB, and a rocprof trace of C2
+    c2size) for n in 32 64 128 32; do run c2size_$n 300 python bench.py --preset c2 --objects $n --bytes-path 0 --steps 20 --warmup 5 $NOLEGS || exit 1; done &&
+            run c2prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/c2prof" -o c2 --output-format csv -- \
+              python3 bench.py --preset c2 --bytes-path 0 --steps 20 --warmup 5 $NOLEGS ;;
+    proxyq) run proxy_q8 300 env GPU_MAX_HW_QUEUES=8 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 &&
+            run proxy_q16 300 env GPU_MAX_HW_QUEUES=16 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 ;;
     tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --bytes-path 0 ;;
