@@ -49,6 +49,10 @@ for step in "$@"; do
               python3 bench.py --preset c2 --bytes-path 0 --steps 20 --warmup 5 $NOLEGS ;;
     proxyq) run proxy_q8 300 env GPU_MAX_HW_QUEUES=8 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 &&
             run proxy_q16 300 env GPU_MAX_HW_QUEUES=16 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 ;;
+    proxysched) for sc in auto yield blocking spin; do
+                  run proxy_sched_$sc 300 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 --sched $sc || exit 1
+                done ;;
+    latc) run latc 200 tools/latency_c 300 ;;
     tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --bytes-path 0 ;;

@@ -24,9 +24,20 @@ def main():
     ap.add_argument("--seconds", type=float, default=1.5)
     ap.add_argument("--need", type=int, default=8)
     ap.add_argument("--total", type=int, default=12)
+    ap.add_argument("--sched", choices=["auto", "spin", "yield", "blocking"], default="auto",
+                    help="hipSetDeviceFlags on every device before the sweep (how host threads wait for the GPU)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process: torch's)
     from slime_amd import _native as N
+    if a.sched != "auto":
+        # the HIP runtime already in the process (torch's), by soname
+        hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+        flag = {"spin": 1, "yield": 2, "blocking": 4}[a.sched]
+        for d in range(N.lib.slime_rs_device_count()):
+            torch.cuda.set_device(d)
+            torch.cuda.synchronize()
+            rc = hip.hipSetDeviceFlags(ctypes.c_uint(flag))
+            print(json.dumps({"hipSetDeviceFlags": a.sched, "device": d, "rc": rc}), flush=True)
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libproxy_load.so"))
     lib.proxy_load.restype = ctypes.c_int
     lib.proxy_load.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
@@ -43,7 +54,7 @@ def main():
             rc = lib.proxy_load(t, mib << 20, a.need, a.total, c_have, a.pattern, a.seconds, 0x77 + t, out)
             after = [N.pool_calls(d)[0] for d in range(ndev)]
             wall = out[1] or 1e-9
-            print(json.dumps({"threads": t, "object_mib": mib, "pattern": a.pattern,
+            print(json.dumps({"threads": t, "object_mib": mib, "pattern": a.pattern, "sched": a.sched,
                               "copy_threads_env": os.environ.get("SLIME_RS_COPY_THREADS"),
                               "gibs": round(2 * out[0] * (mib << 20) / 2**30 / wall, 2),
                               "requests_per_s": round(out[0] / wall, 1),
