@@ -264,3 +264,23 @@ def test_proxy_load_fails_loudly_without_a_gpu():
         rc = lib.proxy_load(2, ctypes.c_uint64(4096), 8, 12, have, pattern, ctypes.c_double(0.05),
                             ctypes.c_uint64(1), out)
         assert rc == 10 and out[2] == 0.0 and out[8] > 0
+
+
+def test_committed_traffic_per_shape_matches_shipped_kernel_code():
+    """profiles/r05/pmc_traffic.json holds one PMC summary per BASELINE shape
+    the line reports (C3, C2, the north star's 64 MiB shards); each was
+    measured on the machine code the built library runs, and each moves its
+    algorithmic bytes 4L(k+r) per launch to within 1%."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from slime_amd.codeobj import kernel_code_id
+    entries = json.load(open(os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json")))
+    lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
+    shapes = {"8/12 L=8388608 nobj=128": (8, 12, 8388608, 128), "4/6 L=4194304 nobj=32": (4, 6, 4194304, 32),
+              "8/12 L=16777216 nobj=64": (8, 12, 16777216, 64)}
+    assert {e["config"] for e in entries} == set(shapes)
+    for e in entries:
+        need, total, L, nobj = shapes[e["config"]]
+        assert e["kernel"] == "rs_apply_queue_kernel"
+        assert e["kernel_code"] == kernel_code_id(lib, (f"rs_apply_queue_kernelILi{need}E",)), e["config"]
+        assert abs(e["hbm_bytes_per_launch"] / (nobj * 4 * L * total) - 1) < 0.01, e["config"]

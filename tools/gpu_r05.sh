@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs="
+NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs= --pooled 0"
 
 run() {  # run <name> <limit-seconds> <command...>
   local name=$1 lim=$2; shift 2
@@ -58,8 +58,10 @@ for step in "$@"; do
     benchq) run benchq 400 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --bytes-path 0 ;;
     hostonly) run hostonly 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
     rehearse2) run rehearse2 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 ;;
+    # the driver's command under the profiler, without the pooled leg (rocprofv3 segfaulted
+    # inside the runtime under its 25 concurrent host threads, profiles/r05/s4_pmc_c2/c2prof.log)
     profdrv) run profdrv 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
-            python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 --pooled 0 ;;
     # PMC traffic passes per BASELINE shape (symbol path), each its own run
     pmc_c3) pmc pmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
             pmc pmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;

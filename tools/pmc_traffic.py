@@ -5,7 +5,9 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): counters are in KiB; FETCH_SIZE
 reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read,
 so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> > profiles/r04/pmc_traffic.json
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <session> [<existing json>] > profiles/r05/pmc_traffic.json
+        # symbol path: one entry per config; with an existing file (one entry or a list) the
+        # entries of other configs are kept and the result is a list
     python tools/pmc_traffic.py --all <fetch_dir> <write_dir>    # every kernel: HBM bytes per dispatch
     python tools/pmc_traffic.py --bytes <fetch_dir> <write_dir> <config> <session> [<existing json>]
         # the fused byte path's kernels (bench.py object_bytes_path), appended to a list
@@ -36,17 +38,29 @@ def kernel_source_id() -> str:
 KERNELS = ("rs_apply_queue_kernel", "rs_apply_pipe_kernel", "rs_apply_kernel")  # product apply kernels (rs_apply.hip)
 
 
-def per_dispatch(d, counter, need):
+def per_dispatch(d, counter, need, only=None):
     """Dispatches of the apply kernels instantiated for k = need (a bench run
-    also launches other k, e.g. its C5 leg's 10/14)."""
+    also launches other k, e.g. its C5 leg's 10/14); `only`: one kernel name."""
     vals, seen = {}, set()
     for path in glob.glob(f"{d}/*counter_collection.csv"):
         for r in csv.DictReader(open(path)):
             name = next((k for k in KERNELS if f"{k}<{need}," in r["Kernel_Name"]), None)
-            if name and r["Counter_Name"] == counter:
+            if name and (only is None or name == only) and r["Counter_Name"] == counter:
                 vals[int(r["Dispatch_Id"])] = float(r["Counter_Value"])
                 seen.add(name)
     return vals, seen
+
+
+def batch_kernel(fetch_dir, need):
+    """The apply kernel of the bench's batch launches: of the kernels seen at
+    k = need, the one with the largest dispatch (host calls of the same k take
+    the static kernel on one-object windows, far smaller)."""
+    best, size = None, -1.0
+    for k in KERNELS:
+        v, _ = per_dispatch(fetch_dir, "FETCH_SIZE", need, k)
+        if v and max(v.values()) > size:
+            best, size = k, max(v.values())
+    return best
 
 
 def dominant(vals):
@@ -126,8 +140,9 @@ def main():
     fetch_dir, write_dir, config = sys.argv[1:4]
     session = sys.argv[4] if len(sys.argv) > 4 else "?"
     need = int(config.split("/")[0])
-    f, fk = per_dispatch(fetch_dir, "FETCH_SIZE", need)
-    w, wk = per_dispatch(write_dir, "WRITE_SIZE", need)
+    only = batch_kernel(fetch_dir, need)
+    f, fk = per_dispatch(fetch_dir, "FETCH_SIZE", need, only)
+    w, wk = per_dispatch(write_dir, "WRITE_SIZE", need, only)
     assert len(fk | wk) == 1, f"expected one apply kernel, saw {fk | wk}"
     # The bench's launches all move the same bytes; the allocator's placement
     # probe over a larger buffer (another leg's) runs the same kernel over
@@ -138,7 +153,7 @@ def main():
     write_kib = sum(w.values()) / len(w)
     read_bytes = 2 * fetch_kib * 1024
     write_bytes = write_kib * 1024
-    print(json.dumps({
+    entry = {
         "config": config,
         "session": session,
         "kernel_source": kernel_source_id(),
@@ -152,7 +167,14 @@ def main():
         "write_bytes_per_launch": int(write_bytes),
         "hbm_bytes_per_launch": int(read_bytes + write_bytes),
         "correction": "read = 2 x FETCH_SIZE (gfx950 wide-stream undercount), x1024 (KiB)",
-    }, indent=1))
+    }
+    existing = sys.argv[5] if len(sys.argv) > 5 else None
+    if not existing:
+        print(json.dumps(entry, indent=1))
+        return
+    old = json.load(open(existing)) if os.path.exists(existing) else []
+    old = old if isinstance(old, list) else [old]
+    print(json.dumps([e for e in old if e.get("config") != config] + [entry], indent=1))
 
 
 if __name__ == "__main__":
