@@ -1185,7 +1185,8 @@ def pooled_leg(args, rank: int, world: int, devices: list[int]) -> dict | None:
                 "get_ms": {"p50": round(res[6], 3), "p99": round(res[7], 3)},
                 "per_device_calls": {str(d): a - b for d, a, b in zip(devices, after, before)},
                 "failed_calls": int(res[8]), "status": rc, "setup_s": round(res[9], 2), "verified": good}
-        out = {"threads": args.pool_threads, "devices": devices, "need": need, "total": total, "erased": erase,
+        out = {"threads": args.pool_threads, "devices": devices, "host_call_slots": N.lib.slime_rs_host_call_slots(),
+               "need": need, "total": total, "erased": erase,
                "workloads": legs, "verified": ok,
                "what": "one process, --pool-threads concurrent PUT (writeChunks) + GET (reconstruct) requests per "
                        "thread loop, every call through the cgo shim's *_ex forms with SLIME_RS_ANY_DEVICE over the "

@@ -408,6 +408,12 @@ typedef struct slime_rs_host_stats {
 int slime_rs_host_stats(slime_rs_host_stats_t *stats, int reset);
 /* Host calls the device pool has routed to `device` so far and calls in flight there. */
 int slime_rs_pool_calls(int device, uint64_t *calls, int *inflight);
+/* Host calls (the data entry points over host memory) that run at once in
+ * this process: half its usable CPUs (affinity mask capped by the cgroup CPU
+ * quota), at least 4.  Further callers wait, asleep, for a slot -- more calls
+ * than CPUs only time-slice, and a process over its CPU quota is throttled
+ * as a whole. */
+int slime_rs_host_call_slots(void);
 /* Ticket-counter sets of the dynamic-schedule kernels on `device`: *sets
  * allocated so far, *held by launches not yet known to have finished plus
  * those owned by captured graphs.  A set is reused by any stream once its

@@ -175,6 +175,7 @@ SIGNATURES = [
     ("slime_rs_plan_cache_stats", ctypes.c_int, [ctypes.POINTER(CacheStats)]),
     ("slime_rs_plan_cache_capacity", ctypes.c_int, [ctypes.c_uint64]),
     ("slime_rs_pool_calls", ctypes.c_int, [ctypes.c_int, c_u64p, c_intp]),
+    ("slime_rs_host_call_slots", ctypes.c_int, []),
     ("slime_rs_ticket_sets", ctypes.c_int, [ctypes.c_int, c_u64p, c_u64p]),
     ("slime_rs_schedule_counts", ctypes.c_int, [ctypes.c_int, c_u64p, c_u64p]),
     ("slime_rs_host_stats", ctypes.c_int, [ctypes.POINTER(HostStats), ctypes.c_int]),

@@ -58,12 +58,24 @@ int status_of(Status st, const char* what);
 // ---- device routing (rs_capi.cpp) -------------------------------------------------
 // The device of one host call: the *_ex call's explicit device, else the
 // thread's selected device, else the device pool's pick (device_pool.hpp).
-// Holds the pool slot for the life of the call.
+// Holds the pool slot for the life of the call, and one of the process's
+// host-call slots (host_call_slots()): callers beyond them wait, asleep, for
+// a slot before a device is picked.
 struct DeviceLease {
   PoolLease lease;
   int device = -1;
   int acquire();
+  ~DeviceLease();
+  DeviceLease() = default;
+  DeviceLease(const DeviceLease&) = delete;
+  DeviceLease& operator=(const DeviceLease&) = delete;
+
+ private:
+  bool slot_ = false;
 };
+// Host calls that may run at once in this process: half the usable CPUs
+// (affinity mask capped by the cgroup quota), at least 4.
+int host_call_slots();
 
 // ---- plans (rs_capi.cpp) ------------------------------------------------------------
 int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, const std::vector<uint32_t>& in_idx,

@@ -3,9 +3,11 @@
 #include "host_pipeline.hpp"
 
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 
 namespace slime {
@@ -48,10 +50,33 @@ int Workspace::ensure_stages() {
   DeviceScope ds(device);
   for (int i = 0; i < kHostStages; ++i) {
     HIP_TRY(hipStreamCreateWithFlags(&sst[i], hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&sev[i], hipEventDisableTiming | hipEventBlockingSync));
   }
-  HIP_TRY(hipEventCreateWithFlags(&cev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&cev, hipEventDisableTiming | hipEventBlockingSync));
   return 0;
+}
+
+// Polling window of wait_event: the kernel of a 4 KiB call finishes ~10 us
+// after its launch; a sleeping wait costs a wake-up on top of that.
+constexpr std::chrono::microseconds kPollWindow{30};
+
+int wait_event(hipEvent_t ev) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return fail_hip(q, "hipEventQuery");
+    if ((i & 7) == 7 && std::chrono::steady_clock::now() - t0 > kPollWindow) break;
+    for (int k = 0; k < 64; ++k) _mm_pause();
+  }
+  HIP_TRY(hipEventSynchronize(ev));
+  return 0;
+}
+
+int sync_ws(Workspace* ws) {
+  if (int rc = ws->ensure_stages()) return rc;
+  HIP_TRY(hipEventRecord(ws->cev, ws->stream));
+  return wait_event(ws->cev);
 }
 
 int Workspace::fence_stages(int nstages) {
@@ -108,7 +133,7 @@ int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
   for (int s = 0; s < S; ++s) HIP_TRY(hipStreamWaitEvent(ws->sst[s], ws->cev, 0));
   auto land = [&](size_t p) -> int {
     const int s = (int)(p % S);
-    HIP_TRY(hipEventSynchronize(ws->sev[s]));
+    if (int rc = wait_event(ws->sev[s])) return rc;
     const CopyItem it{pcs[p].host, ws->pin + (size_t)s * kStageBytes, pcs[p].bytes};
     parallel_copy(&it, 1);
     return 0;

@@ -212,7 +212,7 @@ int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int total, u
     if (!one || (ms[1] & 1u)) {  // every window has landed: the flags are complete
       HIP_TRY(launch_select_mapping(d_map, d_status, 1, ws->stream));
       HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
-      HIP_TRY(hipStreamSynchronize(ws->stream));
+      if (int rc = sync_ws(ws)) return rc;
     } else {
       ms[0] = ms[1] = 0;
     }
@@ -227,7 +227,7 @@ int write_chunks_impl(const uint8_t* data, uint64_t size, int need, int total, u
       if (int rc = slime_rs_resolve_fallbacks(plan, slot, stride, size, 1, d_map, d_status, ws->stream, nullptr))
         return rc;
       HIP_TRY(hipMemcpyAsync(ms, d_map, sizeof(ms), hipMemcpyDeviceToHost, ws->stream));
-      HIP_TRY(hipStreamSynchronize(ws->stream));
+      if (int rc = sync_ws(ws)) return rc;
     } else if (ms[0] != 0) {  // mapping 1<<31: re-encode the whole object (map.go:47-62)
       HIP_TRY(launch_encode_bytes(bytes_launch(plan, slot, stride, 0, L, size, 1, 1, d_status, d_map), ws->stream));
     }

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -31,6 +32,7 @@
 #include "device_pool.hpp"
 #include "digest.hpp"
 #include "gfp_host.hpp"
+#include "host_copy.hpp"
 #include "host_pipeline.hpp"
 #include "kernels.hpp"
 #include "mfma_table.hpp"
@@ -90,14 +92,62 @@ const std::vector<int>& pool_devices() {
 const slime_rs_call_t* active_call() { return t_call; }
 int selected_device() { return t_device; }
 
+// Admission of host calls.  A host call keeps CPUs busy (its host copies,
+// the launches, the waits' polling, the copy pool's help), so more calls at
+// once than the process has CPUs only time-slice them -- and under a cgroup
+// CPU quota the whole process is throttled for the rest of the quota period
+// once it overdraws: 25 concurrent 1 MiB callers on a 16-CPU share ran 17.5
+// GiB/s with a 36 ms p99 against 26.8 GiB/s and 0.8 ms at 16 callers
+// (profiles/r05/s3_refactor, s5_sched).  Callers beyond the slots sleep on a
+// condition variable until one frees; a Go proxy's goroutines (main.go:107-109)
+// wait there instead of on the CPU.
+namespace {
+class HostCallSlots {
+ public:
+  explicit HostCallSlots(int n) : free_(n) {}
+  void enter() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return free_ > 0; });
+    --free_;
+  }
+  void leave() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++free_;
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int free_;
+};
+HostCallSlots& host_slots() {
+  static auto* s = new HostCallSlots(host_call_slots());  // never destroyed (callers may outlive statics)
+  return *s;
+}
+}  // namespace
+
+int host_call_slots() {
+  static const int n = std::max(4, usable_cpus() / 2);
+  return n;
+}
+
 int DeviceLease::acquire() {
   const int call = t_call ? t_call->device : SLIME_RS_ANY_DEVICE;
   const int thread = t_call ? SLIME_RS_ANY_DEVICE : t_device;
   const int want = call != SLIME_RS_ANY_DEVICE ? call : thread;
   if (int rc = check_device(want != SLIME_RS_ANY_DEVICE ? want : 0)) return rc;
+  host_slots().enter();
+  slot_ = true;
   lease.take(g_pool, call, thread, pool_devices());
   device = lease.device;
   return 0;
+}
+
+DeviceLease::~DeviceLease() {
+  if (slot_) host_slots().leave();
 }
 
 // ---- plans -----------------------------------------------------------------
@@ -898,6 +948,8 @@ int slime_rs_host_stats(slime_rs_host_stats_t* st, int reset) {
   st->total_us = take(g_host_stats.total_us);
   return 0;
 }
+
+int slime_rs_host_call_slots(void) { return host_call_slots(); }
 
 int slime_rs_pool_calls(int device, uint64_t* calls, int* inflight) {
   if (device < 0 || device >= DevicePool::kMax) return fail(Status::InvalidArg, "pool_calls: device out of range");
