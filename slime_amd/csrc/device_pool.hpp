@@ -17,6 +17,8 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -124,6 +126,49 @@ class PerDeviceFreeList {
  private:
   mutable std::mutex mu_;
   std::vector<T*> free_;
+};
+
+// A fixed number of slots handed out in arrival order (rs_capi.cpp uses one
+// for the process's concurrent host calls): enter() takes a free slot when
+// nobody waits, else sleeps until leave() hands it the slot of a finishing
+// caller -- a freed slot goes straight to the oldest waiter.
+class HostCallSlots {
+ public:
+  explicit HostCallSlots(int n) : free_(n) {}
+  void enter() {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (free_ > 0 && waiting_.empty()) {
+      --free_;
+      return;
+    }
+    Waiter w;
+    waiting_.push_back(&w);
+    w.cv.wait(lk, [&] { return w.granted; });
+  }
+  size_t waiting() const {  // callers asleep in enter() (tests)
+    std::lock_guard<std::mutex> lk(mu_);
+    return waiting_.size();
+  }
+  void leave() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (waiting_.empty()) {
+      ++free_;
+      return;
+    }
+    Waiter* w = waiting_.front();  // the slot passes to the oldest waiter
+    waiting_.pop_front();
+    w->granted = true;
+    w->cv.notify_one();  // under the lock: w lives on its waiter's stack until it sees `granted`
+  }
+
+ private:
+  struct Waiter {
+    std::condition_variable cv;
+    bool granted = false;
+  };
+  mutable std::mutex mu_;
+  std::deque<Waiter*> waiting_;
+  int free_;
 };
 
 }  // namespace slime

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -98,31 +99,13 @@ int selected_device() { return t_device; }
 // CPU quota the whole process is throttled for the rest of the quota period
 // once it overdraws: 25 concurrent 1 MiB callers on a 16-CPU share ran 17.5
 // GiB/s with a 36 ms p99 against 26.8 GiB/s and 0.8 ms at 16 callers
-// (profiles/r05/s3_refactor, s5_sched).  Callers beyond the slots sleep on a
-// condition variable until one frees; a Go proxy's goroutines (main.go:107-109)
-// wait there instead of on the CPU.
+// (profiles/r05/s3_refactor, s5_sched).  Callers beyond the slots sleep
+// until one frees; a Go proxy's goroutines (main.go:107-109) wait there
+// instead of on the CPU.  Slots pass in arrival order (a freed slot goes
+// straight to the oldest waiter): with a plain condition variable a caller
+// could lose the race for a freed slot again and again -- 64 MiB requests
+// waited up to 1.8 s behind others that took 15 ms (profiles/r05/s6_slots).
 namespace {
-class HostCallSlots {
- public:
-  explicit HostCallSlots(int n) : free_(n) {}
-  void enter() {
-    std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return free_ > 0; });
-    --free_;
-  }
-  void leave() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      ++free_;
-    }
-    cv_.notify_one();
-  }
-
- private:
-  std::mutex mu_;
-  std::condition_variable cv_;
-  int free_;
-};
 HostCallSlots& host_slots() {
   static auto* s = new HostCallSlots(host_call_slots());  // never destroyed (callers may outlive statics)
   return *s;

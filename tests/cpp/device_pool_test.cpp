@@ -146,6 +146,53 @@ int main() {
     CHECK(next.device == freed);
     std::printf("ok   TestLeastLoaded\n");
   }
-  std::printf("4/4 passed\n");
+  {  // host-call slots: at most n callers inside, freed slots go to the oldest waiter
+    constexpr int kSlots = 3, kCallers = 12, kRounds = 40;
+    HostCallSlots slots(kSlots);
+    std::atomic<int> inside{0}, peak{0};
+    std::mutex order_mu;
+    std::vector<int> entered;  // caller ids in the order they got a slot
+    std::vector<std::thread> th;
+    for (int t = 0; t < kCallers; ++t)
+      th.emplace_back([&, t] {
+        for (int r = 0; r < kRounds; ++r) {
+          slots.enter();
+          const int now = inside.fetch_add(1) + 1;
+          int p = peak.load();
+          while (now > p && !peak.compare_exchange_weak(p, now)) {
+          }
+          {
+            std::lock_guard<std::mutex> lk(order_mu);
+            entered.push_back(t);
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(200));
+          inside.fetch_sub(1);
+          slots.leave();
+        }
+      });
+    for (auto& x : th) x.join();
+    CHECK(peak.load() <= kSlots && peak.load() >= 1);
+    CHECK((int)entered.size() == kCallers * kRounds);
+    CHECK(slots.waiting() == 0);
+    // Arrival order: one slot held, six callers queued one after another,
+    // then the slot released -- each finishing caller hands it to the next.
+    HostCallSlots one(1);
+    one.enter();
+    std::vector<int> order;
+    std::vector<std::thread> q;
+    for (int t = 0; t < 6; ++t) {
+      q.emplace_back([&, t] {
+        one.enter();
+        order.push_back(t);  // one caller inside at a time
+        one.leave();
+      });
+      while (one.waiting() != (size_t)t + 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    one.leave();
+    for (auto& x : q) x.join();
+    CHECK((order == std::vector<int>{0, 1, 2, 3, 4, 5}));
+    std::printf("ok   TestHostCallSlotsFifo\n");
+  }
+  std::printf("5/5 passed\n");
   return 0;
 }

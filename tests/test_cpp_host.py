@@ -82,7 +82,8 @@ def test_device_pool_routing_with_a_fixed_device_count():
     subprocess.run(["make", "-C", ROOT, "tests/cpp/device_pool_test"], check=True, capture_output=True)
     r = subprocess.run([POOL_BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    for name in ("TestAllowedDevices", "TestPoolSpreadsConcurrentCallers", "TestPinnedDevices", "TestLeastLoaded"):
+    for name in ("TestAllowedDevices", "TestPoolSpreadsConcurrentCallers", "TestPinnedDevices", "TestLeastLoaded",
+                 "TestHostCallSlotsFifo"):
         assert f"ok   {name}" in r.stdout
 
 
