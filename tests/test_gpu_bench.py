@@ -79,3 +79,21 @@ def test_unchanged_caller_split_adds_up():
         t = u[side]["total_ms"]
         assert t["min"] <= t["median"] <= t["max"] and len(u[side]["reps_ms"]) == 7
     assert "map_from_gf_x12_concurrent" in u["write"]["split_ms"]
+
+
+def test_callers_beyond_the_host_call_slots_queue_and_finish():
+    """More concurrent callers than host-call slots (slime_rs_host_call_slots):
+    the surplus waits asleep for a slot and every request still completes and
+    verifies; the slots pass in arrival order, so no caller's worst request
+    waits more than a few rounds of everyone else's."""
+    lib = _proxy()
+    slots = N.lib.slime_rs_host_call_slots()
+    assert slots >= 4
+    threads = 3 * slots
+    out = (ctypes.c_double * 10)()
+    have = (ctypes.c_int * 8)(*range(4, 12))
+    rc = lib.proxy_load(threads, 96 << 10, 8, 12, have, 0, 0.5, 5, out)
+    assert rc == 0 and out[2] == 1.0 and out[8] == 0, list(out)
+    assert out[0] >= threads
+    put_p50, put_p99 = out[4], out[5]
+    assert put_p99 < max(20 * put_p50, 25.0), (put_p50, put_p99)  # no starved caller (ms)
