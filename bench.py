@@ -1189,7 +1189,8 @@ def pooled_leg(args, rank: int, world: int, devices: list[int]) -> dict | None:
                "need": need, "total": total, "erased": erase,
                "workloads": legs, "verified": ok,
                "what": "one process, --pool-threads concurrent PUT (writeChunks) + GET (reconstruct) requests per "
-                       "thread loop, every call through the cgo shim's *_ex forms with SLIME_RS_ANY_DEVICE over the "
+                       "thread loop (fused: the shim's WriteChunks, whole data chunks aliasing the object), every call "
+                       "through the cgo shim's *_ex forms with SLIME_RS_ANY_DEVICE over the "
                        "GPUs of all N ranks (tools/proxy_load.cpp); gibs = object bytes written + read per second; "
                        "per-request p50/p99 ms; verified = each thread's first and last GET returned its object, "
                        "its chunks were stable, and the unchanged caller's chunks equal the fused path's"}

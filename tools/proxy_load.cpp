@@ -9,7 +9,9 @@
 // proxy_load() through ctypes (no Python between the calls: goroutines do
 // not take a GIL).
 //
-// pattern 0 (fused): slime_rs_write_chunks_ex + slime_rs_reconstruct_ex.
+// pattern 0 (fused): slime_rs_write_chunks_ex + slime_rs_reconstruct_ex, the
+//   data chunks that lie wholly inside the object aliasing it as the shim's
+//   WriteChunks passes them (go/internal/rs/rs.go chunkBuffers: no copy).
 // pattern 1 (unchanged caller, multi_store.go as it is):
 //   PUT = MapToGF (:526) + splitVector (:527, in place) + r x CreateParity
 //         (:528-531) + a MapFromGF per chunk (:554);
@@ -91,8 +93,14 @@ struct Request {
     fill_random(data.data(), S, seed);
     out.assign((size_t)need * cb + 16, 0);
     chunks.assign(total, std::vector<uint8_t>(cb));
-    for (auto& c : chunks) cptr.push_back(c.data());
-    for (int q = 0; q < need; ++q) surv.push_back(chunks[have[q]].data());
+    // The shim's WriteChunks (go/internal/rs/rs.go, chunkBuffers): a data
+    // chunk that lies wholly inside the object is a subslice of it, so the
+    // library never copies it; the unchanged caller's chunks are MapFromGF's
+    // fresh outputs.
+    for (int i = 0; i < total; ++i)
+      cptr.push_back(pattern == 0 && i < need && (uint64_t)(i + 1) * cb <= S ? data.data() + (uint64_t)i * cb
+                                                                             : chunks[i].data());
+    for (int q = 0; q < need; ++q) surv.push_back(cptr[have[q]]);
     if (pattern == 1) {
       words.assign((size_t)need * L, 0u);  // splitVector's zero padding stays zero
       for (int j = 0; j < need; ++j) parts.push_back(words.data() + (size_t)j * L);
@@ -138,7 +146,7 @@ struct Request {
 
   uint64_t chunk_hash() const {
     uint64_t h = 0;
-    for (const auto& c : chunks) h = h * 31 + hash_bytes(c.data(), c.size());
+    for (uint8_t* c : cptr) h = h * 31 + hash_bytes(c, cb);
     return h;
   }
   bool got_object() const { return memcmp(out.data(), data.data(), S) == 0; }
