@@ -112,3 +112,9 @@ tools/libplaceprobe.so: tools/placement_probe.hip
 tools/vmm_probe: tools/vmm_probe.hip include/slime_rs.h $(LIB)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
 	  -Wl,-rpath,'$$ORIGIN/../slime_amd/lib'
+
+# Matrix-core apply variants at five K steps (tools only): make widevar
+widevar: tools/libwidevar.so
+tools/libwidevar.so: tools/wide_variants.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: widevar

@@ -41,6 +41,7 @@ struct slime_rs_plan {
   const uint8_t* d_mfma = nullptr;     // device: matrix-core digit table (mfma_table.hpp), or null
   const uint8_t* d_mfma_be = nullptr;  // the same for big-endian chunk words (the byte path)
   uint32_t in_max = 0;                 // highest input shard index
+  bool in_seq = false;                 // in_idx is 0..k-1 (encode plans)
 };
 
 namespace slime {

@@ -35,6 +35,7 @@ struct ApplyLaunch {
   // index (the kernel's 32-bit offsets need every object under 4 GiB).
   const uint8_t* mfma = nullptr;
   uint32_t in_max = 0, out_max = 0;
+  bool in_seq = false;  // in_idx is 0..k-1 (encode plans): uniform input offsets
 };
 
 // Matrix-core apply kernel: whether this launch can take it (table present,

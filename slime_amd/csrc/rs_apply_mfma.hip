@@ -39,7 +39,7 @@ namespace {
 // per shard, the refill streaming across objects) measured 0-6% slower than
 // this walk at 40/48, 48/64, 64/80 and 80/100 (profiles/r03/s33_mfma_queue_bytes/).
 // Non-temporal loads and stores (read-once / write-once streams).
-template <int KS>
+template <int KS, bool UNI>
 hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint32_t mt = mfma::mtiles(a.rows);
   const uint32_t lds = apply::mfma_lds_bytes(mt, KS);
@@ -47,12 +47,12 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
   const uint64_t gy = nwork < 65535 ? nwork : 65535;
-  const uint64_t target = 256ull * apply::kMfmaWaves;  // resident blocks
+  const uint64_t target = 256ull * apply::mfma_waves(KS, apply::mfma_width(KS));  // resident blocks
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, true, true>), dim3((uint32_t)gx, (uint32_t)gy),
+  hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, true, true, UNI>), dim3((uint32_t)gx, (uint32_t)gy),
                      dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
                      a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
                      a.rows, a.k, nseg);
@@ -63,13 +63,14 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
 
 hipError_t launch_apply_mfma(const ApplyLaunch& a, hipStream_t stream) {
   switch (mfma::ksteps(a.k)) {
-    case 1: return launch_ks<1>(a, stream);
-    case 2: return launch_ks<2>(a, stream);
-    case 3: return launch_ks<3>(a, stream);
-    case 4: return launch_ks<4>(a, stream);
-    case 5: return launch_ks<5>(a, stream);
-    case 6: return launch_ks<6>(a, stream);
-    case 7: return launch_ks<7>(a, stream);
+    case 1: return launch_ks<1, false>(a, stream);
+    case 2: return launch_ks<2, false>(a, stream);
+    case 3: return launch_ks<3, false>(a, stream);
+    case 4: return launch_ks<4, false>(a, stream);
+    // encodes at 65 <= k <= 80 on the uniform offsets
+    case 5: return a.in_seq ? launch_ks<5, true>(a, stream) : launch_ks<5, false>(a, stream);
+    case 6: return launch_ks<6, false>(a, stream);
+    case 7: return launch_ks<7, false>(a, stream);
     default: return hipErrorInvalidValue;  // mfma_eligible() rules this out
   }
 }

@@ -85,19 +85,21 @@ __device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
 __device__ void mfma_recombine4(const i32x4&, const i32x4&, const i32x4&, const i32x4&, uint64_t, uint64_t (&)[4]);
 #endif
 
-#ifndef SLIME_MFMA_W4_MAX_KS
-#define SLIME_MFMA_W4_MAX_KS 4  // 5 (four-column tiles in two passes) spills 9 VGPRs at two waves per SIMD
-#endif
-__host__ __device__ constexpr int mfma_w4_max_ks() { return SLIME_MFMA_W4_MAX_KS; }
-
-// Columns per lane of a tile: 4 up to k = 64, 2 above (at most 64 data VGPRs,
-// the accumulators in VGPRs), so the refill walk runs at two waves per SIMD.
-__host__ __device__ constexpr int mfma_width(int ks) { return ks <= mfma_w4_max_ks() ? 4 : 2; }
+// Columns per lane of a tile: 4 up to k = 80 (16-byte loads), 2 above (at
+// most 64 data VGPRs beside the accumulators at two waves per SIMD).
+__host__ __device__ constexpr int mfma_width(int ks) { return ks <= 5 ? 4 : 2; }
+// Waves per SIMD the matrix-core kernels are compiled for: two, and one for
+// four-column tiles at five K steps, whose data (80 VGPRs) and accumulators
+// (64) in one pass do not fit two -- one pass at one wave per SIMD beat two
+// column passes at two (the refill then overlaps only the second pass) and
+// two-column tiles: 80/100 encode 0.643 vs 0.618 / 0.625 (tools/wide_variants,
+// profiles/r05/s12_widevar/).
+constexpr int kMfmaWaves = 2;
+__host__ __device__ constexpr int mfma_waves(int ks, int w) { return ks == 5 && w == 4 ? 1 : kMfmaWaves; }
 // Column passes per K loop (mfma_rows): 2 where four-column tiles need their
 // accumulators halved to fit two waves per SIMD.
-__host__ __device__ constexpr int mfma_halves(int ks) { return ks > 4 && ks <= mfma_w4_max_ks() ? 2 : 1; }
-// Waves per SIMD the matrix-core kernels are compiled for.
-constexpr int kMfmaWaves = 2;
+__host__ __device__ constexpr int mfma_halves_at(int ks, int w, int waves) { return ks > 4 && w == 4 && waves == 2 ? 2 : 1; }
+__host__ __device__ constexpr int mfma_halves(int ks, int w) { return mfma_halves_at(ks, w, mfma_waves(ks, w)); }
 
 template <int W>
 using vec_t = uint32_t __attribute__((ext_vector_type(W)));
@@ -117,13 +119,56 @@ __device__ __forceinline__ void stw(char* p, vec_t<W> v) {
     *reinterpret_cast<vec_t<W>*>(p) = v;
 }
 
-template <int KS, int W, bool NTL>
-__device__ __forceinline__ void mfma_load_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ib,
-                                               const uint32_t (&soff)[KS][4], uint32_t colb) {
+// A lane's input byte offsets (from the object's base) for shard 16q + 4g + jj
+// of K step q.  General (decode: in_idx names the survivors): one per step and
+// shard.  Uniform (in_idx null, shards in order: the encodes): steps before the
+// last read step 0's shards 16q further on, so a step's address is a
+// wave-uniform base (ib + q * step, scalar registers) plus step 0's four
+// per-lane offsets; the last step keeps its own (shards past k read shard
+// k-1, see mfma_prologue).
+template <int KS, bool UNI>
+struct ShardOffs {
+  uint32_t o[KS][4];
+  __device__ __forceinline__ void init(const uint32_t* __restrict__ in_idx, uint64_t in_unit, uint32_t k, uint32_t g) {
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const uint32_t j = 16 * q + 4 * g + jj;
+        const uint32_t jc = j < k ? j : k - 1;
+        o[q][jj] = (uint32_t)((in_idx ? in_idx[jc] : jc) * in_unit);
+      }
+  }
+  __device__ __forceinline__ const char* at(const char* ib, int q, int jj, uint32_t colb) const {
+    return ib + (uint32_t)(o[q][jj] + colb);
+  }
+};
+template <int KS>
+struct ShardOffs<KS, true> {
+  uint32_t o0[4], ol[4];
+  uint64_t step;  // 16 shards, in bytes
+  __device__ __forceinline__ void init(const uint32_t* __restrict__, uint64_t in_unit, uint32_t k, uint32_t g) {
+    step = 16 * in_unit;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const uint32_t j = 16 * (KS - 1) + 4 * g + jj;
+      o0[jj] = (uint32_t)((4 * g + jj) * in_unit);
+      ol[jj] = (uint32_t)((j < k ? j : k - 1) * in_unit);
+    }
+  }
+  __device__ __forceinline__ const char* at(const char* ib, int q, int jj, uint32_t colb) const {
+    if (q == KS - 1) return ib + (uint32_t)(ol[jj] + colb);
+    return (ib + (uint64_t)q * step) + (uint32_t)(o0[jj] + colb);
+  }
+};
+
+template <int KS, int W, bool NTL, class SO>
+__device__ __forceinline__ void mfma_load_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ib, const SO& so,
+                                               uint32_t colb) {
 #pragma unroll
   for (int q = 0; q < KS; ++q)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ib + (uint32_t)(soff[q][jj] + colb));
+    for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(so.at(ib, q, jj, colb));
 }
 
 // Hook run on every loaded vector of a tile before its B fragments are
@@ -148,9 +193,10 @@ struct MfmaIO {
 // offset colbn), so
 // the next tile streams in one K step at a time behind the math and the wave
 // holds one tile of data registers instead of two.
-template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre>
-__device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn,
-                                          const uint32_t (&soff)[KS][4], uint32_t colbn,
+template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre, class SO,
+          int NH = mfma_halves(KS, W), bool SPLIT = false>
+__device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn, const SO& so,
+                                          uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
                                           const uint32_t* __restrict__ loff, uint32_t mb, uint32_t MT, uint32_t rows,
                                           uint32_t lane, uint32_t g, char* __restrict__ ob, uint32_t colb, bool store,
@@ -158,7 +204,6 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
   // NH passes over the K steps, each for W / NH of the lane's columns (its
   // accumulators and B fragments shrink by NH; the A fragments are read NH
   // times from LDS); the results wait in `out` for one W-wide store per row.
-  constexpr int NH = mfma_halves(KS);
   constexpr int CW = W / NH;
   uint32_t out[4][W];
 #pragma unroll
@@ -174,10 +219,18 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
 #pragma unroll
         for (int c = 0; c < CW; ++c) b[c][jj] = (int)(x[q][jj][h * CW + c] ^ io.xin);
       }
-      if constexpr (REFILL) {
+      if constexpr (REFILL && SPLIT) {
+        // pass h's columns of the next tile, as soon as this pass has its B fragments
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const vec_t<CW> v = ldw<CW, NTL>(so.at(ibn, q, jj, colbn + 4 * CW * h));
+#pragma unroll
+          for (int c = 0; c < CW; ++c) x[q][jj][h * CW + c] = v[c];
+        }
+      } else if constexpr (REFILL) {
         if (h == NH - 1) {
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(ibn + (uint32_t)(soff[q][jj] + colbn));
+          for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(so.at(ibn, q, jj, colbn));
         }
       }
 #pragma unroll
@@ -229,21 +282,22 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
   }
 }
 
-// One tile: every row block; with REFILL the last one reloads x with the
-// next tile (object base ibn, byte offset colbn).
-template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre>
-__device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn,
-                                          const uint32_t (&soff)[KS][4], uint32_t colbn,
+// One tile: every row block, the first (a full block of four M tiles) last:
+// with REFILL it reloads x with the next tile (object base ibn, byte offset
+// colbn), behind the most matrix work (rows 17-20: one M tile in the other).
+template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre, class SO,
+          int NH = mfma_halves(KS, W), bool SPLIT = false>
+__device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn, const SO& so,
+                                          uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
                                           const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows, uint32_t lane,
                                           uint32_t g, char* __restrict__ ob, uint32_t colb, bool store, MfmaIO io,
                                           Pre& pre) {
-  uint32_t mb = 0;
-  for (; mb + 4 < MT; mb += 4)
-    mfma_rows<KS, W, NTL, NTS, false, BSWAP>(x, ibn, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb,
-                                             store, io, pre);
-  mfma_rows<KS, W, NTL, NTS, REFILL, BSWAP>(x, ibn, soff, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g, ob, colb,
-                                            store, io, pre);
+  for (uint32_t mb = (MT - 1) & ~3u; mb > 0; mb -= 4)
+    mfma_rows<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH, SPLIT>(x, ibn, so, colbn, lfrag, lrowc, loff, mb, MT, rows,
+                                                                 lane, g, ob, colb, store, io, pre);
+  mfma_rows<KS, W, NTL, NTS, REFILL, BSWAP, Pre, SO, NH, SPLIT>(x, ibn, so, colbn, lfrag, lrowc, loff, 0, MT, rows, lane,
+                                                                g, ob, colb, store, io, pre);
 }
 
 // The tile walk of one wave over columns [c0, c1) of one object (c0, c1
@@ -251,9 +305,9 @@ __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __re
 // refilled K step by K step behind the math (mfma_rows).  The refill beat two
 // tile buffers and no prefetch at every K step count (profiles/r03/
 // s33_mfma_queue_bytes/, s35_mfma_bytes/), which were removed.
-template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class Pre>
-__device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob,
-                                          const uint32_t (&soff)[KS][4], const i32x4* __restrict__ lfrag,
+template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class Pre, class SO, int NH = mfma_halves(KS, W),
+          bool SPLIT = false>
+__device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so, const i32x4* __restrict__ lfrag,
                                           const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
                                           uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
                                           uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves, MfmaIO io,
@@ -267,14 +321,14 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
   };
   vec_t<W> x[KS][4];
   uint32_t t = wave;
-  if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, ib, soff, colb_of(t));
+  if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, ib, so, colb_of(t));
   while (t < ntiles) {
     const uint32_t tn = t + nwaves;
     if (tn < ntiles)
-      mfma_tile<KS, W, NTL, NTS, true, BSWAP>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
+      mfma_tile<KS, W, NTL, NTS, true, BSWAP, Pre, SO, NH, SPLIT>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
                                               colb_of(t), col_of(t) < c1, io, pre);
     else
-      mfma_tile<KS, W, NTL, NTS, false, BSWAP>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
+      mfma_tile<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH, SPLIT>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
                                                col_of(t) < c1, io, pre);
     t = tn;
   }
@@ -284,12 +338,12 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
 // output rows' byte offsets (out_idx[i] * out_unit), and each lane's input
 // byte offsets (in_idx[j] * in_unit, in_idx null: j; shards past k read shard in_idx[k-1],
 // whose digits are zero -- lines the lanes of shard k-1 fetch anyway).
-template <int KS>
+template <class SO>
 __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restrict__ table,
                                               const uint32_t* __restrict__ in_idx,
                                               const uint32_t* __restrict__ out_idx, uint64_t in_unit,
-                                              uint64_t out_unit, uint32_t MT, uint32_t rows, uint32_t k, uint32_t g,
-                                              uint64_t** lrowc, uint32_t** loff, uint32_t (&soff)[KS][4]) {
+                                              uint64_t out_unit, uint32_t MT, uint32_t KS, uint32_t rows, uint32_t k,
+                                              uint32_t g, uint64_t** lrowc, uint32_t** loff, SO& so) {
   const uint32_t nfrag = MT * KS * 64;
   const i32x4* gfrag = reinterpret_cast<const i32x4*>(table);
   for (uint32_t f = threadIdx.x; f < nfrag; f += kBlock) lds[f] = gfrag[f];
@@ -300,21 +354,15 @@ __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restr
     (*lrowc)[i] = i < rows ? growc[i] : 0;
     (*loff)[i] = i < rows ? (uint32_t)(out_idx[i] * out_unit) : 0;
   }
-#pragma unroll
-  for (int q = 0; q < KS; ++q)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const uint32_t j = 16 * q + 4 * g + jj;
-      const uint32_t jc = j < k ? j : k - 1;
-      soff[q][jj] = (uint32_t)((in_idx ? in_idx[jc] : jc) * in_unit);
-    }
+  so.init(in_idx, in_unit, k, g);
   __syncthreads();
 }
 
 // table: the plan's mfma table (mfma_table.hpp layout); coeff: the plan's
 // coefficient rows (column tails).
-template <int KS, bool NTL, bool NTS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMfmaWaves))) void rs_apply_mfma_kernel(
+// UNI: in_idx is 0..k-1 (ShardOffs<KS, true>: scalar step bases, 8 offset registers instead of 4 KS).
+template <int KS, bool NTL, bool NTS, bool UNI>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, mfma_width(KS))))) void rs_apply_mfma_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
@@ -325,8 +373,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMfmaWav
   const uint32_t lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
   uint64_t* lrowc;
   uint32_t* loff;
-  uint32_t soff[KS][4];
-  mfma_prologue<KS>(lds, table, in_idx, out_idx, in_shard * 4, out_shard * 4, MT, rows, k, g, &lrowc, &loff, soff);
+  ShardOffs<KS, UNI> so;
+  mfma_prologue(lds, table, in_idx, out_idx, in_shard * 4, out_shard * 4, MT, KS, rows, k, g, &lrowc, &loff, so);
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t nthr = (uint64_t)gridDim.x * kBlock;
   const uint32_t nvec = (uint32_t)(ncols >> 2);
@@ -343,7 +391,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMfmaWav
     const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
     const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
     if (v1 > v0)
-      mfma_walk<KS, W, NTL, NTS, false>(ib, ob, soff, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1, wave,
+      mfma_walk<KS, W, NTL, NTS, false>(ib, ob, so, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1, wave,
                                         nwaves, MfmaIO{0x80808080u, 0u}, nopre);
     if (seg == nseg - 1)
       for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)

@@ -78,9 +78,8 @@ struct FlagPre {
 __device__ __forceinline__ uint32_t flags_now(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <int KS, int W>
-__device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, char* __restrict__ ob,
-                                                 const uint32_t (&soff)[KS][4], const i32x4* __restrict__ lfrag,
+template <int KS, int W, int NH, class SO>
+__device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so, const i32x4* __restrict__ lfrag,
                                                  const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
                                                  uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
                                                  uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves,
@@ -92,7 +91,7 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
   uint32_t t = wave;
   if (t >= ntiles) return;
   apply::vec_t<W> x[KS][4];
-  apply::mfma_load_tile<KS, W, true>(x, ib, soff, colb_of(t));
+  apply::mfma_load_tile<KS, W, true>(x, ib, so, colb_of(t));
   uint32_t f = flags_now(fobj);
   while (t < ntiles) {
     const uint32_t tn = t + nwaves;
@@ -102,10 +101,10 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
     if (tn < ntiles) f = flags_now(fobj);  // tile tn's mapping, in flight during tile t
     const MfmaIO io{0x80808080u ^ be(m), m};
     if (tn < ntiles)
-      apply::mfma_tile<KS, W, true, true, true, true>(x, ib, soff, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane,
+      apply::mfma_tile<KS, W, true, true, true, true, FlagPre, SO, NH>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane,
                                                       g, ob, colb_of(t), true, io, pre);
     else
-      apply::mfma_tile<KS, W, true, true, false, true>(x, ib, soff, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob,
+      apply::mfma_tile<KS, W, true, true, false, true, FlagPre, SO, NH>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob,
                                                        colb_of(t), true, io, pre);
     const uint32_t fb = pre.bits();
     const uint32_t wf = (__ballot(fb & 1u) ? 1u : 0u) | (__ballot(fb & 2u) ? 2u : 0u);
@@ -133,10 +132,96 @@ __device__ __forceinline__ uint32_t encode_edges(uint8_t* slot, uint8_t* par, ui
   return F ? fl.bits() : 0u;
 }
 
+// The edge columns of an encode window, [4 e0, ncols): from the end of the
+// last whole matrix-core tile below the object's last word in chunk k-1 to the
+// window's last column.  The last data chunk is short by fewer than k words
+// (L = ceil(ceil(S/4)/k)), so the edges sit in the last segment (`spread`;
+// segments are whole tiles) unless the window is tiny -- then the segments'
+// own edge steps run.  The same columns for every object of a launch.
+struct EdgeSpan {
+  uint64_t e0;
+  bool spread;
+};
+template <uint32_t TCV>
+__device__ __forceinline__ EdgeSpan edge_span(uint64_t S, uint64_t L, uint64_t col0, uint32_t k, uint64_t nvec,
+                                              uint32_t nseg) {
+  const Segment last = segment_of(nseg - 1, nseg, nvec);
+  uint64_t end_max = interior_vectors(S, L, col0, k);
+  if (end_max > last.v1) end_max = last.v1;
+  EdgeSpan s;
+  s.spread = end_max >= last.v0;
+  s.e0 = last.v0 + (end_max > last.v0 ? (end_max - last.v0) / TCV * TCV : 0);
+  return s;
+}
+
+// Edge columns [b0, ncols) of every object `take` selects, as (object, row,
+// column) items spread over the whole grid, one per lane (consecutive lanes,
+// consecutive columns of one chunk): sum_j coeff[r][j] x_j over the data
+// chunks' symbols (splitVector padding, the partial last word), stored with
+// MapFromGF's mapping; row 0's items also write the data-chunk tails and (F)
+// fold MapToGF's flags into flags[obj].  Replaces a single wave's serial VALU
+// edge step per object (80 data chunks x 20 rows per column: ~0.1-0.2 ms of
+// tail on the 80/100 encode and its redo).  Rows of one column may read a
+// tail word before or after row 0 rewrote it: the rewrite is its packed
+// value (padding words read as zero either way), so every read agrees.
+template <bool F, class Take>
+__device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L,
+                                             uint64_t chunk, uint64_t col0, uint64_t ncols, const ObjWords& ow,
+                                             uint32_t nobj, uint32_t rows, uint32_t k, uint32_t cs,
+                                             const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+                                             uint64_t b0, uint32_t* __restrict__ flags, Take take) {
+  if (b0 >= ncols) return;
+  const uint64_t nc = ncols - b0, per = (uint64_t)rows * nc, total = per * nobj;
+  const uint64_t gw = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  const uint64_t gn = (uint64_t)gridDim.x * gridDim.y * kWaves;
+  for (uint64_t it = gw * 64 + (threadIdx.x & 63); it < total; it += gn * 64) {
+    const uint32_t o = (uint32_t)(it / per);
+    const uint64_t rem = it % per;
+    const uint32_t r = (uint32_t)(rem / nc);
+    const uint64_t b = b0 + rem % nc;
+    uint32_t m;
+    if (!take(o, m)) continue;
+    uint8_t* const slot = slots + (uint64_t)o * slot_stride + 4 * col0;
+    const uint32_t* const crow = coeff + (uint64_t)r * cs;
+    // Sixteen chunks at a time: their loads first (one memory latency per
+    // sixteen, not per chunk), then row 0's tail writes, then the sums.  Every
+    // row of a column folds the same flags.
+    Flags fl;
+    uint64_t lo = 0;
+    uint32_t hi = 0;
+    for (uint32_t j0 = 0; j0 < k; j0 += 16) {
+      uint32_t x[16][4];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        x[j][0] = 0;
+        if (j0 + j < k) load_data_symbol<false, F>(slot, chunk, L, col0, j0 + j, b, 1, ow, m, x[j], &fl);
+      }
+      if (r == 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j0 + j < k) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, 1, ow, m, x[j]);
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j0 + j < k) mac(lo, hi, x[j][0], crow[j0 + j]);
+    }
+    *reinterpret_cast<uint32_t*>(slot + ((uint64_t)k + out_idx[r]) * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
+    if constexpr (F) {
+      const uint32_t bits = fl.bits();
+      if (bits) atomicOr(&flags[o], bits);
+    }
+  }
+}
+
 // MODE 0: speculative pass (mapping 0, MapToGF flags into flags[obj]);
 // MODE 1: re-encode of the objects select_mapping gave mapping != 0 (status 0).
+// Phase 0 at two waves per SIMD at every width (at five K steps in two
+// column passes: one pass at one wave ran its flag folding and mapping switch
+// 3-14% slower, profiles/r05/s14_onewave/); the whole-object re-encode as
+// the other matrix-core kernels (mfma_waves).
 template <int KS, int MODE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
+constexpr int enc_waves() { return MODE == 0 ? apply::kMfmaWaves : apply::mfma_waves(KS, apply::mfma_width(KS)); }
+template <int KS, int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(enc_waves<KS, MODE>()))) void
 encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
                          const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
@@ -144,6 +229,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                          const uint32_t* __restrict__ mapping, uint32_t nseg, uint8_t* __restrict__ record,
                          uint32_t units) {
   constexpr int W = apply::mfma_width(KS);
+  constexpr int NH = apply::mfma_halves_at(KS, W, enc_waves<KS, MODE>());
   constexpr uint32_t TCV = 4 * W;  // tile width in 16-byte vectors
   constexpr bool F = MODE == 0;
   extern __shared__ i32x4 lds[];
@@ -151,14 +237,28 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
   uint64_t* lrowc;
   uint32_t* loff;
-  uint32_t soff[KS][4];
-  apply::mfma_prologue<KS>(lds, table, nullptr, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  apply::ShardOffs<KS, true> so;  // data chunks in order
+  apply::mfma_prologue(lds, table, nullptr, out_idx, chunk, chunk, MT, KS, rows, k, lg, &lrowc, &loff, so);
   const uint32_t cs = apply::wide_coeff_stride(k);
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
   const uint64_t nvec = ncols >> 2;
+  // Phase 0: every object's edge columns first, spread over the grid (their
+  // flags published before the tile walks start).
+  bool edges_done = false;
+  if constexpr (F) {
+    const EdgeSpan es = edge_span<TCV>(S, L, col0, k, nvec, nseg);
+    if (es.spread) {
+      spread_edges<true>(slots, slot_stride, L, chunk, col0, ncols, ow, nobj, rows, k, cs, coeff, out_idx, 4 * es.e0,
+                         flags, [](uint32_t, uint32_t& m) {
+                           m = 0;
+                           return true;
+                         });
+      edges_done = true;
+    }
+  }
   // Re-encode of up to 64 objects (one segment each): one flat tile walk over
   // the interior tiles of every object select_mapping gave 1<<31, so the grid
   // streams them back to back (the refill crosses objects) instead of
@@ -199,7 +299,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
       if (t < G * len && flat(t) >= T) t = next(t);
       apply::vec_t<W> x[KS][4];
       if (t < G * len)
-        apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(nth(flat(t) / nint))), soff,
+        apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(nth(flat(t) / nint))), so,
                                            colb_of(flat(t)));
       while (t < G * len) {
         const uint32_t tn = next(t);
@@ -211,10 +311,10 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
         if (tn < G * len) {
           const uint32_t fn = flat(tn);
           apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(nth(fn / nint))),
-                                                          soff, colb_of(fn), lds, lrowc, loff, MT, rows, lane, lg, ob,
+                                                          so, colb_of(fn), lds, lrowc, loff, MT, rows, lane, lg, ob,
                                                           colb_of(f), true, io, pre);
         } else {
-          apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg,
+          apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, so, 0, lds, lrowc, loff, MT, rows, lane, lg,
                                                            ob, colb_of(f), true, io, pre);
         }
         t = tn;
@@ -256,25 +356,25 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
         FlagPre pre;
         if (record) {  // the mid-object switch (mfma_switch_walk)
           uint32_t sent = 0;
-          mfma_switch_walk<KS, W>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), soff, lds, lrowc,
+          mfma_switch_walk<KS, W, NH>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc,
                                   loff, MT, rows, lane, lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves,
                                   flags + obj, record + (uint64_t)obj * units + v0 / TCV, pre, sent);
         } else {
-          apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par),
-                                                    soff, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
+          apply::mfma_walk<KS, W, true, true, true, FlagPre, apply::ShardOffs<KS, true>, NH>(
+              reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
                                                     4 * (v0 + nint * TCV), wave, nwaves, io, pre);
         }
         fbits = pre.bits();
       } else {
         apply::NoPre pre;
-        apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par),
-                                                  soff, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
+        apply::mfma_walk<KS, W, true, true, true, apply::NoPre, apply::ShardOffs<KS, true>, NH>(
+            reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
                                                   4 * (v0 + nint * TCV), wave, nwaves, io, pre);
       }
     }
     // Edge tiles and tail columns (VALU step, with the data-chunk tail fix).
     const uint64_t e0 = (uint64_t)v0 + (uint64_t)nint * TCV;
-    if (e0 < u1)
+    if (e0 < u1 && !edges_done)
       fbits |= encode_edges<F>(slot, par, chunk, L, col0, ow, first_tail_word, m, rows, k, cs, coeff, out_idx, e0, nvec,
                                u1, sg.v1, lane, wave, nwaves);
     if constexpr (F) {
@@ -319,8 +419,12 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
 // next entry's data streaming in behind the current one's math, across
 // objects), then every edge range of the objects mapped with 1<<31, segment
 // by segment as phase 0 cut them (phase 0 writes edges with mapping 0).
+// The redo at five K steps: four-column tiles in one pass at one wave per
+// SIMD (80/100 encode both passes 2.236 vs 2.267 ms at two waves and two
+// column passes, profiles/r05/s15_redowaves/).
+constexpr int redo_waves(int ks) { return ks == 5 ? 1 : apply::kMfmaWaves; }
 template <int KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(redo_waves(KS)))) void
 encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk,
                               uint64_t col0, uint64_t ncols, uint64_t S, uint32_t nobj, uint32_t rows, uint32_t k,
                               const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
@@ -328,14 +432,15 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
                               const uint32_t* __restrict__ mapping, uint32_t nseg, const uint32_t* __restrict__ list,
                               const uint32_t* __restrict__ count, uint32_t units) {
   constexpr int W = apply::mfma_width(KS);
+  constexpr int NH = apply::mfma_halves_at(KS, W, redo_waves(KS));
   constexpr uint32_t TCV = 4 * W;
   extern __shared__ i32x4 lds[];
   const uint32_t MT = (rows + 3) / 4;
   const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
   uint64_t* lrowc;
   uint32_t* loff;
-  uint32_t soff[KS][4];
-  apply::mfma_prologue<KS>(lds, table, nullptr, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  apply::ShardOffs<KS, true> so;
+  apply::mfma_prologue(lds, table, nullptr, out_idx, chunk, chunk, MT, KS, rows, k, lg, &lrowc, &loff, so);
   const uint32_t cs = apply::wide_coeff_stride(k);
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint64_t first_tail_word = ow.nw ? ow.nw - 1 : 0;
@@ -344,6 +449,15 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
   const uint64_t nvec = ncols >> 2;
   auto slot_of = [&](uint32_t o) { return slots + (uint64_t)o * slot_stride + 4 * col0; };
   auto colb_of = [&](uint32_t e) { return ((e % units) * (16 * W) + ln * W) << 2; };
+  // The switched objects' edge columns first, spread over the grid (phase 0
+  // wrote them with mapping 0).
+  const EdgeSpan es = edge_span<TCV>(S, L, col0, k, nvec, nseg);
+  if (es.spread)
+    spread_edges<false>(slots, slot_stride, L, chunk, col0, ncols, ow, nobj, rows, k, cs, coeff, out_idx, 4 * es.e0,
+                        nullptr, [&](uint32_t o, uint32_t& m) {
+                          m = mapping[o];
+                          return m != 0 && status[o] == 0;
+                        });
   const uint32_t n = *count;
   // The list (ascending tiles of each object, roughly) is cut into G
   // contiguous streams of 8 waves each, as the re-encode's flat walk: all
@@ -364,7 +478,7 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
     uint32_t mo = mapping[e / units];
     uint32_t en = i + 8 < hi ? list[i + 8] : e;
     uint32_t mn = i + 8 < hi ? mapping[en / units] : mo;
-    apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(e / units)), soff, colb_of(e));
+    apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(slot_of(e / units)), so, colb_of(e));
     while (i < hi) {
       const uint32_t in_ = i + 8;
       // entry in_ + 8's list word and mapping, in flight during this tile
@@ -374,11 +488,13 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
       const MfmaIO io{0x80808080u ^ be(m), m};
       char* const ob = reinterpret_cast<char*>(slot_of(o) + (uint64_t)k * chunk);
       if (in_ < hi)
-        apply::mfma_tile<KS, W, true, true, true, true>(x, reinterpret_cast<const char*>(slot_of(en / units)), soff,
+        apply::mfma_tile<KS, W, true, true, true, true, apply::NoPre, apply::ShardOffs<KS, true>, NH>(
+            x, reinterpret_cast<const char*>(slot_of(en / units)), so,
                                                         colb_of(en), lds, lrowc, loff, MT, rows, lane, lg, ob,
                                                         colb_of(e), true, io, pre);
       else
-        apply::mfma_tile<KS, W, true, true, false, true>(x, nullptr, soff, 0, lds, lrowc, loff, MT, rows, lane, lg, ob,
+        apply::mfma_tile<KS, W, true, true, false, true, apply::NoPre, apply::ShardOffs<KS, true>, NH>(
+            x, nullptr, so, 0, lds, lrowc, loff, MT, rows, lane, lg, ob,
                                                          colb_of(e), true, io, pre);
       const uint32_t mnn = in_ + 8 < hi ? mapping[enn / units] : mn;
       i = in_;
@@ -393,6 +509,7 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
   // a time with one ballot (a serial scan of every object's mapping and status
   // put two dependent loads per object in front of every wave); object i's
   // ranges start on waves offset by i * nwaves / count so they run side by side.
+  if (es.spread) return;
   const uint64_t iv = interior_vectors(S, L, col0, k);
   uint32_t nsel = 0;
   for (uint32_t ob = 0; ob < nobj; ob += 64) {
@@ -426,7 +543,7 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
 
 // Decode: survivors in_idx -> rebuilt chunks out_idx of the same slot.
 template <int KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::kMfmaWaves))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, apply::mfma_width(KS))))) void
 decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, const uint8_t* __restrict__ table,
                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
@@ -437,8 +554,8 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   const uint32_t lane = threadIdx.x & 63, lg = lane >> 4, ln = lane & 15;
   uint64_t* lrowc;
   uint32_t* loff;
-  uint32_t soff[KS][4];
-  apply::mfma_prologue<KS>(lds, table, in_idx, out_idx, chunk, chunk, MT, rows, k, lg, &lrowc, &loff, soff);
+  apply::ShardOffs<KS, false> so;  // survivors in_idx
+  apply::mfma_prologue(lds, table, in_idx, out_idx, chunk, chunk, MT, KS, rows, k, lg, &lrowc, &loff, so);
   const uint32_t cs = apply::wide_coeff_stride(k);
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
@@ -450,7 +567,7 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
     const uint32_t m = mapping[sg.obj];
     uint8_t* const slot = slots + (uint64_t)sg.obj * slot_stride + 4 * col0;  // window base
     if (sg.v1 > sg.v0)
-      apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot), soff,
+      apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot), so,
                                                 lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * (uint32_t)sg.v0,
                                                 4 * (uint32_t)sg.v1, wave, nwaves, MfmaIO{0x80808080u ^ be(m), m}, pre);
     // Columns past the last whole vector of the window, one per lane.
@@ -485,7 +602,9 @@ template <int KS>
 hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
-  const uint64_t blocks = 256ull * apply::kMfmaWaves;
+  const uint64_t blocks = 256ull * bytes::enc_waves<KS, 0>();  // resident blocks
+  const uint64_t blocks1 = 256ull * bytes::enc_waves<KS, 1>();
+  const uint64_t rblocks = 256ull * bytes::redo_waves(KS);
   if (a.phase == 0) {
     const uint32_t nseg = object_segments(a.nobj, ncols);
     // The mid-object switch runs when the caller handed scratch for its
@@ -522,12 +641,12 @@ hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
     hipLaunchKernelGGL(bytes::mfma_redo_list_kernel, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(kBlock), 0, s,
                        l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.list(a.scratch), count);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((bytes::encode_bytes_mfma_redo_kernel<KS>), dim3((uint32_t)blocks), dim3(kBlock), lds, s,
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_redo_kernel<KS>), dim3((uint32_t)rblocks), dim3(kBlock), lds, s,
                        a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma,
                        a.coeff, a.out_idx, a.flags, a.mapping, a.sw->nseg, l.list(a.scratch), count, l.units);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1>), bytes_grid(ncols, 1, 1, blocks, 1), dim3(kBlock), lds,
+  hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1>), bytes_grid(ncols, 1, 1, blocks1, 1), dim3(kBlock), lds,
                      s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma,
                      a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u);
   return hipGetLastError();
@@ -537,7 +656,7 @@ template <int KS>
 hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
-  const uint64_t blocks = 256ull * apply::kMfmaWaves;
+  const uint64_t blocks = 256ull * apply::mfma_waves(KS, apply::mfma_width(KS));
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS>),
                      bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,

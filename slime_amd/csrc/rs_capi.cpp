@@ -166,6 +166,8 @@ int build_plan(int device, uint32_t rows, uint32_t k, const uint32_t* coeff, con
     memcpy(host.data() + n_head + mt.size() / 4, mtb.data(), mtb.size());
   }
   plan->in_max = in_idx.empty() ? 0 : *std::max_element(in_idx.begin(), in_idx.end());
+  plan->in_seq = true;
+  for (uint32_t j = 0; j < in_idx.size(); ++j) plan->in_seq = plan->in_seq && in_idx[j] == j;
   DeviceScope ds(device);
   void* p = nullptr;
   HIP_TRY(hipMalloc(&p, host.size() * sizeof(uint32_t)));
@@ -218,6 +220,7 @@ int execute(const slime_rs_plan* plan, const uint32_t* src, uint64_t src_obj, ui
   a.coeff = plan->d_coeff;
   a.in_idx = plan->d_in_idx;
   a.out_idx = plan->d_out_idx;
+  a.in_seq = plan->in_seq;
   a.ncols = L;
   a.nobj = (uint32_t)nobj;
   a.rows = plan->rows;

@@ -53,6 +53,43 @@ for step in "$@"; do
                   run proxy_sched_$sc 300 python tools/proxy_sweep.py --threads 8,16,25 --mib 64,1 --seconds 1.5 --sched $sc || exit 1
                 done ;;
     latc) run latc 200 tools/latency_c 300 ;;
+    # wide codes, this tree's library against ab/base (the previous build), alternating in one box
+    wideab) E16=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15
+            WB="--steps 5 --warmup 2 $NOLEGS"
+            cp slime_amd/lib/libslime_rs.so /tmp/ab_new.so
+            for rep in 1 2; do
+              for v in new $(ls ab); do
+                if [ "$v" = new ]; then cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so; else cp ab/$v/libslime_rs.so slime_amd/lib/libslime_rs.so; fi
+                for shp in "80 100 $E16,16,17,18,19" "64 80 $E16" "72 90 $E16,16,17"; do
+                  set -- $shp
+                  run wab_$1_$2_${v}_$rep 300 python bench.py --need $1 --total $2 --objects 32 --erase $3 $WB || exit 1
+                done
+              done
+            done
+            cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
+    # which part of the wide kernel costs: rows 16 vs 20 at K steps 4 and 5 (symbol path)
+    wshape) for shp in "64 80" "64 84" "80 96" "80 100" "72 88" "72 90" "48 64" "48 68"; do
+              set -- $shp
+              E=$(python -c "print(','.join(map(str,range($2-$1))))")
+              run wsh_$1_$2 300 python bench.py --need $1 --total $2 --objects 32 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
+            done ;;
+    widevar) run widevar_80_100 300 python tools/wide_variants.py --need 80 --total 100 &&
+             run widevar_80_96 300 python tools/wide_variants.py --need 80 --total 96 &&
+             run widevar_72_90 300 python tools/wide_variants.py --need 72 --total 90 &&
+             run widevar_80_100b 300 python tools/wide_variants.py --need 80 --total 100 ;;
+    wpmc80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
+            pmc wpmc80_fetch FETCH_SIZE --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS &&
+            pmc wpmc80_write WRITE_SIZE --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS &&
+            pmc wpmc80_sq "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM" \
+              --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;
+    wshape2) for shp in "64 96" "80 96" "48 80" "64 80" "32 64" "80 100"; do
+              set -- $shp
+              E=$(python -c "print(','.join(map(str,range($2-$1))))")
+              run wsh2_$1_$2 300 python bench.py --need $1 --total $2 --objects 32 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
+            done ;;
+    wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
+             run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
+               python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;
     tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --bytes-path 0 ;;
