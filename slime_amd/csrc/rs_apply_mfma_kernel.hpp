@@ -11,7 +11,7 @@
 // fold per output symbol.
 //
 // Wave tile: 16 W consecutive columns of one object segment (W = 4, or 2
-// for k > 64 to halve the data registers).  Lane l (group g = l >> 4,
+// for k > 80 to halve the data registers).  Lane l (group g = l >> 4,
 // n = l & 15) loads 4W bytes (columns nW..nW+W-1 of the tile) of the shards
 // 16q + 4g + jj, jj = 0..3, for every K step q: one load instruction reads
 // 64W contiguous bytes of each of 4 shards.  Component c of those four
