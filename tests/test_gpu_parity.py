@@ -653,7 +653,7 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total
                                                # steps, four- and two-column lane tiles, many segments
                                                (25, 32, (3 << 20) + 1, 8), (40, 48, (4 << 20) + 2, 8),
                                                (64, 80, (8 << 20) + 3, 8), (80, 100, (6 << 20) + 1, 8),
-                                               (33, 40, (2 << 20) + 7, 16)])
+                                               (33, 40, (2 << 20) + 7, 16), (72, 90, (5 << 20) + 2, 8)])
 def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
     """The dynamic-schedule encode (and the matrix-core encode of wide codes)
     switches an object to 1<<31 as soon as a word >= p has been seen and the
