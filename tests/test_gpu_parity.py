@@ -1032,6 +1032,62 @@ def test_fuzz_random_shapes_and_layouts(torch_dev):
                 assert np.array_equal(got[o, i], h[o, t]), (case, need, total, L, erase, o, t)
 
 
+def test_fuzz_byte_path_random_shapes(torch_dev):
+    """Seeded random shapes on the fused byte path (writeChunks / reconstruct on
+    device, multi_store.go:526-557 and 185-242): the VALU, k-template and
+    matrix-core encodes with the mid-object switch, a word >= p planted at the
+    start, a random place or the last whole word (an edge column) of half the
+    objects, object sizes with every remainder mod 4, then a random erasure set
+    repaired in place from shuffled survivors; every chunk byte against the
+    oracle's framing."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = random.Random(0xB17E)
+    for case in range(24):
+        need = rng.choice([1, 2, 3, 4, 8, 10, 12, 16, 17, 24, 25, 32, 33, 40, 48, 64, 65, 72, 80, 96])
+        total = need + rng.randint(1, min(20, 100 - need))
+        S = rng.choice([1, 3, 4, 17, 4097, rng.randint(1, 1 << 16), rng.randint(1 << 18, 3 << 20)])
+        nobj = rng.randint(1, 6)
+        nrng = np.random.default_rng(case)
+        objs = []
+        for _ in range(nobj):
+            b = bytearray(nrng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+            nfull = S // 4
+            if nfull:
+                w = np.frombuffer(b, dtype=">u4", count=nfull).copy()
+                w[(w >= 0x7FFFFFFB) & (w < 0x80000000)] ^= 0x00100000  # no random fallback
+                w[w >= 4294967291] = 0x01020304
+                b[:4 * nfull] = w.astype(">u4").tobytes()
+                if rng.random() < 0.5:
+                    a = rng.choice([0, rng.randrange(nfull), nfull - 1])
+                    b[4 * a: 4 * a + 4] = b"\xff\xff\xff\xfd"
+            objs.append(bytes(b))
+        slots, L, chunk, stride = _make_slots(torch, objs, need, total, extra=64)
+        mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+        status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+        D.encode_objects(D.Plan.encode(need, total), slots, stride, S, nobj, mapping, status)
+        torch.cuda.synchronize()
+        assert status.cpu().numpy().tolist() == [0] * nobj, (case, need, total, S)
+        ms = mapping.cpu().numpy().view(np.uint32)
+        h = slots.cpu().numpy()
+        for o, obj in enumerate(objs):
+            m, chunks = _oracle_chunks(obj, need, total)
+            assert ms[o] == m, (case, need, total, S, o)
+            for c in range(total):
+                got = h[o * stride + c * chunk: o * stride + (c + 1) * chunk].tobytes()
+                assert got == chunks[c], (case, need, total, S, o, c)
+            assert (h[o * stride + total * chunk: (o + 1) * stride] == 0xA5).all(), (case, "wrote past the chunks")
+        truth = slots.clone()
+        erase = sorted(rng.sample(range(total), rng.randint(1, total - need)))
+        have = [i for i in range(total) if i not in erase]
+        rng.shuffle(have)
+        rec = D.Plan.reconstruct(need, total, have[:need], erase).set_outputs(erase)
+        slots.view(nobj, stride)[:, : total * chunk].view(nobj, total, chunk)[:, erase, : 4 * L] = 0x5A
+        D.decode_objects(rec, slots, stride, L, nobj, mapping)
+        torch.cuda.synchronize()
+        assert torch.equal(slots, truth), (case, need, total, S, erase)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("need,total", [(4, 6), (8, 12), (10, 14), (16, 20), (20, 24), (17, 30), (40, 56)])
 def test_fallback_kernel_vs_oracle(torch_dev, need, total):
