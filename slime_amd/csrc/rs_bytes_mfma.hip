@@ -12,9 +12,12 @@
 // -- and results are stored as bswap(r ^ m).  No per-word byte swap on the
 // data path; the encode's MapToGF flags take bswap(w) of every data word.
 // Tiles whose every data word is a whole object word (the bulk) run on the
-// matrix cores; edge tiles (splitVector padding, the partial last word, the
-// data-chunk tails MapFromGF writes) and column tails take the VALU step of
-// the wide byte kernels (encode_wide_step, rs_bytes_kernel.hpp).
+// matrix cores; the encode's edge columns (splitVector padding, the partial
+// last word, the data-chunk tails MapFromGF writes, the vectors short of a
+// whole tile) run as (object, row, column) items spread over the grid
+// (spread_edges), or -- for windows too small to hold them in the last
+// segment -- the VALU step of the wide byte kernels (encode_wide_step,
+// rs_bytes_kernel.hpp); the repair's column tails run per lane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -116,8 +119,9 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
   }
 }
 
-// The edge steps of one segment (vectors [e0, u1)), out of line: inlined,
-// their registers would crowd the matrix-core walk's (two waves per SIMD).
+// The edge steps of one segment (vectors [e0, u1)), one vector per lane: the
+// windows whose edges spread_edges does not take, and the whole-object
+// re-encode.
 template <bool F>
 __device__ __forceinline__ uint32_t encode_edges(uint8_t* slot, uint8_t* par, uint64_t chunk, uint64_t L, uint64_t col0,
                                               ObjWords ow, uint64_t first_tail_word, uint32_t m, uint32_t rows,
