@@ -98,7 +98,9 @@ constexpr int kMfmaWaves = 2;
 __host__ __device__ constexpr int mfma_waves(int ks, int w) { return ks == 5 && w == 4 ? 1 : kMfmaWaves; }
 // Column passes per K loop (mfma_rows): 2 where four-column tiles need their
 // accumulators halved to fit two waves per SIMD.
-__host__ __device__ constexpr int mfma_halves_at(int ks, int w, int waves) { return ks > 4 && w == 4 && waves == 2 ? 2 : 1; }
+__host__ __device__ constexpr int mfma_halves_at(int ks, int w, int waves) {
+  return ks > 4 && w == 4 && waves == 2 ? 2 : 1;
+}
 __host__ __device__ constexpr int mfma_halves(int ks, int w) { return mfma_halves_at(ks, w, mfma_waves(ks, w)); }
 
 template <int W>
@@ -194,7 +196,7 @@ struct MfmaIO {
 // the next tile streams in one K step at a time behind the math and the wave
 // holds one tile of data registers instead of two.
 template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre, class SO,
-          int NH = mfma_halves(KS, W), bool SPLIT = false>
+          int NH = mfma_halves(KS, W)>
 __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn, const SO& so,
                                           uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
@@ -219,15 +221,9 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
 #pragma unroll
         for (int c = 0; c < CW; ++c) b[c][jj] = (int)(x[q][jj][h * CW + c] ^ io.xin);
       }
-      if constexpr (REFILL && SPLIT) {
-        // pass h's columns of the next tile, as soon as this pass has its B fragments
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const vec_t<CW> v = ldw<CW, NTL>(so.at(ibn, q, jj, colbn + 4 * CW * h));
-#pragma unroll
-          for (int c = 0; c < CW; ++c) x[q][jj][h * CW + c] = v[c];
-        }
-      } else if constexpr (REFILL) {
+      // (Refilling each pass's columns right after that pass -- half-width
+      // loads -- ran 0.36 of peak against 0.62: profiles/r05/s12_widevar/.)
+      if constexpr (REFILL) {
         if (h == NH - 1) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) x[q][jj] = ldw<W, NTL>(so.at(ibn, q, jj, colbn));
@@ -286,7 +282,7 @@ __device__ __forceinline__ void mfma_rows(vec_t<W> (&x)[KS][4], const char* __re
 // with REFILL it reloads x with the next tile (object base ibn, byte offset
 // colbn), behind the most matrix work (rows 17-20: one M tile in the other).
 template <int KS, int W, bool NTL, bool NTS, bool REFILL, bool BSWAP, class Pre, class SO,
-          int NH = mfma_halves(KS, W), bool SPLIT = false>
+          int NH = mfma_halves(KS, W)>
 __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __restrict__ ibn, const SO& so,
                                           uint32_t colbn,
                                           const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
@@ -294,10 +290,10 @@ __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __re
                                           uint32_t g, char* __restrict__ ob, uint32_t colb, bool store, MfmaIO io,
                                           Pre& pre) {
   for (uint32_t mb = (MT - 1) & ~3u; mb > 0; mb -= 4)
-    mfma_rows<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH, SPLIT>(x, ibn, so, colbn, lfrag, lrowc, loff, mb, MT, rows,
-                                                                 lane, g, ob, colb, store, io, pre);
-  mfma_rows<KS, W, NTL, NTS, REFILL, BSWAP, Pre, SO, NH, SPLIT>(x, ibn, so, colbn, lfrag, lrowc, loff, 0, MT, rows, lane,
-                                                                g, ob, colb, store, io, pre);
+    mfma_rows<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH>(x, ibn, so, colbn, lfrag, lrowc, loff, mb, MT, rows, lane, g,
+                                                          ob, colb, store, io, pre);
+  mfma_rows<KS, W, NTL, NTS, REFILL, BSWAP, Pre, SO, NH>(x, ibn, so, colbn, lfrag, lrowc, loff, 0, MT, rows, lane, g,
+                                                         ob, colb, store, io, pre);
 }
 
 // The tile walk of one wave over columns [c0, c1) of one object (c0, c1
@@ -305,9 +301,9 @@ __device__ __forceinline__ void mfma_tile(vec_t<W> (&x)[KS][4], const char* __re
 // refilled K step by K step behind the math (mfma_rows).  The refill beat two
 // tile buffers and no prefetch at every K step count (profiles/r03/
 // s33_mfma_queue_bytes/, s35_mfma_bytes/), which were removed.
-template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class Pre, class SO, int NH = mfma_halves(KS, W),
-          bool SPLIT = false>
-__device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so, const i32x4* __restrict__ lfrag,
+template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class Pre, class SO, int NH = mfma_halves(KS, W)>
+__device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so,
+                                          const i32x4* __restrict__ lfrag,
                                           const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
                                           uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
                                           uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves, MfmaIO io,
@@ -325,11 +321,11 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
   while (t < ntiles) {
     const uint32_t tn = t + nwaves;
     if (tn < ntiles)
-      mfma_tile<KS, W, NTL, NTS, true, BSWAP, Pre, SO, NH, SPLIT>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g, ob,
-                                              colb_of(t), col_of(t) < c1, io, pre);
+      mfma_tile<KS, W, NTL, NTS, true, BSWAP, Pre, SO, NH>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane,
+                                                          g, ob, colb_of(t), col_of(t) < c1, io, pre);
     else
-      mfma_tile<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH, SPLIT>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob, colb_of(t),
-                                               col_of(t) < c1, io, pre);
+      mfma_tile<KS, W, NTL, NTS, false, BSWAP, Pre, SO, NH>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob,
+                                                           colb_of(t), col_of(t) < c1, io, pre);
     t = tn;
   }
 }
@@ -362,7 +358,8 @@ __device__ __forceinline__ void mfma_prologue(i32x4* lds, const uint8_t* __restr
 // coefficient rows (column tails).
 // UNI: in_idx is 0..k-1 (ShardOffs<KS, true>: scalar step bases, 8 offset registers instead of 4 KS).
 template <int KS, bool NTL, bool NTS, bool UNI>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, mfma_width(KS))))) void rs_apply_mfma_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(mfma_waves(KS, mfma_width(KS))))) void
+rs_apply_mfma_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,

@@ -82,8 +82,9 @@ __device__ __forceinline__ uint32_t flags_now(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <int KS, int W, int NH, class SO>
-__device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so, const i32x4* __restrict__ lfrag,
-                                                 const uint64_t* __restrict__ lrowc, const uint32_t* __restrict__ loff,
+__device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, char* __restrict__ ob, const SO& so,
+                                                 const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
+                                                 const uint32_t* __restrict__ loff,
                                                  uint32_t MT, uint32_t rows, uint32_t lane, uint32_t g, uint32_t n,
                                                  uint32_t c0, uint32_t c1, uint32_t wave, uint32_t nwaves,
                                                  uint32_t* __restrict__ fobj, uint8_t* __restrict__ rec, FlagPre& pre,
@@ -104,11 +105,11 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
     if (tn < ntiles) f = flags_now(fobj);  // tile tn's mapping, in flight during tile t
     const MfmaIO io{0x80808080u ^ be(m), m};
     if (tn < ntiles)
-      apply::mfma_tile<KS, W, true, true, true, true, FlagPre, SO, NH>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane,
-                                                      g, ob, colb_of(t), true, io, pre);
+      apply::mfma_tile<KS, W, true, true, true, true, FlagPre, SO, NH>(x, ib, so, colb_of(tn), lfrag, lrowc, loff, MT,
+                                                                       rows, lane, g, ob, colb_of(t), true, io, pre);
     else
-      apply::mfma_tile<KS, W, true, true, false, true, FlagPre, SO, NH>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows, lane, g, ob,
-                                                       colb_of(t), true, io, pre);
+      apply::mfma_tile<KS, W, true, true, false, true, FlagPre, SO, NH>(x, ib, so, 0, lfrag, lrowc, loff, MT, rows,
+                                                                        lane, g, ob, colb_of(t), true, io, pre);
     const uint32_t fb = pre.bits();
     const uint32_t wf = (__ballot(fb & 1u) ? 1u : 0u) | (__ballot(fb & 2u) ? 2u : 0u);
     if (wf & ~sent) {
@@ -365,15 +366,15 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                                   flags + obj, record + (uint64_t)obj * units + v0 / TCV, pre, sent);
         } else {
           apply::mfma_walk<KS, W, true, true, true, FlagPre, apply::ShardOffs<KS, true>, NH>(
-              reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
-                                                    4 * (v0 + nint * TCV), wave, nwaves, io, pre);
+              reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane,
+              lg, ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io, pre);
         }
         fbits = pre.bits();
       } else {
         apply::NoPre pre;
         apply::mfma_walk<KS, W, true, true, true, apply::NoPre, apply::ShardOffs<KS, true>, NH>(
-            reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * v0,
-                                                  4 * (v0 + nint * TCV), wave, nwaves, io, pre);
+            reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(par), so, lds, lrowc, loff, MT, rows, lane, lg,
+            ln, 4 * v0, 4 * (v0 + nint * TCV), wave, nwaves, io, pre);
       }
     }
     // Edge tiles and tail columns (VALU step, with the data-chunk tail fix).
@@ -547,7 +548,8 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
 
 // Decode: survivors in_idx -> rebuilt chunks out_idx of the same slot.
 template <int KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, apply::mfma_width(KS))))) void
+__global__ __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, apply::mfma_width(KS))))) void
 decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, const uint8_t* __restrict__ table,
                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,

@@ -17,11 +17,11 @@ using namespace slime::apply;
 
 namespace {
 
-template <int KS, int W, int NH, bool SPLIT, int WAVES>
+template <int KS, int W, int NH, int WAVES>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void wv_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
-    uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ out_idx,
-    uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, uint32_t nseg) {
+    uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table,
+    const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, uint32_t nseg) {
   extern __shared__ i32x4 lds[];
   const uint32_t MT = (rows + 3) / 4;
   const uint32_t lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
@@ -43,13 +43,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, W
     const uint32_t v0 = seg * seg_vec < nvec ? seg * seg_vec : nvec;
     const uint32_t v1 = nvec - v0 > seg_vec ? v0 + seg_vec : nvec;
     if (v1 > v0)
-      mfma_walk<KS, W, true, true, false, NoPre, ShardOffs<KS, true>, NH, SPLIT>(
+      mfma_walk<KS, W, true, true, false, NoPre, ShardOffs<KS, true>, NH>(
           ib, ob, so, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1, wave, nwaves, MfmaIO{0x80808080u, 0u},
           nopre);
   }
 }
 
-template <int KS, int W, int NH, bool SPLIT, int WAVES>
+template <int KS, int W, int NH, int WAVES>
 hipError_t launch(const uint32_t* in, uint32_t* out, uint64_t in_obj, uint64_t in_shard, uint64_t out_obj,
                   uint64_t out_shard, const uint8_t* table, const uint32_t* out_idx, uint64_t ncols, uint32_t nobj,
                   uint32_t rows, uint32_t k, hipStream_t s) {
@@ -61,7 +61,7 @@ hipError_t launch(const uint32_t* in, uint32_t* out, uint64_t in_obj, uint64_t i
   const uint64_t gy = nwork < 65535 ? nwork : 65535;
   uint64_t gx = (256ull * WAVES + gy - 1) / gy;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((wv_kernel<KS, W, NH, SPLIT, WAVES>), dim3((uint32_t)gx, (uint32_t)gy), dim3(kBlock), lds, s, in,
+  hipLaunchKernelGGL((wv_kernel<KS, W, NH, WAVES>), dim3((uint32_t)gx, (uint32_t)gy), dim3(kBlock), lds, s, in,
                      out, in_obj, in_shard, out_obj, out_shard, table, out_idx, ncols, nobj, rows, k, nseg);
   return hipGetLastError();
 }
@@ -72,8 +72,8 @@ extern "C" {
 
 // Variant names, one per id (nullptr past the last).
 const char* wv_name(int v) {
-  static const char* names[] = {"W4 NH2 2w (product)", "W4 NH2 split-refill 2w", "W2 NH1 2w", "W4 NH1 1w",
-                                "W4 NH2 split-refill 1w", "W4 NH1 2w (spills)"};
+  // (split refills -- each column pass's half reloaded right after it -- ran 0.36 of peak: removed)
+  static const char* names[] = {"W4 NH2 2w", "W2 NH1 2w", "W4 NH1 1w (product)", "W4 NH1 2w (spills)"};
   return v >= 0 && v < (int)(sizeof(names) / sizeof(names[0])) ? names[v] : nullptr;
 }
 
@@ -88,15 +88,13 @@ int wv_launch(int v, const uint32_t* in, uint32_t* out, uint64_t in_obj, uint64_
               uint64_t out_shard, const uint8_t* table, const uint32_t* out_idx, uint64_t ncols, uint32_t nobj,
               uint32_t rows, uint32_t k, hipStream_t s) {
   if (mfma::ksteps(k) != 5 || rows > 32 || (ncols & 63)) return (int)hipErrorInvalidValue;
-#define WV(W, NH, SP, WV_) \
-  launch<5, W, NH, SP, WV_>(in, out, in_obj, in_shard, out_obj, out_shard, table, out_idx, ncols, nobj, rows, k, s)
+#define WV(W, NH, WV_) \
+  launch<5, W, NH, WV_>(in, out, in_obj, in_shard, out_obj, out_shard, table, out_idx, ncols, nobj, rows, k, s)
   switch (v) {
-    case 0: return (int)WV(4, 2, false, 2);
-    case 1: return (int)WV(4, 2, true, 2);
-    case 2: return (int)WV(2, 1, false, 2);
-    case 3: return (int)WV(4, 1, false, 1);
-    case 4: return (int)WV(4, 2, true, 1);
-    case 5: return (int)WV(4, 1, false, 2);
+    case 0: return (int)WV(4, 2, 2);
+    case 1: return (int)WV(2, 1, 2);
+    case 2: return (int)WV(4, 1, 1);
+    case 3: return (int)WV(4, 1, 2);
     default: return (int)hipErrorInvalidValue;
   }
 #undef WV
