@@ -10,8 +10,8 @@
 // the VALU does one XOR per loaded word plus an in-lane recombination and
 // fold per output symbol.
 //
-// Wave tile: 16 W consecutive columns of one object segment (W = 4, or 2
-// for k > 80 to halve the data registers).  Lane l (group g = l >> 4,
+// Wave tile: 16 W consecutive columns of one object segment (W = 4; the
+// byte encodes above k = 80 use 2, mfma_width).  Lane l (group g = l >> 4,
 // n = l & 15) loads 4W bytes (columns nW..nW+W-1 of the tile) of the shards
 // 16q + 4g + jj, jj = 0..3, for every K step q: one load instruction reads
 // 64W contiguous bytes of each of 4 shards.  Component c of those four
@@ -85,17 +85,19 @@ __device__ uint64_t mfma_recombine(const i32x4& d, uint64_t R);
 __device__ void mfma_recombine4(const i32x4&, const i32x4&, const i32x4&, const i32x4&, uint64_t, uint64_t (&)[4]);
 #endif
 
-// Columns per lane of a tile: 4 up to k = 80 (16-byte loads), 2 above (at
-// most 64 data VGPRs beside the accumulators at two waves per SIMD).
-__host__ __device__ constexpr int mfma_width(int ks) { return ks <= 5 ? 4 : 2; }
-// Waves per SIMD the matrix-core kernels are compiled for: two, and one for
-// four-column tiles at five K steps, whose data (80 VGPRs) and accumulators
-// (64) in one pass do not fit two -- one pass at one wave per SIMD beat two
-// column passes at two (the refill then overlaps only the second pass) and
-// two-column tiles: 80/100 encode 0.643 vs 0.618 / 0.625 (tools/wide_variants,
-// profiles/r05/s12_widevar/).
+// Columns per lane of a tile: 4 at every K step count (16-byte loads; the
+// byte encodes keep 2 above five K steps, rs_bytes_mfma.hip enc_width).
+__host__ __device__ constexpr int mfma_width(int ks) { return ks <= 7 ? 4 : 2; }
+// Waves per SIMD the matrix-core kernels are compiled for: two, and one from
+// five K steps on, where four-column tiles' data (80-112 VGPRs) and
+// accumulators (64) in one pass do not fit two -- one pass at one wave per
+// SIMD beat two column passes at two (the refill then overlaps only the
+// second pass) and two-column tiles: 80/100 encode 0.643 vs 0.618 / 0.625
+// (tools/wide_variants, profiles/r05/s12_widevar/); 96/100, 90/100 and
+// 100/116 encode and repair 2-7% faster than on two-column tiles
+// (profiles/r05/s21_ks67/).
 constexpr int kMfmaWaves = 2;
-__host__ __device__ constexpr int mfma_waves(int ks, int w) { return ks == 5 && w == 4 ? 1 : kMfmaWaves; }
+__host__ __device__ constexpr int mfma_waves(int ks, int w) { return ks >= 5 && w == 4 ? 1 : kMfmaWaves; }
 // Column passes per K loop (mfma_rows): 2 where four-column tiles need their
 // accumulators halved to fit two waves per SIMD.
 __host__ __device__ constexpr int mfma_halves_at(int ks, int w, int waves) {

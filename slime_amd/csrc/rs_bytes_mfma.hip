@@ -219,12 +219,16 @@ __device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64
 
 // MODE 0: speculative pass (mapping 0, MapToGF flags into flags[obj]);
 // MODE 1: re-encode of the objects select_mapping gave mapping != 0 (status 0).
-// Phase 0 at two waves per SIMD at every width (at five K steps in two
-// column passes: one pass at one wave ran its flag folding and mapping switch
-// 3-14% slower, profiles/r05/s14_onewave/); the whole-object re-encode as
-// the other matrix-core kernels (mfma_waves).
+// The encodes' tiles: four columns a lane up to five K steps, two above (six
+// and seven K steps on four columns spill at two waves per SIMD, and phase 0
+// stays at two: at five K steps in two column passes -- one pass at one wave
+// ran its flag folding and mapping switch 3-14% slower,
+// profiles/r05/s14_onewave/).  Phase 0, its redo and the whole-object
+// re-encode share the width (the redo walks phase 0's tiles); the redo and
+// the re-encode run at the other matrix-core kernels' waves (mfma_waves).
+constexpr int enc_width(int ks) { return ks <= 5 ? 4 : 2; }
 template <int KS, int MODE>
-constexpr int enc_waves() { return MODE == 0 ? apply::kMfmaWaves : apply::mfma_waves(KS, apply::mfma_width(KS)); }
+constexpr int enc_waves() { return MODE == 0 ? apply::kMfmaWaves : apply::mfma_waves(KS, enc_width(KS)); }
 template <int KS, int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(enc_waves<KS, MODE>()))) void
 encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
@@ -233,7 +237,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                          const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
                          const uint32_t* __restrict__ mapping, uint32_t nseg, uint8_t* __restrict__ record,
                          uint32_t units) {
-  constexpr int W = apply::mfma_width(KS);
+  constexpr int W = enc_width(KS);
   constexpr int NH = apply::mfma_halves_at(KS, W, enc_waves<KS, MODE>());
   constexpr uint32_t TCV = 4 * W;  // tile width in 16-byte vectors
   constexpr bool F = MODE == 0;
@@ -427,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
 // The redo at five K steps: four-column tiles in one pass at one wave per
 // SIMD (80/100 encode both passes 2.236 vs 2.267 ms at two waves and two
 // column passes, profiles/r05/s15_redowaves/).
-constexpr int redo_waves(int ks) { return ks == 5 ? 1 : apply::kMfmaWaves; }
+constexpr int redo_waves(int ks) { return apply::mfma_waves(ks, enc_width(ks)); }
 template <int KS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(redo_waves(KS)))) void
 encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk,
@@ -436,7 +440,7 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
                               const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ status,
                               const uint32_t* __restrict__ mapping, uint32_t nseg, const uint32_t* __restrict__ list,
                               const uint32_t* __restrict__ count, uint32_t units) {
-  constexpr int W = apply::mfma_width(KS);
+  constexpr int W = enc_width(KS);
   constexpr int NH = apply::mfma_halves_at(KS, W, redo_waves(KS));
   constexpr uint32_t TCV = 4 * W;
   extern __shared__ i32x4 lds[];
@@ -599,7 +603,7 @@ using apply::kBlock;
 // Interior tiles per object the switch record covers (one byte each).
 template <int KS>
 uint32_t switch_units(const BytesLaunch& a) {
-  constexpr uint64_t TCV = 4 * apply::mfma_width(KS);
+  constexpr uint64_t TCV = 4 * bytes::enc_width(KS);
   const uint64_t nvec = (a.ncols ? a.ncols : a.L) >> 2;
   return (uint32_t)((nvec + TCV - 1) / TCV);
 }

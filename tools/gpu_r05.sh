@@ -88,6 +88,20 @@ for step in "$@"; do
               E=$(python -c "print(','.join(map(str,range($2-$1))))")
               run wsh2_$1_$2 300 python bench.py --need $1 --total $2 --objects 32 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
             done ;;
+    # k > 80: this tree vs ab/* on 96/100, 90/100 (six K steps) and 100/116 (seven)
+    wideab2) WB="--steps 5 --warmup 2 $NOLEGS"
+             cp slime_amd/lib/libslime_rs.so /tmp/ab_new.so
+             for rep in 1 2; do
+               for v in new $(ls ab); do
+                 if [ "$v" = new ]; then cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so; else cp ab/$v/libslime_rs.so slime_amd/lib/libslime_rs.so; fi
+                 for shp in "96 100" "90 100" "100 116"; do
+                   set -- $shp
+                   E=$(python -c "print(','.join(map(str,range($2-$1))))")
+                   run wab_$1_$2_${v}_$rep 300 python bench.py --need $1 --total $2 --objects 32 --erase $E $WB || exit 1
+                 done
+               done
+             done
+             cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
     wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
              run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
                python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;
