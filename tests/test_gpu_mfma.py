@@ -61,8 +61,8 @@ def _apply_ref(coeff, x):
 
 @pytest.mark.parametrize("need,total", [(33, 34), (33, 50), (40, 56), (47, 48), (48, 64), (64, 80), (80, 100),
                                         (64, 96), (99, 100), (17, 25), (24, 32), (31, 40), (20, 24),
-                                        # five K steps with a clamped last step (uniform offsets)
-                                        (72, 90), (65, 81)])
+                                        # five K steps with a clamped last step (uniform offsets); six, seven
+                                        (72, 90), (65, 81), (90, 100), (100, 116)])
 @pytest.mark.parametrize("L", [1, 5, 64, 67, 1001, 4096 + 3])
 def test_encode_vs_oracle(torch_dev, matrix_cores, need, total, L):
     torch = torch_dev
@@ -82,7 +82,7 @@ def test_encode_vs_oracle(torch_dev, matrix_cores, need, total, L):
 
 
 @pytest.mark.parametrize("need,total,nerase", [(64, 80, 16), (40, 56, 5), (50, 82, 32), (96, 100, 4), (33, 50, 17),
-                                               (72, 90, 18), (80, 100, 20)])
+                                               (72, 90, 18), (80, 100, 20), (90, 100, 10), (100, 116, 16)])
 def test_reconstruct_shuffled_survivors_separate_dst(torch_dev, matrix_cores, need, total, nerase):
     torch = torch_dev
     from slime_amd import device as D
@@ -216,7 +216,8 @@ def test_bytes_encode_objects_vs_oracle(torch_dev, matrix_cores, need, total, S)
 
 @pytest.mark.parametrize("need,total,S,align", [(64, 80, (2 << 20) + 5, 256), (40, 56, 300001, 4096),
                                                 (80, 100, 1 << 20, 0), (33, 49, 123457, 0), (24, 32, 300001, 0),
-                                                (32, 40, 1 << 20, 256), (17, 25, 65537, 0), (72, 90, (1 << 20) + 3, 256)])
+                                                (32, 40, 1 << 20, 256), (17, 25, 65537, 0), (72, 90, (1 << 20) + 3, 256),
+                                                (96, 100, 300001, 0), (100, 116, (1 << 20) + 1, 256)])
 def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, total, S, align):
     torch = torch_dev
     from slime_amd import device as D
