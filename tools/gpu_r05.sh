@@ -38,6 +38,7 @@ for step in "$@"; do
     tests_switch) run pytest_switch 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "mid_object_switch or encode_objects or write_chunks or redo" ;;
     tests_mfma) run pytest_mfma 600 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 300 --timeout-method thread ;;
     tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "map or recover or host or unchanged or RecoverData or reconstruct or pool" ;;
+    tests_sched) run pytest_sched 400 python -u -m pytest tests/test_gpu_schedule.py -x -v --timeout 200 --timeout-method thread ;;
     tests_fuzz) run pytest_fuzz 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "fuzz" ;;
     tests_bench) run pytest_bench 400 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 200 --timeout-method thread ;;
     hostrep) for i in 1 2 3; do run hostrep_$i 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= --pooled 0 || exit 1; done ;;
