@@ -110,7 +110,10 @@ for step in "$@"; do
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchq) run benchq 400 python bench.py --steps 5 --warmup 1 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --bytes-path 0 ;;
     hostonly) run hostonly 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
-    rehearse2) run rehearse2 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 ;;
+    rehearse2) run rehearse2 400 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 &&
+               run rehearse2_torchrun 400 env SLIME_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --bytes-path 0 \
+                 --cpu-baseline 0 --alloc-probe 0 ;;
     # the driver's command under the profiler, without the pooled leg (rocprofv3 segfaulted
     # inside the runtime under its 25 concurrent host threads, profiles/r05/s4_pmc_c2/c2prof.log)
     profdrv) run profdrv 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
