@@ -103,6 +103,20 @@ for step in "$@"; do
                done
              done
              cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
+    widevar) for rep in 1 2; do
+               run wv_80_100_$rep 300 python tools/wide_variants.py --need 80 --total 100 --variants 0,2,5,6,7 &&
+               run wv_76_96_$rep 300 python tools/wide_variants.py --need 76 --total 96 --variants 0,2,5,6,7 || exit 1
+             done ;;
+    # do many input shards per wave cost through the address translation? the same bytes in
+    # objects whose shards share 2 MiB pages (32 MiB and 8 MiB objects) against 256 MiB objects
+    wtlb) for shp in "80 100" "64 80" "8 12"; do
+            set -- $shp
+            E=$(python -c "print(','.join(map(str,range(min(4, $2-$1)))))")
+            for om in "256 32" "32 256" "8 1024"; do
+              set -- $1 $2 $om
+              run wtlb_$1_$2_$3 300 python bench.py --need $1 --total $2 --object-mib $3 --objects $4 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
+            done
+          done ;;
     wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
              run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
                python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;

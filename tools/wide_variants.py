@@ -27,19 +27,20 @@ def main():
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--nobj", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--variants", default="0,2,5,6,7")
     a = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libwidevar.so"))
     lib.wv_name.restype = ctypes.c_char_p
     lib.wv_table.restype = ctypes.c_uint64
-    lib.wv_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+    lib.wv_table.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                             ctypes.c_uint64]
     lib.wv_launch.restype = ctypes.c_int
     lib.wv_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint64] * 4 + \
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
          ctypes.c_void_p]
     k, rows = a.need, a.total - a.need
     L = ((a.mib << 20) // 4 + k - 1) // k
-    L -= L % 64  # whole tiles (the harness has no column tail)
+    L -= L % 128  # whole tiles (the harness has no column tail)
     stride = L  # a multiple of 64 symbols
     obj = stride * a.total
     dev = torch.device("cuda:0")
@@ -48,16 +49,19 @@ def main():
     buf = torch.randint(-2**31, 2**31 - 5, (a.nobj * obj,), dtype=torch.int32, device=dev, generator=g)
     c = np.ascontiguousarray((np.random.default_rng(7).integers(0, 0xFFFFFFFB, rows * k, dtype=np.uint64))
                              .astype(np.uint32))
-    n = lib.wv_table(c.ctypes.data, rows, k, None, 0)
-    host = np.zeros(n, dtype=np.uint8)
-    lib.wv_table(c.ctypes.data, rows, k, host.ctypes.data, n)
-    table = torch.from_numpy(host).to(dev)
+    tables = {}
+    for form in (0, 4):  # the 16x16 table, the 32x32 table
+        n = lib.wv_table(form, c.ctypes.data, rows, k, None, 0)
+        host = np.zeros(n, dtype=np.uint8)
+        lib.wv_table(form, c.ctypes.data, rows, k, host.ctypes.data, n)
+        tables[form] = torch.from_numpy(host).to(dev)
     out_idx = torch.arange(k, a.total, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
     variants = [int(v) for v in a.variants.split(",")]
 
     def launch(v):
+        table = tables[4 if v >= 4 else 0]
         rc = lib.wv_launch(v, buf.data_ptr(), buf.data_ptr(), obj, stride, obj, stride, table.data_ptr(),
                            out_idx.data_ptr(), L, a.nobj, rows, k, sp)
         if rc:
