@@ -75,10 +75,6 @@ for step in "$@"; do
               E=$(python -c "print(','.join(map(str,range($2-$1))))")
               run wsh_$1_$2 300 python bench.py --need $1 --total $2 --objects 32 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
             done ;;
-    widevar) run widevar_80_100 300 python tools/wide_variants.py --need 80 --total 100 &&
-             run widevar_80_96 300 python tools/wide_variants.py --need 80 --total 96 &&
-             run widevar_72_90 300 python tools/wide_variants.py --need 72 --total 90 &&
-             run widevar_80_100b 300 python tools/wide_variants.py --need 80 --total 100 ;;
     wpmc80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
             pmc wpmc80_fetch FETCH_SIZE --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS &&
             pmc wpmc80_write WRITE_SIZE --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS &&
