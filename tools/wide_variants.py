@@ -12,7 +12,6 @@ import ctypes
 import json
 import os
 import statistics
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
