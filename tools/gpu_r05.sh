@@ -113,6 +113,10 @@ for step in "$@"; do
               run wtlb_$1_$2_$3 300 python bench.py --need $1 --total $2 --object-mib $3 --objects $4 --erase $E --bytes-path 0 --steps 5 --warmup 2 $NOLEGS || exit 1
             done
           done ;;
+    wilv) for rep in 1 2; do
+            run wilv_80_100_$rep 300 python tools/wide_variants.py --need 80 --total 100 --variants 0,2,8 &&
+            run wilv_72_90_$rep 300 python tools/wide_variants.py --need 72 --total 90 --variants 0,2,8 || exit 1
+          done ;;
     wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
              run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
                python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;

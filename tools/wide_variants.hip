@@ -203,6 +203,47 @@ std::vector<uint8_t> build(const uint32_t* coeff, uint32_t rows, uint32_t k) {
 }
 }  // namespace m32
 
+// ---- column-block interleaved layout (research: is the wide-code rate the
+// DRAM side of k concurrent shard streams?) ----
+// Block t of the buffer holds 64 columns of every shard: [total shards][64
+// symbols], 256 B per shard, so one wave tile reads one contiguous
+// total x 256 B region instead of k far-apart rows.  Same math as the
+// product's walk (mfma_tile, four-column tiles); the parity rows land in
+// their 256 B slots of the same block.
+template <int KS, int WAVES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void ilv_kernel(
+    const uint32_t* __restrict__ in, const uint8_t* __restrict__ table, const uint32_t* __restrict__ out_idx,
+    uint64_t nblocks, uint32_t total, uint32_t rows, uint32_t k) {
+  extern __shared__ i32x4 lds[];
+  const uint32_t MT = (rows + 3) / 4;
+  const uint32_t lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  uint64_t* lrowc;
+  uint32_t* loff;
+  ShardOffs<KS, true> so;
+  mfma_prologue(lds, table, nullptr, out_idx, 256, 256, MT, KS, rows, k, g, &lrowc, &loff, so);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gn = (uint64_t)gridDim.x * kWaves;
+  const uint64_t bstride = (uint64_t)total * 256;  // bytes per block
+  const char* base = reinterpret_cast<const char*>(in);
+  const uint32_t colb = n * 16;  // the lane's four columns in each 256 B shard slot
+  NoPre nopre;
+  vec_t<4> x[KS][4];
+  uint64_t t = gw;
+  if (t < nblocks) mfma_load_tile<KS, 4, true>(x, base + t * bstride, so, colb);
+  while (t < nblocks) {
+    const uint64_t tn = t + gn;
+    char* ob = const_cast<char*>(base + t * bstride);
+    if (tn < nblocks)
+      mfma_tile<KS, 4, true, true, true, false, NoPre, ShardOffs<KS, true>, 1>(
+          x, base + tn * bstride, so, colb, lds, lrowc, loff, MT, rows, lane, g, ob, colb, true,
+          MfmaIO{0x80808080u, 0u}, nopre);
+    else
+      mfma_tile<KS, 4, true, true, false, false, NoPre, ShardOffs<KS, true>, 1>(
+          x, nullptr, so, 0, lds, lrowc, loff, MT, rows, lane, g, ob, colb, true, MfmaIO{0x80808080u, 0u}, nopre);
+    t = tn;
+  }
+}
+
 template <int KS, int W, int NH, int WAVES>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void wv_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
@@ -260,7 +301,8 @@ extern "C" {
 const char* wv_name(int v) {
   // (split refills -- each column pass's half reloaded right after it -- ran 0.36 of peak: removed)
   static const char* names[] = {"W4 NH2 2w", "W2 NH1 2w", "W4 NH1 1w (product)", "W4 NH1 2w (spills)",
-                                "32x32 W2 2w", "32x32 W2 1w", "32x32 W1 2w", "32x32 W1 3w"};
+                                "32x32 W2 2w", "32x32 W2 1w", "32x32 W1 2w", "32x32 W1 3w",
+                                "interleaved 256 B blocks W4 1w (timing only)"};
   return v >= 0 && v < (int)(sizeof(names) / sizeof(names[0])) ? names[v] : nullptr;
 }
 
@@ -276,6 +318,15 @@ int wv_launch(int v, const uint32_t* in, uint32_t* out, uint64_t in_obj, uint64_
               uint64_t out_shard, const uint8_t* table, const uint32_t* out_idx, uint64_t ncols, uint32_t nobj,
               uint32_t rows, uint32_t k, hipStream_t s) {
   if (rows > 32 || (ncols & 127)) return (int)hipErrorInvalidValue;
+  if (v == 8) {  // the same buffer as 64-column blocks of every shard (ncols x nobj columns)
+    if (mfma::ksteps(k) != 5 || in_shard != ncols) return (int)hipErrorInvalidValue;
+    const uint32_t total = (uint32_t)(in_obj / in_shard);
+    const uint64_t nblocks = (uint64_t)nobj * ncols / 64;
+    const uint32_t lds = mfma_lds_bytes(mfma::mtiles(rows), 5);
+    hipLaunchKernelGGL((ilv_kernel<5, 1>), dim3(256), dim3(kBlock), lds, s, in, table, out_idx, nblocks, total, rows,
+                       k);
+    return (int)hipGetLastError();
+  }
   if (v >= 4) {  // 32x32x32: k 73..80 (ten K steps of 8 shards), rows 17..24 (three M tiles of 8)
     if (m32::ksteps(k) != 10 || m32::mtiles(rows) != 3) return (int)hipErrorInvalidValue;
 #define W32(W, WV_) \

@@ -60,7 +60,7 @@ def main():
     variants = [int(v) for v in a.variants.split(",")]
 
     def launch(v):
-        table = tables[4 if v >= 4 else 0]
+        table = tables[4 if 4 <= v <= 7 else 0]
         rc = lib.wv_launch(v, buf.data_ptr(), buf.data_ptr(), obj, stride, obj, stride, table.data_ptr(),
                            out_idx.data_ptr(), L, a.nobj, rows, k, sp)
         if rc:
@@ -74,7 +74,7 @@ def main():
         parity.zero_()
         launch(v)
         torch.cuda.synchronize()
-        ok[v] = bool(torch.equal(parity, ref))
+        ok[v] = bool(torch.equal(parity, ref)) if v != 8 else None  # 8: another layout, timing only
     times = {v: [] for v in variants}
     for r in range(a.rounds):
         for v in variants:
