@@ -3,6 +3,7 @@
 // product on v_mfma_i32_16x16x64_i8, for plans whose table carries the digit
 // fragments (built for k >= 17 with rows <= 32, k <= 112: mfma_table.hpp).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <atomic>
 
 #include "kernels.hpp"
@@ -44,10 +45,26 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   const uint32_t mt = mfma::mtiles(a.rows);
   const uint32_t lds = apply::mfma_lds_bytes(mt, KS);
   const uint64_t per_block = 4ull * 16 * 4;  // 4 waves x 16 vectors
+  const uint64_t target = 256ull * apply::mfma_waves(KS, apply::mfma_width(KS));  // resident blocks
+  // Short objects take one walk over every object's tiles across the whole
+  // grid: the per-object walk gives each object a block, most of whose waves
+  // have no tile.  4096 objects of 64 columns: 2-3.4x; of 512 columns at five
+  // K steps (one wave per SIMD) +25% encode, +7% repair, but at four K steps
+  // the per-object walk stays 4% ahead from 8 tiles (profiles/r05/s34_flat/).
+  const uint64_t kFlatTiles = apply::mfma_waves(KS, apply::mfma_width(KS)) == 1 ? 32 : 4;
+  const uint64_t tc = 16ull * apply::mfma_width(KS);
+  const uint64_t tpo = ((a.ncols >> 2) * 4 + tc - 1) / tc;
+  if (a.nobj > 1 && tpo <= kFlatTiles) {
+    const uint64_t tiles = tpo * a.nobj, nb = (tiles + apply::kWaves - 1) / apply::kWaves;
+    const uint64_t gx = std::max<uint64_t>(1, std::min(target, nb));
+    hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, true, true, UNI>), dim3((uint32_t)gx), dim3(apply::kBlock),
+                       lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride, a.out_obj_stride,
+                       a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj, a.rows, a.k, 1u, 1u);
+    return hipGetLastError();
+  }
   const uint32_t nseg = object_segments(a.nobj, a.ncols);
   const uint64_t nwork = (uint64_t)a.nobj * nseg;
   const uint64_t gy = nwork < 65535 ? nwork : 65535;
-  const uint64_t target = 256ull * apply::mfma_waves(KS, apply::mfma_width(KS));  // resident blocks
   uint64_t gx = (target + gy - 1) / gy;
   const uint64_t need = ((a.ncols >> 2) / nseg + per_block - 1) / per_block;
   if (gx > need) gx = need;
@@ -55,7 +72,7 @@ hipError_t launch_ks(const ApplyLaunch& a, hipStream_t stream) {
   hipLaunchKernelGGL((apply::rs_apply_mfma_kernel<KS, true, true, UNI>), dim3((uint32_t)gx, (uint32_t)gy),
                      dim3(apply::kBlock), lds, stream, a.in, a.out, a.in_obj_stride, a.in_shard_stride,
                      a.out_obj_stride, a.out_shard_stride, a.mfma, a.coeff, a.in_idx, a.out_idx, a.ncols, a.nobj,
-                     a.rows, a.k, nseg);
+                     a.rows, a.k, nseg, 0u);
   return hipGetLastError();
 }
 

@@ -332,6 +332,43 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
   }
 }
 
+// The tile walk over short objects: tiles of every object numbered object by
+// object (tpo a object, the last partial as in mfma_walk), walked by every
+// wave of the grid (wave, wave + nwaves, ...), the refill streaming the next
+// tile in across object boundaries.  Objects of a few tiles otherwise leave
+// most of a block's waves idle (one work item per block) and restart the
+// refill per object.
+template <int KS, int W, bool NTL, bool NTS, class SO>
+__device__ __forceinline__ void mfma_flat_walk(const char* __restrict__ in, char* __restrict__ out,
+                                               uint64_t in_obj_bytes, uint64_t out_obj_bytes, const SO& so,
+                                               const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
+                                               const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows,
+                                               uint32_t lane, uint32_t g, uint32_t n, uint32_t c1, uint32_t tpo,
+                                               uint64_t ntiles, uint64_t wave, uint64_t nwaves, MfmaIO io) {
+  constexpr uint32_t TC = 16 * W;
+  NoPre pre;
+  auto col_of = [&](uint64_t f) { return (uint32_t)(f % tpo) * TC + n * W; };
+  auto colb_of = [&](uint64_t f) {
+    const uint32_t c = col_of(f);
+    return (c < c1 ? c : c1 - W) << 2;
+  };
+  auto in_of = [&](uint64_t f) { return in + (f / tpo) * in_obj_bytes; };
+  vec_t<W> x[KS][4];
+  uint64_t t = wave;
+  if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, in_of(t), so, colb_of(t));
+  while (t < ntiles) {
+    const uint64_t tn = t + nwaves;
+    char* const ob = out + (t / tpo) * out_obj_bytes;
+    if (tn < ntiles)
+      mfma_tile<KS, W, NTL, NTS, true, false, NoPre, SO>(x, in_of(tn), so, colb_of(tn), lfrag, lrowc, loff, MT, rows,
+                                                         lane, g, ob, colb_of(t), col_of(t) < c1, io, pre);
+    else
+      mfma_tile<KS, W, NTL, NTS, false, false, NoPre, SO>(x, nullptr, so, 0, lfrag, lrowc, loff, MT, rows, lane, g,
+                                                          ob, colb_of(t), col_of(t) < c1, io, pre);
+    t = tn;
+  }
+}
+
 // Block prologue: the plan's A fragments and row constants into LDS, the
 // output rows' byte offsets (out_idx[i] * out_unit), and each lane's input
 // byte offsets (in_idx[j] * in_unit, in_idx null: j; shards past k read shard in_idx[k-1],
@@ -365,7 +402,7 @@ rs_apply_mfma_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
-    uint32_t rows, uint32_t k, uint32_t nseg) {
+    uint32_t rows, uint32_t k, uint32_t nseg, uint32_t flat) {
   constexpr int W = mfma_width(KS);
   extern __shared__ i32x4 lds[];
   const uint32_t MT = (rows + 3) / 4;
@@ -382,6 +419,21 @@ rs_apply_mfma_kernel(
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * kWaves;
   NoPre nopre;
+  if (flat) {  // short objects (a 1D grid, nseg 1): one walk over every object's tiles, then the column tails
+    constexpr uint32_t TC = 16 * W;
+    const uint32_t c1 = 4 * nvec, tpo = (c1 + TC - 1) / TC;
+    if (tpo)
+      mfma_flat_walk<KS, W, NTL, NTS>(reinterpret_cast<const char*>(in), reinterpret_cast<char*>(out),
+                                      in_obj_stride * 4, out_obj_stride * 4, so, lds, lrowc, loff, MT, rows, lane, g,
+                                      n, c1, tpo, (uint64_t)nobj * tpo, wave, nwaves, MfmaIO{0x80808080u, 0u});
+    const uint32_t tailc = (uint32_t)(ncols - c1);
+    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * tailc; i += nthr) {
+      const uint64_t obj = i / tailc;
+      apply_column<0>(in + obj * in_obj_stride, out + obj * out_obj_stride, coeff, in_idx, in_shard, out_idx,
+                      out_shard, rows, k, c1 + i % tailc);
+    }
+    return;
+  }
   for (uint64_t wi = blockIdx.y; wi < nwork; wi += gridDim.y) {
     const uint64_t obj = wi / nseg;
     const uint32_t seg = (uint32_t)(wi % nseg);

@@ -81,6 +81,38 @@ def test_encode_vs_oracle(torch_dev, matrix_cores, need, total, L):
         assert np.array_equal(got[o], ref), (o, need, total, L)
 
 
+@pytest.mark.parametrize("need,total,L,nobj", [(80, 100, 200, 300), (40, 56, 64, 500), (64, 80, 1500, 40),
+                                               (33, 50, 7, 200), (72, 90, 3, 64), (96, 100, 2047, 9)])
+def test_many_short_objects_vs_oracle(torch_dev, need, total, L, nobj):
+    """Batches of many short objects (at most 32 tiles each: the matrix-core
+    kernel's flat walk over every object's tiles, rs_apply_mfma_kernel): encode
+    in place, then rebuild a data-and-parity erasure set into a separate
+    buffer; every object against the oracle."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(need * 7 + L + nobj)
+    h = _rand(rng, (nobj, total, L))
+    buf = torch.from_numpy(h.reshape(-1).view(np.int32).copy()).cuda()
+    lay = D.layout_of(total, L)
+    D.Plan.encode(need, total)(buf, lay, buf, lay, L, nobj, dst_offset=need * L)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().view(np.uint32).reshape(nobj, total, L)
+    for o in range(nobj):
+        ref = np.ascontiguousarray(h[o].copy())
+        OC.encode_object(ref, need, total)
+        assert np.array_equal(got[o], ref), (o, need, total, L)
+    erase = sorted({0, need - 1, need, total - 1})
+    have = [i for i in range(total) if i not in erase][:need]
+    e = len(erase)
+    out = torch.zeros(nobj * e * L, dtype=torch.int32, device="cuda")
+    D.Plan.reconstruct(need, total, have, erase)(buf, lay, out, D.layout_of(e, L), L, nobj)
+    torch.cuda.synchronize()
+    rec = out.cpu().numpy().view(np.uint32).reshape(nobj, e, L)
+    for o in range(nobj):
+        for i, t in enumerate(erase):  # rebuilt as canonical residues (the data holds words >= p)
+            assert np.array_equal(rec[o, i], got[o, t] % P), (o, t)
+
+
 @pytest.mark.parametrize("need,total,nerase", [(64, 80, 16), (40, 56, 5), (50, 82, 32), (96, 100, 4), (33, 50, 17),
                                                (72, 90, 18), (80, 100, 20), (90, 100, 10), (100, 116, 16)])
 def test_reconstruct_shuffled_survivors_separate_dst(torch_dev, matrix_cores, need, total, nerase):

@@ -117,6 +117,15 @@ for step in "$@"; do
             run wilv_80_100_$rep 300 python tools/wide_variants.py --need 80 --total 100 --variants 0,2,8 &&
             run wilv_72_90_$rep 300 python tools/wide_variants.py --need 72 --total 90 --variants 0,2,8 || exit 1
           done ;;
+    # many short objects at wide codes (the flat walk), this tree vs ab/*, alternating
+    wshort) cp slime_amd/lib/libslime_rs.so /tmp/ab_new.so
+            for rep in 1 2; do
+              for v in new $(ls ab); do
+                if [ "$v" = new ]; then cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so; else cp ab/$v/libslime_rs.so slime_amd/lib/libslime_rs.so; fi
+                run wshort_${v}_$rep 300 python tools/short_objects.py --shapes 80/100,40/56,64/80 --L 64,512,2048 --nobj 4096 || exit 1
+              done
+            done
+            cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
     wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
              run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
                python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;
