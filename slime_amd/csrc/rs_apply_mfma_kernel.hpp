@@ -338,13 +338,15 @@ __device__ __forceinline__ void mfma_walk(const char* __restrict__ ib, char* __r
 // tile in across object boundaries.  Objects of a few tiles otherwise leave
 // most of a block's waves idle (one work item per block) and restart the
 // refill per object.
-template <int KS, int W, bool NTL, bool NTS, class SO>
+// io_of(obj): the object's word mapping (MfmaIO; the byte path's BSWAP
+// chunks carry one mapping an object).
+template <int KS, int W, bool NTL, bool NTS, bool BSWAP, class SO, class IOF>
 __device__ __forceinline__ void mfma_flat_walk(const char* __restrict__ in, char* __restrict__ out,
                                                uint64_t in_obj_bytes, uint64_t out_obj_bytes, const SO& so,
                                                const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
                                                const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows,
                                                uint32_t lane, uint32_t g, uint32_t n, uint32_t c1, uint32_t tpo,
-                                               uint64_t ntiles, uint64_t wave, uint64_t nwaves, MfmaIO io) {
+                                               uint64_t ntiles, uint64_t wave, uint64_t nwaves, IOF io_of) {
   constexpr uint32_t TC = 16 * W;
   NoPre pre;
   auto col_of = [&](uint64_t f) { return (uint32_t)(f % tpo) * TC + n * W; };
@@ -358,12 +360,14 @@ __device__ __forceinline__ void mfma_flat_walk(const char* __restrict__ in, char
   if (t < ntiles) mfma_load_tile<KS, W, NTL>(x, in_of(t), so, colb_of(t));
   while (t < ntiles) {
     const uint64_t tn = t + nwaves;
-    char* const ob = out + (t / tpo) * out_obj_bytes;
+    const uint64_t obj = t / tpo;
+    char* const ob = out + obj * out_obj_bytes;
+    const MfmaIO io = io_of(obj);
     if (tn < ntiles)
-      mfma_tile<KS, W, NTL, NTS, true, false, NoPre, SO>(x, in_of(tn), so, colb_of(tn), lfrag, lrowc, loff, MT, rows,
+      mfma_tile<KS, W, NTL, NTS, true, BSWAP, NoPre, SO>(x, in_of(tn), so, colb_of(tn), lfrag, lrowc, loff, MT, rows,
                                                          lane, g, ob, colb_of(t), col_of(t) < c1, io, pre);
     else
-      mfma_tile<KS, W, NTL, NTS, false, false, NoPre, SO>(x, nullptr, so, 0, lfrag, lrowc, loff, MT, rows, lane, g,
+      mfma_tile<KS, W, NTL, NTS, false, BSWAP, NoPre, SO>(x, nullptr, so, 0, lfrag, lrowc, loff, MT, rows, lane, g,
                                                           ob, colb_of(t), col_of(t) < c1, io, pre);
     t = tn;
   }
@@ -423,9 +427,10 @@ rs_apply_mfma_kernel(
     constexpr uint32_t TC = 16 * W;
     const uint32_t c1 = 4 * nvec, tpo = (c1 + TC - 1) / TC;
     if (tpo)
-      mfma_flat_walk<KS, W, NTL, NTS>(reinterpret_cast<const char*>(in), reinterpret_cast<char*>(out),
-                                      in_obj_stride * 4, out_obj_stride * 4, so, lds, lrowc, loff, MT, rows, lane, g,
-                                      n, c1, tpo, (uint64_t)nobj * tpo, wave, nwaves, MfmaIO{0x80808080u, 0u});
+      mfma_flat_walk<KS, W, NTL, NTS, false>(reinterpret_cast<const char*>(in), reinterpret_cast<char*>(out),
+                                             in_obj_stride * 4, out_obj_stride * 4, so, lds, lrowc, loff, MT, rows,
+                                             lane, g, n, c1, tpo, (uint64_t)nobj * tpo, wave, nwaves,
+                                             [](uint64_t) { return MfmaIO{0x80808080u, 0u}; });
     const uint32_t tailc = (uint32_t)(ncols - c1);
     for (uint64_t i = tid; tailc && i < (uint64_t)nobj * tailc; i += nthr) {
       const uint64_t obj = i / tailc;

@@ -557,7 +557,8 @@ __attribute__((amdgpu_waves_per_eu(apply::mfma_waves(KS, apply::mfma_width(KS)))
 decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0,
                          uint64_t ncols, uint32_t nobj, uint32_t rows, uint32_t k, const uint8_t* __restrict__ table,
                          const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ in_idx,
-                         const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg) {
+                         const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping, uint32_t nseg,
+                         uint32_t flat) {
   constexpr int W = apply::mfma_width(KS);
   extern __shared__ i32x4 lds[];
   const uint32_t MT = (rows + 3) / 4;
@@ -572,6 +573,35 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   const uint64_t nvec = ncols >> 2;
   (void)L;
   apply::NoPre pre;
+  auto tail_column = [&](uint8_t* slot, uint32_t m, uint64_t b) {
+    for (uint32_t i = 0; i < rows; ++i) {
+      const uint32_t* crow = coeff + (uint64_t)i * cs;
+      uint64_t lo = 0;
+      uint32_t hi = 0;
+      for (uint32_t j = 0; j < k; ++j)
+        mac(lo, hi, be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m, crow[j]);
+      *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
+    }
+  };
+  if (flat) {  // short chunks (a 1D grid, nseg 1): one walk over every object's tiles, then the column tails
+    constexpr uint32_t TC = 16 * W;
+    const uint32_t c1 = 4 * (uint32_t)nvec, tpo = (c1 + TC - 1) / TC;
+    uint8_t* const base = slots + 4 * col0;
+    if (tpo)
+      apply::mfma_flat_walk<KS, W, true, true, true>(
+          reinterpret_cast<const char*>(base), reinterpret_cast<char*>(base), slot_stride, slot_stride, so, lds, lrowc,
+          loff, MT, rows, lane, lg, ln, c1, tpo, (uint64_t)nobj * tpo, wave, nwaves, [&](uint64_t o) {
+            const uint32_t m = mapping[o];
+            return MfmaIO{0x80808080u ^ be(m), m};
+          });
+    const uint32_t tailc = (uint32_t)(ncols - c1);
+    const uint64_t tid = (uint64_t)wave * 64 + lane, nthr = (uint64_t)nwaves * 64;
+    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * tailc; i += nthr) {
+      const uint64_t o = i / tailc;
+      tail_column(base + o * slot_stride, mapping[o], c1 + i % tailc);
+    }
+    return;
+  }
   for (uint64_t wi = blockIdx.y; wi < (uint64_t)nobj * nseg; wi += gridDim.y) {
     const Segment sg = segment_of(wi, nseg, nvec);
     const uint32_t m = mapping[sg.obj];
@@ -581,16 +611,8 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                                                 lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * (uint32_t)sg.v0,
                                                 4 * (uint32_t)sg.v1, wave, nwaves, MfmaIO{0x80808080u ^ be(m), m}, pre);
     // Columns past the last whole vector of the window, one per lane.
-    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64) {
-      for (uint32_t i = 0; i < rows; ++i) {
-        const uint32_t* crow = coeff + (uint64_t)i * cs;
-        uint64_t lo = 0;
-        uint32_t hi = 0;
-        for (uint32_t j = 0; j < k; ++j)
-          mac(lo, hi, be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m, crow[j]);
-        *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
-      }
-    }
+    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64)
+      tail_column(slot, m, b);
   }
 }
 
@@ -667,11 +689,23 @@ hipError_t dec_ks(const BytesLaunch& a, hipStream_t s) {
   const uint64_t ncols = a.ncols ? a.ncols : a.L;
   const uint32_t lds = apply::mfma_lds_bytes(mfma::mtiles(a.rows), KS);
   const uint64_t blocks = 256ull * apply::mfma_waves(KS, apply::mfma_width(KS));
+  // Batches of short chunks: the flat walk (the apply path's rule, rs_apply_mfma.hip).
+  const uint64_t flat_tiles = apply::mfma_waves(KS, apply::mfma_width(KS)) == 1 ? 32 : 4;
+  const uint64_t tc = 16ull * apply::mfma_width(KS);
+  const uint64_t tpo = ((ncols >> 2) * 4 + tc - 1) / tc;
+  if (a.nobj > 1 && tpo <= flat_tiles) {
+    const uint64_t nb = (tpo * a.nobj + apply::kWaves - 1) / apply::kWaves;
+    const uint64_t gx = nb < 1 ? 1 : nb < blocks ? nb : blocks;
+    hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS>), dim3((uint32_t)gx), dim3(kBlock), lds, s, a.slots,
+                       a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.mfma, a.coeff,
+                       a.in_idx, a.out_idx, a.mapping, 1u, 1u);
+    return hipGetLastError();
+  }
   const uint32_t nseg = object_segments(a.nobj, ncols);
   hipLaunchKernelGGL((bytes::decode_bytes_mfma_kernel<KS>),
                      bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
                      a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.nobj, a.rows, a.k, a.mfma, a.coeff,
-                     a.in_idx, a.out_idx, a.mapping, nseg);
+                     a.in_idx, a.out_idx, a.mapping, nseg, 0u);
   return hipGetLastError();
 }
 

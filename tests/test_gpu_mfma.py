@@ -293,6 +293,45 @@ def test_bytes_decode_objects_repairs_chunks(torch_dev, matrix_cores, need, tota
         assert torch.equal(slots, truth), erase
 
 
+@pytest.mark.parametrize("need,total,S,nobj", [(80, 100, 65536, 120), (40, 56, 3001, 300), (33, 50, 777, 200),
+                                               (96, 100, 20001, 64), (64, 80, 131075, 40), (72, 90, 9, 50)])
+def test_bytes_many_short_objects_round_trip(torch_dev, matrix_cores, need, total, S, nobj):
+    """Batches of short objects (a few tiles a chunk) take the flat walk in
+    the matrix-core byte decode (rs_bytes_mfma.hip dec_ks): encode, pin a
+    sample of objects to the oracle's framing (multi_store.go:526-557), erase
+    and rebuild every object's chunks byte for byte."""
+    torch = torch_dev
+    from slime_amd import device as D
+    from test_gpu_parity import _make_slots, _oracle_chunks
+    rng = np.random.default_rng(S * 7 + nobj)
+    objs = _byte_objects(rng, S, nobj)
+    slots, L, chunk, stride = _make_slots(torch, objs, need, total)
+    plan = D.Plan.encode(need, total)
+    mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+    D.encode_objects(plan, slots, stride, S, nobj, mapping, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    h = slots.cpu().numpy()
+    ms = mapping.cpu().numpy().view(np.uint32)
+    for o in sorted({0, 1, 2, nobj // 2, nobj - 1}):
+        m, want = _oracle_chunks(objs[o], need, total)
+        assert ms[o] == m, o
+        for c in range(total):
+            assert h[o * stride + c * chunk: o * stride + c * chunk + 4 * L].tobytes() == want[c], (o, c)
+    truth = slots.clone()
+    r = total - need
+    for erase in (list(range(min(r, 16))), sorted(rng.choice(total, size=min(r, 20), replace=False).tolist())):
+        have = [i for i in range(total) if i not in erase]
+        rng.shuffle(have)
+        rec = D.Plan.reconstruct(need, total, have[:need], erase).set_outputs(erase)
+        v = slots.view(nobj, stride)[:, : total * chunk].view(nobj, total, chunk)
+        v[:, erase, : 4 * L] = 0x5A
+        D.decode_objects(rec, slots, stride, L, nobj, mapping)
+        torch.cuda.synchronize()
+        assert torch.equal(slots, truth), erase
+
+
 def test_objects_over_4gib_take_the_valu_kernels(torch_dev):
     """The matrix-core kernel addresses an object with 32-bit byte offsets; a
     layout whose object spans 4 GiB or more (here 40 shards 128 MiB + 256 B

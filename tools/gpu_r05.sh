@@ -126,6 +126,23 @@ for step in "$@"; do
               done
             done
             cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
+    wshortb) cp slime_amd/lib/libslime_rs.so /tmp/ab_new.so
+            for rep in 1 2; do
+              for v in new $(ls ab); do
+                if [ "$v" = new ]; then cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so; else cp ab/$v/libslime_rs.so slime_amd/lib/libslime_rs.so; fi
+                run wshortb_${v}_$rep 300 python tools/short_objects.py --shapes 80/100,40/56,64/80 --bytes 16384,65536,262144 --nobj 1024 || exit 1
+              done
+            done
+            cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
+    wilvapi) for rep in 1 2; do
+               run wilvapi_contig_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 4194304 --nobj 1 &&
+               run wilvapi_blocks_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 64 --nobj 65536 || exit 1
+             done ;;
+    profshort) for cfg in "80/100 16384" "80/100 262144" "40/56 16384"; do
+                 read -r shp sz <<< "$cfg"; tag=$(echo "${shp}_$sz" | tr / _)
+                 run profshort_$tag 300 rocprofv3 --kernel-trace --stats -d "$OUT/profshort_$tag" -o short --output-format csv -- \
+                   python3 tools/short_objects.py --shapes $shp --bytes $sz --nobj 1024 --rounds 3 || exit 1
+               done ;;
     wprof80) E20=0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19
              run wprof80 300 rocprofv3 --kernel-trace --stats -d "$OUT/wprof80" -o bench --output-format csv -- \
                python3 bench.py --need 80 --total 100 --objects 32 --erase $E20 --steps 3 --warmup 1 $NOLEGS ;;
