@@ -431,11 +431,12 @@ rs_apply_mfma_kernel(
                                              in_obj_stride * 4, out_obj_stride * 4, so, lds, lrowc, loff, MT, rows,
                                              lane, g, n, c1, tpo, (uint64_t)nobj * tpo, wave, nwaves,
                                              [](uint64_t) { return MfmaIO{0x80808080u, 0u}; });
+    // Tails as (object, row, column) cells, one per lane.
     const uint32_t tailc = (uint32_t)(ncols - c1);
-    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * tailc; i += nthr) {
-      const uint64_t obj = i / tailc;
-      apply_column<0>(in + obj * in_obj_stride, out + obj * out_obj_stride, coeff, in_idx, in_shard, out_idx,
-                      out_shard, rows, k, c1 + i % tailc);
+    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * rows * tailc; i += nthr) {
+      const uint64_t or_ = i / tailc, obj = or_ / rows;
+      apply_cell(in + obj * in_obj_stride, out + obj * out_obj_stride, coeff, in_idx, in_shard, out_idx, out_shard, k,
+                 (uint32_t)(or_ % rows), c1 + i % tailc);
     }
     return;
   }
@@ -449,10 +450,11 @@ rs_apply_mfma_kernel(
     if (v1 > v0)
       mfma_walk<KS, W, NTL, NTS, false>(ib, ob, so, lds, lrowc, loff, MT, rows, lane, g, n, 4 * v0, 4 * v1, wave,
                                         nwaves, MfmaIO{0x80808080u, 0u}, nopre);
+    const uint32_t tailc = (uint32_t)(ncols - 4 * (uint64_t)nvec);  // (row, column) cells, one per lane
     if (seg == nseg - 1)
-      for (uint64_t b = ((uint64_t)nvec << 2) + tid; b < ncols; b += nthr)
-        apply_column<0>(reinterpret_cast<const uint32_t*>(ib), reinterpret_cast<uint32_t*>(ob), coeff, in_idx,
-                        in_shard, out_idx, out_shard, rows, k, b);
+      for (uint64_t i = tid; tailc && i < (uint64_t)rows * tailc; i += nthr)
+        apply_cell(reinterpret_cast<const uint32_t*>(ib), reinterpret_cast<uint32_t*>(ob), coeff, in_idx, in_shard,
+                   out_idx, out_shard, k, (uint32_t)(i / tailc), 4 * (uint64_t)nvec + i % tailc);
   }
 }
 

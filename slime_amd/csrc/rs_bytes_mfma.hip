@@ -159,16 +159,19 @@ __device__ __forceinline__ EdgeSpan edge_span(uint64_t S, uint64_t L, uint64_t c
   return s;
 }
 
-// Edge columns [b0, ncols) of every object `take` selects, as (object, row,
-// column) items spread over the whole grid, one per lane (consecutive lanes,
-// consecutive columns of one chunk): sum_j coeff[r][j] x_j over the data
-// chunks' symbols (splitVector padding, the partial last word), stored with
-// MapFromGF's mapping; row 0's items also write the data-chunk tails and (F)
-// fold MapToGF's flags into flags[obj].  Replaces a single wave's serial VALU
-// edge step per object (80 data chunks x 20 rows per column: ~0.1-0.2 ms of
-// tail on the 80/100 encode and its redo).  Rows of one column may read a
-// tail word before or after row 0 rewrote it: the rewrite is its packed
-// value (padding words read as zero either way), so every read agrees.
+// Edge columns [b0, ncols) of every object `take` selects, spread over the
+// whole grid: a wave takes 64 consecutive columns of one object and eight of
+// its rows (object and rows uniform, so the coefficients are scalar loads),
+// a lane one column: the k data chunks' symbols (splitVector padding, the
+// partial last word) loaded sixteen at a time, summed into the eight rows,
+// stored with MapFromGF's mapping; the first row block also writes the
+// data-chunk tails and (F) folds MapToGF's flags into flags[obj].  Replaces a
+// single wave's serial VALU edge step per object, and then one lane per (row,
+// column) that loaded and unpacked every symbol once per row: batches of short
+// objects are mostly edge (80/100 at 16 KiB: all 52 columns), and that ran
+// 345 us for 16 MiB of objects.  Row blocks of one column may read a tail word
+// before or after the first rewrote it: the rewrite is its packed value
+// (padding words read as zero either way), so every read agrees.
 template <bool F, class Take>
 __device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L,
                                              uint64_t chunk, uint64_t col0, uint64_t ncols, const ObjWords& ow,
@@ -176,24 +179,28 @@ __device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64
                                              const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                              uint64_t b0, uint32_t* __restrict__ flags, Take take) {
   if (b0 >= ncols) return;
-  const uint64_t nc = ncols - b0, per = (uint64_t)rows * nc, total = per * nobj;
-  const uint64_t gw = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  constexpr uint32_t RB = 8;
+  const uint64_t ncb = (ncols - b0 + 63) / 64, nrb = (rows + RB - 1) / RB;
+  const uint64_t per = nrb * ncb, total = per * nobj;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t gw = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWaves +
+                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t gn = (uint64_t)gridDim.x * gridDim.y * kWaves;
-  for (uint64_t it = gw * 64 + (threadIdx.x & 63); it < total; it += gn * 64) {
-    const uint32_t o = (uint32_t)(it / per);
-    const uint64_t rem = it % per;
-    const uint32_t r = (uint32_t)(rem / nc);
-    const uint64_t b = b0 + rem % nc;
+  for (uint64_t u = gw; u < total; u += gn) {
+    const uint32_t o = (uint32_t)(u / per);
+    const uint64_t rem = u % per;
+    const uint32_t r0 = (uint32_t)(rem / ncb) * RB;
+    const uint64_t bl = b0 + (rem % ncb) * 64 + lane;
+    const bool act = bl < ncols;
+    const uint64_t b = act ? bl : ncols - 1;  // idle lanes re-read the last column, store nothing
     uint32_t m;
     if (!take(o, m)) continue;
     uint8_t* const slot = slots + (uint64_t)o * slot_stride + 4 * col0;
-    const uint32_t* const crow = coeff + (uint64_t)r * cs;
-    // Sixteen chunks at a time: their loads first (one memory latency per
-    // sixteen, not per chunk), then row 0's tail writes, then the sums.  Every
-    // row of a column folds the same flags.
     Flags fl;
-    uint64_t lo = 0;
-    uint32_t hi = 0;
+    uint64_t lo[RB];
+    uint32_t hi[RB];
+#pragma unroll
+    for (uint32_t rr = 0; rr < RB; ++rr) lo[rr] = 0, hi[rr] = 0;
     for (uint32_t j0 = 0; j0 < k; j0 += 16) {
       uint32_t x[16][4];
 #pragma unroll
@@ -201,17 +208,27 @@ __device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64
         x[j][0] = 0;
         if (j0 + j < k) load_data_symbol<false, F>(slot, chunk, L, col0, j0 + j, b, 1, ow, m, x[j], &fl);
       }
-      if (r == 0)
+      if (r0 == 0 && act)
 #pragma unroll
         for (int j = 0; j < 16; ++j)
           if (j0 + j < k) fix_data_tail_one(slot, chunk, L, col0, j0 + j, b, 1, ow, m, x[j]);
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j0 + j < k) mac(lo, hi, x[j][0], crow[j0 + j]);
+      for (uint32_t rr = 0; rr < RB; ++rr) {
+        if (r0 + rr >= rows) break;
+        const uint32_t* const crow = coeff + (uint64_t)(r0 + rr) * cs + j0;  // cs: rows padded to 16
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mac(lo[rr], hi[rr], x[j][0], crow[j]);
+      }
     }
-    *reinterpret_cast<uint32_t*>(slot + ((uint64_t)k + out_idx[r]) * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
+    if (act)
+#pragma unroll
+      for (uint32_t rr = 0; rr < RB; ++rr) {
+        if (r0 + rr >= rows) break;
+        *reinterpret_cast<uint32_t*>(slot + ((uint64_t)k + out_idx[r0 + rr]) * chunk + 4 * b) =
+            be(fold96(lo[rr], hi[rr]) ^ m);
+      }
     if constexpr (F) {
-      const uint32_t bits = fl.bits();
+      const uint32_t bits = r0 == 0 ? fl.bits() : 0u;
       if (bits) atomicOr(&flags[o], bits);
     }
   }
@@ -573,15 +590,12 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
   const uint64_t nvec = ncols >> 2;
   (void)L;
   apply::NoPre pre;
-  auto tail_column = [&](uint8_t* slot, uint32_t m, uint64_t b) {
-    for (uint32_t i = 0; i < rows; ++i) {
-      const uint32_t* crow = coeff + (uint64_t)i * cs;
-      uint64_t lo = 0;
-      uint32_t hi = 0;
-      for (uint32_t j = 0; j < k; ++j)
-        mac(lo, hi, be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m, crow[j]);
-      *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(fold96(lo, hi) ^ m);
-    }
+  // Row i of tail column b (columns past the last whole vector), one per lane.
+  auto tail_cell = [&](uint8_t* slot, uint32_t m, uint32_t i, uint64_t b) {
+    const uint32_t v = apply::wide_dot(coeff + (uint64_t)i * cs, k, [&](uint32_t j) {
+      return be(*reinterpret_cast<const uint32_t*>(slot + (uint64_t)in_idx[j] * chunk + 4 * b)) ^ m;
+    });
+    *reinterpret_cast<uint32_t*>(slot + (uint64_t)out_idx[i] * chunk + 4 * b) = be(v ^ m);
   };
   if (flat) {  // short chunks (a 1D grid, nseg 1): one walk over every object's tiles, then the column tails
     constexpr uint32_t TC = 16 * W;
@@ -596,9 +610,9 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
           });
     const uint32_t tailc = (uint32_t)(ncols - c1);
     const uint64_t tid = (uint64_t)wave * 64 + lane, nthr = (uint64_t)nwaves * 64;
-    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * tailc; i += nthr) {
-      const uint64_t o = i / tailc;
-      tail_column(base + o * slot_stride, mapping[o], c1 + i % tailc);
+    for (uint64_t i = tid; tailc && i < (uint64_t)nobj * rows * tailc; i += nthr) {
+      const uint64_t or_ = i / tailc, o = or_ / rows;
+      tail_cell(base + o * slot_stride, mapping[o], (uint32_t)(or_ % rows), c1 + i % tailc);
     }
     return;
   }
@@ -610,9 +624,10 @@ decode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
       apply::mfma_walk<KS, W, true, true, true>(reinterpret_cast<const char*>(slot), reinterpret_cast<char*>(slot), so,
                                                 lds, lrowc, loff, MT, rows, lane, lg, ln, 4 * (uint32_t)sg.v0,
                                                 4 * (uint32_t)sg.v1, wave, nwaves, MfmaIO{0x80808080u ^ be(m), m}, pre);
-    // Columns past the last whole vector of the window, one per lane.
-    for (uint64_t b = (nvec << 2) + (uint64_t)wave * 64 + lane; sg.last && b < ncols; b += (uint64_t)nwaves * 64)
-      tail_column(slot, m, b);
+    const uint32_t tailc = (uint32_t)(ncols - (nvec << 2));
+    for (uint64_t i = (uint64_t)wave * 64 + lane; sg.last && tailc && i < (uint64_t)rows * tailc;
+         i += (uint64_t)nwaves * 64)
+      tail_cell(slot, m, (uint32_t)(i / tailc), (nvec << 2) + i % tailc);
   }
 }
 

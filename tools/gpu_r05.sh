@@ -134,6 +134,14 @@ for step in "$@"; do
               done
             done
             cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
+    wshortt) cp slime_amd/lib/libslime_rs.so /tmp/ab_new.so
+            for rep in 1 2; do
+              for v in new $(ls ab); do
+                if [ "$v" = new ]; then cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so; else cp ab/$v/libslime_rs.so slime_amd/lib/libslime_rs.so; fi
+                run wshortt_${v}_$rep 300 python tools/short_objects.py --shapes 80/100,40/56 --L 67,515,2051 --nobj 4096 || exit 1
+              done
+            done
+            cp /tmp/ab_new.so slime_amd/lib/libslime_rs.so ;;
     wilvapi) for rep in 1 2; do
                run wilvapi_contig_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 4194304 --nobj 1 &&
                run wilvapi_blocks_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 64 --nobj 65536 || exit 1
