@@ -120,6 +120,54 @@ __device__ __forceinline__ void mfma_switch_walk(const char* __restrict__ ib, ch
   }
 }
 
+// Phase 0 over short objects (one segment each, nint interior tiles an
+// object): one walk over every object's interior tiles across the grid, the
+// refill crossing objects (as apply::mfma_flat_walk), each tile encoded with
+// its object's mapping as phase 0 has found it so far when `record` (the
+// mid-object switch: one record byte per tile, as mfma_switch_walk) or with 0,
+// and its flag bits published after the tile.  A block per object left most
+// of its waves idle and restarted the refill per object.
+template <int KS, int W, int NH, class SO>
+__device__ __forceinline__ void mfma_flat_phase0(uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t col0,
+                                                 uint64_t chunk, uint32_t k, const SO& so,
+                                                 const i32x4* __restrict__ lfrag, const uint64_t* __restrict__ lrowc,
+                                                 const uint32_t* __restrict__ loff, uint32_t MT, uint32_t rows,
+                                                 uint32_t lane, uint32_t g, uint32_t n, uint32_t nint, uint64_t ntiles,
+                                                 uint32_t wave, uint32_t nwaves, uint32_t* __restrict__ flags,
+                                                 uint8_t* __restrict__ record, uint32_t units) {
+  constexpr uint32_t TC = 16 * W;
+  auto colb_of = [&](uint64_t f) { return (uint32_t)(((f % nint) * TC + n * W) << 2); };
+  auto base_of = [&](uint64_t o) { return slots + o * slot_stride + 4 * col0; };
+  uint64_t t = wave;
+  if (t >= ntiles) return;
+  apply::vec_t<W> x[KS][4];
+  apply::mfma_load_tile<KS, W, true>(x, reinterpret_cast<const char*>(base_of(t / nint)), so, colb_of(t));
+  uint32_t f = record ? flags_now(flags + t / nint) : 0u;
+  while (t < ntiles) {
+    const uint64_t tn = t + nwaves;
+    const uint64_t obj = t / nint;
+    const uint32_t m = (__builtin_amdgcn_readlane(f, 0) & 1u) ? 0x80000000u : 0u;
+    if (record) {
+      if (lane == 0) record[obj * units + t % nint] = m ? 1 : 0;
+      if (tn < ntiles) f = flags_now(flags + tn / nint);  // tile tn's mapping, in flight during tile t
+    }
+    const MfmaIO io{0x80808080u ^ be(m), m};
+    char* const ob = reinterpret_cast<char*>(base_of(obj) + (uint64_t)k * chunk);
+    FlagPre pre;
+    if (tn < ntiles)
+      apply::mfma_tile<KS, W, true, true, true, true, FlagPre, SO, NH>(
+          x, reinterpret_cast<const char*>(base_of(tn / nint)), so, colb_of(tn), lfrag, lrowc, loff, MT, rows, lane, g,
+          ob, colb_of(t), true, io, pre);
+    else
+      apply::mfma_tile<KS, W, true, true, false, true, FlagPre, SO, NH>(x, nullptr, so, 0, lfrag, lrowc, loff, MT, rows,
+                                                                        lane, g, ob, colb_of(t), true, io, pre);
+    const uint32_t fb = pre.bits();
+    const uint32_t wf = (__ballot(fb & 1u) ? 1u : 0u) | (__ballot(fb & 2u) ? 2u : 0u);
+    if (wf && lane == 0) atomicOr(flags + obj, wf);
+    t = tn;
+  }
+}
+
 // The edge steps of one segment (vectors [e0, u1)), one vector per lane: the
 // windows whose edges spread_edges does not take, and the whole-object
 // re-encode.
@@ -253,7 +301,7 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                          const uint8_t* __restrict__ table, const uint32_t* __restrict__ coeff,
                          const uint32_t* __restrict__ out_idx, uint32_t* __restrict__ flags,
                          const uint32_t* __restrict__ mapping, uint32_t nseg, uint8_t* __restrict__ record,
-                         uint32_t units) {
+                         uint32_t units, uint32_t flat0) {
   constexpr int W = enc_width(KS);
   constexpr int NH = apply::mfma_halves_at(KS, W, enc_waves<KS, MODE>());
   constexpr uint32_t TCV = 4 * W;  // tile width in 16-byte vectors
@@ -283,6 +331,15 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
                            return true;
                          });
       edges_done = true;
+    }
+    if (flat0) {  // short objects (a 1D grid, nseg 1, edges spread): the flat interior walk, then done
+      uint64_t end_max = interior_vectors(S, L, col0, k);
+      if (end_max > nvec) end_max = nvec;
+      const uint32_t nint = (uint32_t)(end_max / TCV);
+      if (nint)
+        mfma_flat_phase0<KS, W, NH>(slots, slot_stride, col0, chunk, k, so, lds, lrowc, loff, MT, rows, lane, lg, ln,
+                                    nint, (uint64_t)nobj * nint, wave, nwaves, flags, record, units);
+      return;
     }
   }
   // Re-encode of up to 64 objects (one segment each): one flat tile walk over
@@ -665,10 +722,15 @@ hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
       record = l.record(a.scratch, a.nobj);
       if (hipError_t e = hipMemsetAsync(record, 2, (uint64_t)a.nobj * units, s)) return e;
     }
-    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0>),
-                       bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1), dim3(kBlock), lds, s, a.slots,
-                       a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma, a.coeff,
-                       a.out_idx, a.flags, a.mapping, nseg, record, units);
+    // Batches of short objects (one segment, at most four interior tiles an
+    // object: the apply path's rule at two waves per SIMD) walk flat.
+    constexpr uint64_t TCV = 4 * bytes::enc_width(KS);
+    const uint64_t nint = std::min<uint64_t>(bytes::interior_vectors(a.S, a.L, a.col0, a.k), ncols >> 2) / TCV;
+    const bool flat = a.nobj > 1 && nseg == 1 && nint <= 4;
+    const dim3 grid = flat ? dim3((uint32_t)blocks) : bytes_grid(ncols, (uint64_t)a.nobj * nseg, nseg, blocks, 1);
+    hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 0>), grid, dim3(kBlock), lds, s, a.slots, a.slot_stride,
+                       a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma, a.coeff, a.out_idx,
+                       a.flags, a.mapping, nseg, record, units, flat ? 1u : 0u);
     if (hipError_t e = hipGetLastError()) return e;
     if (record) {
       a.sw->switched = true;
@@ -695,7 +757,7 @@ hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
   }
   hipLaunchKernelGGL((bytes::encode_bytes_mfma_kernel<KS, 1>), bytes_grid(ncols, 1, 1, blocks1, 1), dim3(kBlock), lds,
                      s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.k, a.mfma,
-                     a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u);
+                     a.coeff, a.out_idx, a.flags, a.mapping, 1u, nullptr, 0u, 0u);
   return hipGetLastError();
 }
 

@@ -352,17 +352,19 @@ def test_graph_exec_keeps_its_set_after_the_graph_is_destroyed(torch_dev, schedu
     assert _held_settles(held0), "the last exec died: the set is back"
 
 
-@pytest.mark.parametrize("need,total", [(10, 14), (40, 56), (80, 100)])
-def test_graph_captured_byte_path_replays_exactly(torch_dev, need, total):
+@pytest.mark.parametrize("need,total,nobj,S", [(10, 14, 6, (24 << 20) + 5), (40, 56, 6, (24 << 20) + 5),
+                                               (80, 100, 6, (24 << 20) + 5), (80, 100, 64, 65541),
+                                               (40, 56, 96, 9005)])
+def test_graph_captured_byte_path_replays_exactly(torch_dev, need, total, nobj, S):
     """The fused byte path captured into a graph: encode_objects (no scratch
     inside a capture, so no mid-object switch: objects mapped with 1<<31 are
     re-encoded whole -- the VALU queue kernel at 10/14, the matrix cores'
     whole-object re-encode at 40/56 and 80/100) and decode_objects on 256 B
     chunk strides, replayed three times over fresh objects, each time equal to
-    the uncaptured calls."""
+    the uncaptured calls.  Batches of short objects walk flat (phase 0 with
+    and without the switch record: the uncaptured calls have one)."""
     torch = torch_dev
     from slime_amd import device as D
-    nobj, S = 6, (24 << 20) + 5
     L, cs, slot = D.slot_geometry(S, need, total, chunk_align=256)
     erase = [0, 3, need, total - 1]
     have = [i for i in range(total) if i not in erase][:need]

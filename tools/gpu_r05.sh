@@ -146,7 +146,7 @@ for step in "$@"; do
                run wilvapi_contig_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 4194304 --nobj 1 &&
                run wilvapi_blocks_$rep 300 python tools/short_objects.py --shapes 80/100,72/90,96/100,40/56 --L 64 --nobj 65536 || exit 1
              done ;;
-    profshort) for cfg in "80/100 16384" "80/100 262144" "40/56 16384"; do
+    profshort) for cfg in "80/100 16384" "80/100 262144" "40/56 16384" "64/80 16384" "64/80 262144"; do
                  read -r shp sz <<< "$cfg"; tag=$(echo "${shp}_$sz" | tr / _)
                  run profshort_$tag 300 rocprofv3 --kernel-trace --stats -d "$OUT/profshort_$tag" -o short --output-format csv -- \
                    python3 tools/short_objects.py --shapes $shp --bytes $sz --nobj 1024 --rounds 3 || exit 1
