@@ -208,10 +208,12 @@ __device__ __forceinline__ EdgeSpan edge_span(uint64_t S, uint64_t L, uint64_t c
 }
 
 // Edge columns [b0, ncols) of every object `take` selects, spread over the
-// whole grid: a wave takes 64 consecutive columns of one object and eight of
+// whole grid: a wave takes 64 consecutive columns of one object and sixteen of
 // its rows (object and rows uniform, so the coefficients are scalar loads),
 // a lane one column: the k data chunks' symbols (splitVector padding, the
-// partial last word) loaded sixteen at a time, summed into the eight rows,
+// partial last word) loaded sixteen at a time, summed into the sixteen rows
+// (eight or four reloaded the symbols more often and ran 15-25% slower at
+// 80/100, profiles/r05/s42_rb/),
 // stored with MapFromGF's mapping; the first row block also writes the
 // data-chunk tails and (F) folds MapToGF's flags into flags[obj].  Replaces a
 // single wave's serial VALU edge step per object, and then one lane per (row,
@@ -227,7 +229,7 @@ __device__ __forceinline__ void spread_edges(uint8_t* __restrict__ slots, uint64
                                              const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
                                              uint64_t b0, uint32_t* __restrict__ flags, Take take) {
   if (b0 >= ncols) return;
-  constexpr uint32_t RB = 8;
+  constexpr uint32_t RB = 16;
   const uint64_t ncb = (ncols - b0 + 63) / 64, nrb = (rows + RB - 1) / RB;
   const uint64_t per = nrb * ncb, total = per * nobj;
   const uint32_t lane = threadIdx.x & 63;
