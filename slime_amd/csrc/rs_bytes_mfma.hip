@@ -473,7 +473,10 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
 // The redo list of a switched matrix-core phase 0: every interior tile of an
 // object whose mapping came out 1<<31 (status 0) that phase 0 encoded with
 // mapping 0 (record 0; 1 = encoded with 1<<31, 2 = not an interior tile), as
-// entries obj * units + tile; *count (zero on entry) receives their number.
+// entries obj * units + tile; *count (zero on entry) receives their number,
+// or'd with kSwitchedBit when any object switched (units >= 1: every object
+// has entries), so the redo skips its edge pass outright when none did.
+constexpr uint32_t kSwitchedBit = 0x80000000u;  // list entries stay far below 2^31
 __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* __restrict__ record,
                                                                 const uint32_t* __restrict__ mapping,
                                                                 const uint32_t* __restrict__ status, uint32_t nobj,
@@ -485,16 +488,18 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
   const uint64_t total = (uint64_t)nobj * units;
   for (uint64_t base = wave * 64; base < total; base += nwaves * 64) {
     const uint64_t e = base + lane;
-    bool need = false;
+    bool sw = false, need = false;
     if (e < total) {
       const uint32_t o = (uint32_t)(e / units);
-      need = mapping[o] != 0 && status[o] == 0 && record[e] == 0;
+      sw = mapping[o] != 0 && status[o] == 0;
+      need = sw && record[e] == 0;
     }
+    if (__ballot(sw) && lane == 0) atomicOr(count, kSwitchedBit);
     const uint64_t mask = __ballot(need);
     if (!mask) continue;
     uint32_t at = 0;
     if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
-    at = __builtin_amdgcn_readlane(at, 0);  // lane 0 drew it, whatever the exec mask
+    at = __builtin_amdgcn_readlane(at, 0) & ~kSwitchedBit;  // lane 0 drew it, whatever the exec mask
     if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
   }
 }
@@ -537,13 +542,15 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
   // The switched objects' edge columns first, spread over the grid (phase 0
   // wrote them with mapping 0).
   const EdgeSpan es = edge_span<TCV>(S, L, col0, k, nvec, nseg);
+  const uint32_t listed = *count;
+  if (!(listed & kSwitchedBit)) return;  // no object switched: nothing to redo
   if (es.spread)
     spread_edges<false>(slots, slot_stride, L, chunk, col0, ncols, ow, nobj, rows, k, cs, coeff, out_idx, 4 * es.e0,
                         nullptr, [&](uint32_t o, uint32_t& m) {
                           m = mapping[o];
                           return m != 0 && status[o] == 0;
                         });
-  const uint32_t n = *count;
+  const uint32_t n = listed & ~kSwitchedBit;
   // The list (ascending tiles of each object, roughly) is cut into G
   // contiguous streams of 8 waves each, as the re-encode's flat walk: all
   // waves on one window of one object streamed at 2.3 TB/s
