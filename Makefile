@@ -16,14 +16,24 @@ CACHETEST := tests/cpp/plan_cache_test
 COPYTEST := tests/cpp/copy_pool_test
 POOLTEST := tests/cpp/device_pool_test
 MFMATEST := tests/cpp/mfma_table_test
+DMATEST  := tests/cpp/dma_plan_test
+REDOTEST := tests/cpp/redo_list_test
 PROXYLOAD := tools/libproxy_load.so
 
-all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST) $(PROXYLOAD)
+all: $(LIB) oracle $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST) $(DMATEST) $(REDOTEST) $(PROXYLOAD)
 
 # Proxy-level load generator over the C-ABI (bench.py host_path.pooled): C++ threads, no GIL.
-$(PROXYLOAD): tools/proxy_load.cpp include/slime_rs.h $(LIB)
-	g++ -std=c++17 -O2 -Wall -Wextra -pthread -fPIC -shared -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs \
+$(PROXYLOAD): tools/proxy_load.cpp tools/crash_report.hpp include/slime_rs.h $(LIB)
+	g++ -std=c++17 -O2 -g -Wall -Wextra -pthread -fPIC -shared -Iinclude -o $@ $< -Lslime_amd/lib -lslime_rs -ldl \
 	  -Wl,-rpath,'$$ORIGIN/../slime_amd/lib'
+
+# The matrix-core redo list's counter protocol (redo_list.hpp) emulated with threads, CPU only.
+$(REDOTEST): tests/cpp/redo_list_test.cpp $(SRC)/redo_list.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -pthread -I$(SRC) -o $@ tests/cpp/redo_list_test.cpp
+
+# The host pipeline's copy planning and extent checks (dma_plan.hpp), CPU only.
+$(DMATEST): tests/cpp/dma_plan_test.cpp $(SRC)/dma_plan.hpp
+	g++ -std=c++17 -O2 -Wall -Wextra -I$(SRC) -o $@ tests/cpp/dma_plan_test.cpp
 
 # The matrix-core kernel's int8-limb arithmetic emulated on its table (mfma_table.hpp), CPU only.
 $(MFMATEST): tests/cpp/mfma_table_test.cpp $(SRC)/mfma_table.hpp $(SRC)/gfp.hpp $(SRC)/gfp_host.hpp
@@ -63,7 +73,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(PROXYLOAD) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST)
+	rm -rf build $(LIB) $(PROXYLOAD) $(CXXTEST) $(CACHETEST) $(COPYTEST) $(POOLTEST) $(MFMATEST) $(DMATEST) $(REDOTEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -128,6 +128,9 @@ int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
   if (int rc = ws->reserve_pinned(kStageBytes * kHostStages)) return rc;
   if (int rc = ws->ensure_stages()) return rc;
   const std::vector<Span> pcs = pieces_of(sp, n);
+  for (const Span& x : pcs)  // every download inside the device buffer (each piece fits its stage by construction)
+    if (dev < ws->dbuf || copy_end((uint64_t)(dev - ws->dbuf) + x.dev_off, 1, 0, x.bytes) > ws->dcap)
+      return fail(Status::InvalidArg, "download outside the workspace");
   const int S = kHostStages;
   HIP_TRY(hipEventRecord(ws->cev, ws->stream));
   for (int s = 0; s < S; ++s) HIP_TRY(hipStreamWaitEvent(ws->sst[s], ws->cev, 0));
@@ -151,69 +154,36 @@ int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n) {
   return 0;
 }
 
-// Windows moving at most this many bytes one way go as one copy kernel over
-// the mapped pinned ring instead of copy-engine transfers (host_blit.hip):
-// uploads up to 4 MiB (a kernel reading host memory is latency-bound, so
-// larger uploads keep the copy engines: a 64 MiB CreateParity ran 1.88 ms
-// instead of 1.41 with kernel uploads), downloads of every window size (the
-// kernel's writes are posted and run beside the copy engines' uploads --
-// fused reconstruct +4-7%, write_chunks +3-10%, profiles/r04/s19-s20).
-constexpr uint64_t kBlitUpBytes = 4u << 20;
-constexpr uint64_t kBlitDownBytes = 64u << 20;
-
-// DMA spans one by one, merging neighbours contiguous on both sides.  Runs of
-// equal-length spans at constant device and pinned strides (a window's rows:
-// one per chunk) go as one pitched copy: per-span copies reach the copy
-// engine as separate commands ~10 us apart, and one pitched copy took the
-// fused reconstruct from 22 to 27 GiB/s and write_chunks from 32 to 36
-// (profiles/r04/s24_rctrace, s25_dma2d).
-int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
-              hipStream_t st) {
-  uint64_t total = 0;
-  for (const Span& s : sp) total += s.bytes;
-  if (total && total <= (h2d ? kBlitUpBytes : kBlitDownBytes)) {
+int dma_spans(uint8_t* dev, uint64_t dev_cap, uint8_t* pin, uint64_t pin_cap, const std::vector<Span>& sp,
+              const std::vector<size_t>& off, bool h2d, hipStream_t st) {
+  const DmaPlan p = plan_dma(sp, off, h2d);
+  if (first_out_of_bounds(p, dev_cap, pin_cap) >= 0)
+    return fail(Status::InvalidArg, h2d ? "window upload outside its buffers" : "window download outside its buffers");
+  if (p.blit) {
     std::vector<BlitSpan> bl;
-    bl.reserve(sp.size());
-    for (size_t i = 0; i < sp.size();) {  // neighbours contiguous on both sides merge, as below
-      size_t j = i + 1, bytes = sp[i].bytes;
-      while (j < sp.size() && sp[j].dev_off == sp[i].dev_off + bytes && off[j] == off[i] + bytes) bytes += sp[j++].bytes;
+    bl.reserve(p.copies.size());
+    for (const DmaCopy& c : p.copies)
       if (h2d)
-        bl.push_back({dev + sp[i].dev_off, pin + off[i], bytes});
+        bl.push_back({dev + c.dev_off, pin + c.pin_off, c.width});
       else
-        bl.push_back({pin + off[i], dev + sp[i].dev_off, bytes});
-      i = j;
-    }
+        bl.push_back({pin + c.pin_off, dev + c.dev_off, c.width});
     HIP_TRY(launch_blit(bl.data(), (int)bl.size(), st));
     return 0;
   }
-  for (size_t i = 0; i < sp.size();) {
-    size_t j = i + 1;
-    const uint64_t bytes = sp[i].bytes;
-    const int64_t dd = j < sp.size() ? (int64_t)sp[j].dev_off - (int64_t)sp[i].dev_off : 0;
-    const int64_t dp = j < sp.size() ? (int64_t)off[j] - (int64_t)off[i] : 0;
-    if (dd >= (int64_t)bytes && dp >= (int64_t)bytes)
-      while (j < sp.size() && sp[j].bytes == bytes && (int64_t)sp[j].dev_off - (int64_t)sp[j - 1].dev_off == dd &&
-             (int64_t)off[j] - (int64_t)off[j - 1] == dp)
-        ++j;
-    if (j - i >= 2) {
+  for (const DmaCopy& c : p.copies) {
+    if (!c.width) continue;
+    if (c.rows >= 2) {
       if (h2d)
-        HIP_TRY(hipMemcpy2DAsync(dev + sp[i].dev_off, (size_t)dd, pin + off[i], (size_t)dp, bytes, j - i,
+        HIP_TRY(hipMemcpy2DAsync(dev + c.dev_off, c.dev_pitch, pin + c.pin_off, c.pin_pitch, c.width, c.rows,
                                  hipMemcpyHostToDevice, st));
       else
-        HIP_TRY(hipMemcpy2DAsync(pin + off[i], (size_t)dp, dev + sp[i].dev_off, (size_t)dd, bytes, j - i,
+        HIP_TRY(hipMemcpy2DAsync(pin + c.pin_off, c.pin_pitch, dev + c.dev_off, c.dev_pitch, c.width, c.rows,
                                  hipMemcpyDeviceToHost, st));
-      i = j;
-      continue;
+    } else if (h2d) {
+      HIP_TRY(hipMemcpyAsync(dev + c.dev_off, pin + c.pin_off, c.width, hipMemcpyHostToDevice, st));
+    } else {
+      HIP_TRY(hipMemcpyAsync(pin + c.pin_off, dev + c.dev_off, c.width, hipMemcpyDeviceToHost, st));
     }
-    // a run of spans contiguous on both sides as one copy
-    uint64_t run = bytes;
-    for (j = i + 1; j < sp.size() && sp[j].dev_off == sp[i].dev_off + run && off[j] == off[i] + run; ++j)
-      run += sp[j].bytes;
-    if (h2d)
-      HIP_TRY(hipMemcpyAsync(dev + sp[i].dev_off, pin + off[i], run, hipMemcpyHostToDevice, st));
-    else
-      HIP_TRY(hipMemcpyAsync(pin + off[i], dev + sp[i].dev_off, run, hipMemcpyDeviceToHost, st));
-    i = j;
   }
   return 0;
 }

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "capi_internal.hpp"
+#include "dma_plan.hpp"
 #include "host_copy.hpp"
 
 namespace slime {
@@ -70,22 +71,18 @@ struct WsLease {
 // Waits for everything the workspace queued (error paths).
 void drain_stages(Workspace* ws);
 
-// A host range and its device offset.
-struct Span {
-  uint8_t* host;
-  uint64_t dev_off;
-  uint64_t bytes;
-};
-
 // dev -> host spans after everything queued on ws->stream so far, through
 // the pinned stages; returns when the host copies are complete.
 int staged_d2h(Workspace* ws, const uint8_t* dev, const Span* sp, size_t n);
 
-// DMA spans between the device layout at `dev` and the pinned stage `pin`
-// (offsets `off`): one copy kernel when the window is small, pitched copies
-// for runs of equal rows, else one copy per run of contiguous spans.
-int dma_spans(uint8_t* dev, uint8_t* pin, const std::vector<Span>& sp, const std::vector<size_t>& off, bool h2d,
-              hipStream_t st);
+// DMA spans between the device layout at `dev` (dev_cap bytes) and the
+// pinned stage `pin` (pin_cap bytes; span i at offset off[i]) as plan_dma
+// (dma_plan.hpp) cuts them: one copy kernel when the window is small,
+// pitched copies for runs of equal rows, else one copy per run of contiguous
+// spans.  A copy reaching past either buffer is refused before anything is
+// enqueued (SLIME_RS_ERR_INVALID_ARG).
+int dma_spans(uint8_t* dev, uint64_t dev_cap, uint8_t* pin, uint64_t pin_cap, const std::vector<Span>& sp,
+              const std::vector<size_t>& off, bool h2d, hipStream_t st);
 
 // Inputs (bytes) up to which a one-window call runs its kernel on the mapped
 // pinned stage itself (env SLIME_RS_DIRECT_KIB, default 16384; 0 = never).
@@ -139,6 +136,10 @@ int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&
                                              : stage_bytes * S))
     return rc;
   if (int rc = ws->ensure_stages()) return rc;
+  // `dev` lies in the workspace's device buffer (every caller passes
+  // ws->dbuf); its copies are bounded by what is left of that buffer.
+  if (dev < ws->dbuf || dev > ws->dbuf + ws->dcap) return fail(Status::InvalidArg, "window layout outside the workspace");
+  const uint64_t dev_cap = (uint64_t)(ws->dbuf + ws->dcap - dev);
   std::vector<Window> win(S);
   std::vector<CopyItem> items;
   auto pin_of = [&](int s) { return ws->pin + (size_t)s * stage_bytes; };
@@ -223,9 +224,9 @@ int run_windows(Workspace* ws, uint8_t* dev, uint64_t n, size_t stage_bytes, Io&
       if (direct) {  // the kernel on the stage: no copies across PCIe besides its own accesses
         if (int rc = launch(c, s, st, pin)) return rc;
       } else {
-        if (int rc = dma_spans(dev, pin, w.in, w.in_off, true, st)) return rc;
+        if (int rc = dma_spans(dev, dev_cap, pin, stage_bytes, w.in, w.in_off, true, st)) return rc;
         if (int rc = launch(c, s, st, dev)) return rc;
-        if (int rc = dma_spans(dev, pin, w.out, w.out_off, false, st)) return rc;
+        if (int rc = dma_spans(dev, dev_cap, pin, stage_bytes, w.out, w.out_off, false, st)) return rc;
       }
       HIP_TRY(hipEventRecord(ws->sev[s], st));
       t_enq += ms_since(t0);

@@ -27,6 +27,7 @@
 #include "rs_apply_mfma_kernel.hpp"
 #include "rs_bytes_kernel.hpp"
 #include "rs_bytes_launch.hpp"
+#include "redo_list.hpp"
 
 namespace slime {
 namespace bytes {
@@ -475,8 +476,9 @@ encode_bytes_mfma_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride, uint
 // mapping 0 (record 0; 1 = encoded with 1<<31, 2 = not an interior tile), as
 // entries obj * units + tile; *count (zero on entry) receives their number,
 // or'd with kSwitchedBit when any object switched (units >= 1: every object
-// has entries), so the redo skips its edge pass outright when none did.
-constexpr uint32_t kSwitchedBit = 0x80000000u;  // list entries stay far below 2^31
+// has entries), so the redo skips its edge pass outright when none did.  The
+// word's protocol and its bound are redo_list.hpp's (the host launches this
+// only when redo_list_fits(nobj, units)).
 __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* __restrict__ record,
                                                                 const uint32_t* __restrict__ mapping,
                                                                 const uint32_t* __restrict__ status, uint32_t nobj,
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void mfma_redo_list_kernel(const uint8_t* _
     if (!mask) continue;
     uint32_t at = 0;
     if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(mask));
-    at = __builtin_amdgcn_readlane(at, 0) & ~kSwitchedBit;  // lane 0 drew it, whatever the exec mask
+    at = redo_offset(__builtin_amdgcn_readlane(at, 0));  // lane 0 drew it, whatever the exec mask
     if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
   }
 }
@@ -543,14 +545,14 @@ encode_bytes_mfma_redo_kernel(uint8_t* __restrict__ slots, uint64_t slot_stride,
   // wrote them with mapping 0).
   const EdgeSpan es = edge_span<TCV>(S, L, col0, k, nvec, nseg);
   const uint32_t listed = *count;
-  if (!(listed & kSwitchedBit)) return;  // no object switched: nothing to redo
+  if (!redo_switched(listed)) return;  // no object switched: nothing to redo
   if (es.spread)
     spread_edges<false>(slots, slot_stride, L, chunk, col0, ncols, ow, nobj, rows, k, cs, coeff, out_idx, 4 * es.e0,
                         nullptr, [&](uint32_t o, uint32_t& m) {
                           m = mapping[o];
                           return m != 0 && status[o] == 0;
                         });
-  const uint32_t n = listed & ~kSwitchedBit;
+  const uint32_t n = redo_count(listed);
   // The list (ascending tiles of each object, roughly) is cut into G
   // contiguous streams of 8 waves each, as the re-encode's flat walk: all
   // waves on one window of one object streamed at 2.3 TB/s
@@ -724,7 +726,7 @@ hipError_t enc_ks(const BytesLaunch& a, hipStream_t s) {
     // record (never inside a graph capture).
     uint8_t* record = nullptr;
     uint32_t units = 0;
-    if (a.scratch && a.sw) {
+    if (a.scratch && a.sw && bytes::redo_list_fits(a.nobj, switch_units<KS>(a))) {
       units = switch_units<KS>(a);
       bytes::SwitchLayout l;
       l.units = units;
@@ -811,7 +813,10 @@ uint64_t encode_switch_bytes_mfma(const BytesLaunch& a) {
     case 7: units = switch_units<7>(a); break;
     default: return 0;
   }
-  return units ? 256 + 5ull * a.nobj * units : 0;
+  // No switch scratch when the list could reach the counter's flag bit: the
+  // batch then re-encodes its switched objects whole (redo_list.hpp).
+  if (!units || !bytes::redo_list_fits(a.nobj, units)) return 0;
+  return 256 + 5ull * a.nobj * units;
 }
 
 bool bytes_mfma_eligible(const BytesLaunch& a, bool encode) {

@@ -102,3 +102,39 @@ def test_mfma_table_arithmetic_emulated():
     r = subprocess.run([MFMA_BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bit-exact" in r.stdout
+
+
+DMA_BIN = os.path.join(ROOT, "tests", "cpp", "dma_plan_test")
+
+
+def test_dma_plan_extents_are_checked():
+    """slime_amd/csrc/dma_plan.hpp (the copies dma_spans issues): host_apply's
+    and write_chunks' window layouts plan to the expected pitched / blit
+    commands whose last byte is the last span's; 3000 random span lists
+    replayed byte by byte copy exactly their spans and nothing else; the
+    extent check refuses a plan one byte past either buffer and a pitched
+    extent that overflows 64 bits (the bound on every
+    hipMemcpy2DAsync / hipMemcpyAsync extent)."""
+    subprocess.run(["make", "-C", ROOT, "tests/cpp/dma_plan_test"], check=True, capture_output=True)
+    r = subprocess.run([DMA_BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestHostApplyLayout", "TestWriteChunksLayout", "TestPlanFaithful", "TestExtentOverflow"):
+        assert f"ok   {name}" in r.stdout
+
+
+REDO_BIN = os.path.join(ROOT, "tests", "cpp", "redo_list_test")
+
+
+def test_redo_list_counter_protocol_emulated():
+    """slime_amd/csrc/redo_list.hpp (the matrix-core redo list's counter word,
+    rs_bytes_mfma.hip): waves setting the switched bit before and after
+    others draw offsets, in every fixed order and on 8 real threads over 60
+    random batches -- every drawn offset masked, each needed entry listed
+    once, the count and the switched flag recovered; redo_list_fits refuses
+    batches of 2^31 entries or more, which then take the whole-object redo
+    (VERDICT r05 item 2)."""
+    subprocess.run(["make", "-C", ROOT, "tests/cpp/redo_list_test"], check=True, capture_output=True)
+    r = subprocess.run([REDO_BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestRedoListFixedOrders", "TestRedoListConcurrent", "TestRedoListFits"):
+        assert f"ok   {name}" in r.stdout

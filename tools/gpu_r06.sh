@@ -1,0 +1,58 @@
+#!/usr/bin/env bash
+# Round-6 GPU-box session: every GPU step under its own time limit; the first
+# crash/abort/timeout ends the session (nothing more runs on the GPU).
+# Usage (repo root, on the box):  bash tools/gpu_r06.sh <step> [<step>...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs= --pooled 0"
+
+run() {  # run <name> <limit-seconds> <command...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then
+    echo "!!! $name ended with rc=$rc: stopping the session" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+}
+
+# pmc <name> <counter> <bench args...>: one counter pass of bench.py
+pmc() {
+  local name=$1 counter=$2; shift 2
+  run "$name" 300 timeout -s KILL 240 rocprofv3 --pmc "$counter" -d "$OUT/$name" -o pmc --output-format csv -- \
+    python3 bench.py "$@"
+}
+
+nproc > "$OUT/host.txt"; grep -m1 "model name" /proc/cpuinfo >> "$OUT/host.txt" || true
+for step in "$@"; do
+  case "$step" in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    tests_host) run pytest_host 400 python -u -m pytest tests/test_gpu_parity.py tests/test_cpp_host.py -x -q --timeout 120 --timeout-method thread -m gpu -k "map or recover or host or unchanged or RecoverData or reconstruct or pool or create or parity or write_chunks" ;;
+    tests_switch) run pytest_switch 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "mid_object_switch or encode_objects or write_chunks or redo" ;;
+    tests_mfma) run pytest_mfma 600 python -u -m pytest tests/test_gpu_mfma.py -x -q --timeout 300 --timeout-method thread ;;
+    tests_bench) run pytest_bench 400 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 200 --timeout-method thread ;;
+    tests_full) run pytest_full 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    # the driver's command under the profiler WITH the pooled leg
+    profpool) run profpool 700 rocprofv3 --kernel-trace --stats -d "$OUT/profpool" -o bench --output-format csv -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    # only the pooled leg under the profiler (short), to reproduce the r05 fault quickly
+    profpoolonly) run profpoolonly 400 rocprofv3 --kernel-trace --stats -d "$OUT/profpoolonly" -o pool --output-format csv -- \
+            python3 bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
+    hostonly) run hostonly 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
+    pmc_c3) pmc pmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
+            pmc pmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
+    bpmc_c5) pmc bpmc_c5_fetch FETCH_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
+             pmc bpmc_c5_write WRITE_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
+    *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
+  esac
+done
+echo "=== session done" | tee -a "$OUT/session.log"

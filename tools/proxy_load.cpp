@@ -27,7 +27,9 @@
 // its chunks after the last PUT hash the same as after the first, and (pattern
 // 1) equal the fused path's chunks for that object.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -36,6 +38,7 @@
 #include <thread>
 #include <vector>
 
+#include "crash_report.hpp"
 #include "slime_rs.h"
 
 namespace {
@@ -168,6 +171,17 @@ double pct(std::vector<double> v, double q) {
 extern "C" int proxy_load(int threads, uint64_t object_bytes, int need, int total, const int* have, int pattern,
                           double seconds, uint64_t seed, double* out) {
   if (threads < 1 || need < 1 || total < need || !have || !out || (pattern != 0 && pattern != 1)) return 9;
+  // A fault in any thread prints a resolved report first (crash_report.hpp;
+  // PROXY_LOAD_CRASH_REPORT=0 turns it off).
+  const char* cr = getenv("PROXY_LOAD_CRASH_REPORT");
+  const bool report = !cr || atoi(cr) != 0;
+  if (report) crash_report::install();
+  struct Uninstall {
+    bool on;
+    ~Uninstall() {
+      if (on) crash_report::uninstall();
+    }
+  } uninstall_at_exit{report};
   const auto t_setup = Clock::now();
   std::vector<std::unique_ptr<Request>> reqs(threads);
   {
@@ -270,4 +284,18 @@ extern "C" int proxy_load(int threads, uint64_t object_bytes, int need, int tota
   out[8] = (double)failed.load();
   out[9] = warm_s;
   return first_rc.load();
+}
+
+// Test hook of the crash report (tests/test_host.py): installs it, then
+// writes past the end of a mapping into a PROT_NONE page as a runaway memcpy
+// would.  The process then dies of SIGSEGV after the report.
+extern "C" void proxy_load_fault_selftest(void) {
+  crash_report::install();
+  const long pg = sysconf(_SC_PAGESIZE);
+  uint8_t* p = (uint8_t*)mmap(nullptr, 2 * pg, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return;
+  mprotect(p + pg, pg, PROT_NONE);
+  static uint8_t src[1 << 16];
+  volatile size_t n = 2 * (size_t)pg;
+  memcpy(p, src, n);
 }
