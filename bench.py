@@ -81,6 +81,9 @@ def parse(argv=None):
                          "decode {0,1,2,3}) and report it as c5_partitioned")
     ap.add_argument("--bytes-path", type=int, default=1,
                     help="also time the fused object-bytes pipeline (MapToGF+encode+MapFromGF, repair)")
+    ap.add_argument("--c5-bytes", type=int, default=1,
+                    help="also time the fused object-bytes pipeline at BASELINE config 5's shape per GPU: 10/14, "
+                         "16 x 1 GiB objects on 256 B-aligned chunk strides (object_bytes_path_c5)")
     ap.add_argument("--ceilings", type=int, default=1,
                     help="measure torch copy/fill HBM rates after the timed region (roofline.measured_streams)")
     ap.add_argument("--host-path", type=int, default=1,
@@ -316,7 +319,8 @@ def _matrix_cores(k: int, rows: int) -> bool:
     return k >= 33 or (k >= 17 and k * rows >= 128)
 
 
-def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[int], seconds: float) -> dict:
+def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[int], seconds: float,
+                 samples: dict | None = None) -> dict:
     """The reference's algorithm on host cores, on the
     bench's own input: `sample` is one object of the timed batch copied out of
     HBM after the timed steps (total x L symbols: its data shards and the
@@ -331,6 +335,9 @@ def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[in
     from oracle import oracle_c as OC
 
     have = [i for i in range(total) if i not in erase][:need]
+    t_pin = time.perf_counter()
+    pin = oracle_pin(samples or {})
+    pin_s = time.perf_counter() - t_pin
     # Every core this process may run on: its affinity set, capped by its
     # cgroup's CPU quota when there is one (a 1-GPU share of the GPU box sees
     # 256 CPUs but may use 16; more threads than that only time-slice).
@@ -371,6 +378,7 @@ def cpu_baseline(sample, sample_name: str, need: int, total: int, erase: list[in
     return {"value": allc["value"], "unit": "GiB/s", "cores": ncores, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cores": affinity,
             "cgroup_cpu_quota": quota, "verified": ok,
+            "oracle_pin": pin, "oracle_pin_seconds": round(pin_s, 2),
             "single_thread": one, "all_cores": allc,
             "small_objects_one_thread": {"sizes": small,
                                          "what": "per object, in C with the reference's matrix cache: r "
@@ -394,18 +402,82 @@ def batch_empty(args, numel: int, dtype: torch.dtype, dev: int) -> torch.Tensor:
     return torch.empty(numel, dtype=dtype, device=f"cuda:{dev}")
 
 
+ORACLE_COLS = 4096  # columns per object pinned to the oracle (plus the last column)
+
+
+def column_sample(v3: torch.Tensor, L: int, seed: int, ncols: int = ORACLE_COLS) -> dict:
+    """Columns of every object of a batch for the oracle pin (oracle_pin, run
+    inside the cpu_baseline leg): a window of `ncols` consecutive columns at a
+    per-object seeded offset, plus the last column L-1, gathered on the
+    device from v3 = [object][row][column] int32 words and copied to the host.
+    A copy only: nothing here computes."""
+    import numpy as np
+
+    nobj, rows, _ = v3.shape
+    w = min(ncols, L)
+    g = torch.Generator().manual_seed(seed)
+    off = torch.randint(0, L - w + 1, (nobj,), generator=g)
+    idx = torch.cat([off[:, None] + torch.arange(w)[None, :], torch.full((nobj, 1), L - 1)], dim=1)
+    cols = torch.gather(v3, 2, idx.to(v3.device)[:, None, :].expand(nobj, rows, w + 1))
+    return {"cols": cols.cpu().numpy().view(np.uint32), "offsets": off.tolist(), "window": w, "L": L}
+
+
+def oracle_pin(samples: dict) -> dict:
+    """Every object of every timed batch against the reference's arithmetic
+    (oracle/rs_oracle.c: vector.go:90-102 applyMatrix, :50-88 RecoverData), on
+    the sampled columns: the parity rows equal the oracle's encode of the data
+    rows, and the oracle's RecoverData from the survivors (the first `need`
+    available rows, multi_store.go:218-235) returns the data rows -- the
+    erased ones as the timed decode rebuilt them.  Byte batches are taken
+    back to symbols with the object's mapping first (MapToGFWith, map.go:74-98:
+    big-endian words XOR the mapping); the mapping choice itself is pinned by
+    tests/test_gpu_fullsize.py.  Runs only inside the cpu_baseline leg."""
+    import numpy as np
+
+    from oracle import oracle_c as OC
+
+    out = {}
+    for name, smp in samples.items():
+        need, total, have = smp["need"], smp["total"], smp["have"]
+        cols = smp["cols"]
+        good = 0
+        for o in range(cols.shape[0]):
+            sym = cols[o]
+            if smp.get("mapping") is not None:
+                sym = sym.byteswap() ^ np.uint32(smp["mapping"][o])
+            sym = np.ascontiguousarray(sym, dtype=np.uint32)
+            enc = np.zeros_like(sym)
+            enc[:need] = sym[:need]
+            OC.encode_object(enc, need, total)
+            rc, rec = OC.recover_data([sym[i] for i in have], have)
+            if rc == 0 and np.array_equal(enc[need:], sym[need:]) and \
+                    all(np.array_equal(rec[t], sym[t]) for t in range(need)):
+                good += 1
+        out[name] = {"objects": int(cols.shape[0]), "verified_objects": good,
+                     "columns_per_object": int(cols.shape[2]), "window": smp["window"],
+                     "includes_last_column": True, "domain": "bytes" if smp.get("mapping") is not None else "symbols"}
+    return out
+
+
 ALLOCATOR_NOTE = {"vmm": "slime_rs_device_alloc: HIP virtual memory, physical chunks mapped in order",
                   "torch": "torch.empty (hipMalloc via the caching allocator)"}
 
 
-def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int) -> dict:
+def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int], nobj: int, mib: int | None = None,
+              samples: dict | None = None, tag: str = "bytes") -> dict:
     """writeChunks / reconstruct on device from object bytes (rs_bytes.hip): one
     speculative encode pass that also picks gf.MapToGF's mapping (switching an
     object to 1<<31 once one of its words >= p has been seen), a redo pass over
     the units encoded before that, and an in-place repair of the erased chunks
     from chunk bytes.  Objects that would need MapToGF's random
-    fallback are re-drawn before timing and counted."""
-    S = args.object_mib << 20
+    fallback are re-drawn before timing and counted.  A HIP
+    event recorded by the library between the two encode passes
+    (slime_rs_encode_objects_phased) splits the encode time into the
+    speculative pass and the 1<<31 re-encode.  `samples`: where to leave the
+    column sample of every object for the oracle pin (cpu_baseline leg)."""
+    import numpy as np
+
+    S = (mib or args.object_mib) << 20
     L, cs, slot = D.slot_geometry(S, need, total, chunk_align=args.chunk_align)
     chunk_stride = cs if args.chunk_align > 1 else 0
     slots = batch_empty(args, nobj * slot, torch.uint8, dev)
@@ -436,7 +508,8 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream, chunk_stride)
+        D.encode_objects(enc, slots, slot, S, nobj, mapping, status, stream, chunk_stride,
+                         phase_event=None if ev is None else ev[3])
         if ev is not None:
             ev[1].record(stream)
         D.decode_objects(dec, slots, slot, L, nobj, mapping, stream, chunk_stride)
@@ -445,7 +518,9 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
 
     for _ in range(args.warmup):
         step()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    for e in events:  # torch creates an event at its first record; the library records e[3] again mid-encode
+        e[3].record(stream)
     batch.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -455,9 +530,15 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     batch.barrier()
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    pass0_ms = sum(e[0].elapsed_time(e[3]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
     ok = bool(torch.equal(erased(), truth)) and int(status.sum().item()) == 0
     ms = mapping.cpu().numpy().view("uint32")
+    if samples is not None:
+        smp = column_sample(words.view(nobj, slot // 4)[:, : total * cs // 4].view(nobj, total, cs // 4), L,
+                            0x5A3D + need)
+        smp.update(need=need, total=total, have=have, mapping=ms.copy())
+        samples[tag] = smp
     elapsed, = batch.max_over_ranks([elapsed])
     del slots, words, truth
     torch.cuda.empty_cache()
@@ -480,9 +561,13 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": t, "traffic_over_alg": round(t / alg, 4) if t else None}
     return {"value": round(2 * nobj * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
+            "config": f"need={need} total={total}, {S >> 20} MiB objects x {nobj} per GPU, chunk stride {cs} B; "
+                      f"encode (both passes) + repair erased {erase}",
             "encode_gibs": round(nobj * S / GIB / (enc_ms * 1e-3), 2),
             "decode_gibs": round(nobj * S / GIB / (dec_ms * 1e-3), 2),
-            "kernel_ms": {"encode_both_passes": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+            "kernel_ms": {"encode_both_passes": round(enc_ms, 4), "encode_pass0": round(pass0_ms, 4),
+                          "encode_redo": round(enc_ms - pass0_ms, 4), "decode": round(dec_ms, 4)},
+            "redo_share": round((enc_ms - pass0_ms) / enc_ms, 4) if enc_ms else None,
             "roofline": {"encode": leg("encode", alg_enc, enc_ms), "decode": leg("decode", alg_dec, dec_ms),
                          "traffic_source": replay.get("source")},
             "mappings": {"0": int((ms == 0).sum()), "1<<31": int((ms == 0x80000000).sum()),
@@ -491,30 +576,33 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
             "chunk_stride": cs, "chunk_bytes": 4 * L,
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
                     "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
-                    "erased chunks from chunk bytes"}
+                    "erased chunks from chunk bytes; encode_pass0 / encode_redo split at a HIP event the library "
+                    "records between the passes (the redo includes its list build and the 1<<31 edge columns)"}
 
 
 def _bytes_traffic(args, config: str, need: int, kernels: dict) -> dict:
     """PMC bytes per step of the byte path's kernels at `config`, replayed from
-    profiles/r04/pmc_bytes.json only where every kernel's machine code matches
-    this build (slime_amd/codeobj.py); {} otherwise."""
-    path = os.path.join(ROOT, "profiles", "r04", "pmc_bytes.json")
-    try:
-        entries = json.load(open(path))
-    except (OSError, ValueError):
-        return {}
-    e = next((x for x in entries if x.get("config") == config), None)
-    if not e:
-        return {}
-    ks = e.get("kernels", {})
-    out = {}
-    for what, names in kernels.items():
-        if not all(n in ks and ks[n].get("kernel_code") == kernel_code_id(D.N.LIB_PATH, (f"{n}ILi{need}E",))
-                   for n in names):
-            return {}
-        out[what] = sum(ks[n]["hbm_bytes"] for n in names)
-    out["source"] = f"replayed: profiles/r04/pmc_bytes.json (session {e.get('session', '?')}, matching machine code)"
-    return out
+    profiles/r06/pmc_bytes.json (then r04's) only where every kernel's machine
+    code matches this build (slime_amd/codeobj.py); {} otherwise."""
+    for rnd in ("r06", "r04"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_bytes.json")
+        try:
+            entries = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for e in (x for x in entries if x.get("config") == config):
+            ks = e.get("kernels", {})
+            out = {}
+            for what, names in kernels.items():
+                if not all(n in ks and ks[n].get("kernel_code") == kernel_code_id(D.N.LIB_PATH, (f"{n}ILi{need}E",))
+                           for n in names):
+                    break
+                out[what] = sum(ks[n]["hbm_bytes"] for n in names)
+            else:
+                out["source"] = (f"replayed: profiles/{rnd}/pmc_bytes.json (session {e.get('session', '?')}, "
+                                 "matching machine code)")
+                return out
+    return {}
 
 
 def host_leg(need, total, erase, obj_mib=64, reps=5):
@@ -1048,6 +1136,17 @@ class SymbolBatch:
         return {"elapsed": elapsed, "enc_all": [e[0].elapsed_time(e[1]) for e in events],
                 "dec_all": [e[1].elapsed_time(e[2]) for e in events], "ok": ok}
 
+    def sample(self, seed: int) -> dict:
+        """column_sample of every object as the timed steps left it: the data
+        rows (erased ones rebuilt by the last decode) and the parity rows of
+        the last encode."""
+        smp = column_sample(self.buf.view(self.nobj, self.total, self.SS), self.L, seed)
+        if self.decode_dst != "inplace":  # the rebuilt rows live in self.rec (same seed: same columns)
+            rec = column_sample(self.rec.view(self.nobj, len(self.erase), self.SS), self.L, seed)
+            smp["cols"][:, self.erase] = rec["cols"]
+        smp.update(need=self.need, total=self.total, have=self.have)
+        return smp
+
     def alg_bytes(self) -> tuple[int, int]:
         """Algorithmic HBM bytes per launch: encode 4L(k + r),
         decode 4L(k + e) per object."""
@@ -1095,7 +1194,7 @@ def apply_kernel_name(need: int, rows: int, L: int, shard_bytes_span: int) -> st
     return kname
 
 
-def c5_leg(args, dev: int, rank: int, world: int) -> dict:
+def c5_leg(args, dev: int, rank: int, world: int, samples: dict | None = None) -> dict:
     """BASELINE config 5 inside every `bench.py --gpus N` run: need=10/total=14,
     64 x 1 GiB objects partitioned over the N ranks (batch.partition: 64 at
     N=1, 8 each at N=8), encode all parity + decode erased {0,1,2,3}.  Objects
@@ -1108,6 +1207,8 @@ def c5_leg(args, dev: int, rank: int, world: int) -> dict:
     S = mib << 20
     sb = SymbolBatch(args, dev, 0xC5C5 + 7919 * rank, need, total, S, nobj, erase)
     res = sb.run(args.steps, args.warmup)
+    if samples is not None and nobj:
+        samples["c5_partitioned"] = sb.sample(0xC5C5)
     enc_ms = sum(res["enc_all"]) / len(res["enc_all"])
     dec_ms = sum(res["dec_all"]) / len(res["dec_all"])
     enc_alg, dec_alg = sb.alg_bytes()
@@ -1198,7 +1299,8 @@ def pooled_leg(args, rank: int, world: int, devices: list[int]) -> dict | None:
     return out
 
 
-def shape_leg(args, name: str, dev: int, rank: int, world: int, reuse: torch.Tensor | None) -> dict:
+def shape_leg(args, name: str, dev: int, rank: int, world: int, reuse: torch.Tensor | None,
+              samples: dict | None = None) -> dict:
     """A BASELINE shape beside the headline C3+C4 (PRESETS[name]: c2 = config
     2, 4/6 x 32 x 64 MiB; ns64 = the north star's "8/12 on 64 MiB shards", 64 x
     512 MiB), timed like the main region (W untimed steps, K timed ones of one
@@ -1213,6 +1315,8 @@ def shape_leg(args, name: str, dev: int, rank: int, world: int, reuse: torch.Ten
     sb = SymbolBatch(args, dev, 0x5113E + 0x1000 * (1 + sorted(PRESETS).index(name)) + 7919 * rank,
                      need, total, S, per_gpu, erase, reuse=reuse)
     res = sb.run(args.steps, args.warmup)
+    if samples is not None and per_gpu:
+        samples[name] = sb.sample(0x5A30 + need)
     enc_ms = sum(res["enc_all"]) / len(res["enc_all"])
     dec_ms = sum(res["dec_all"]) / len(res["dec_all"])
     enc_alg, dec_alg = sb.alg_bytes()
@@ -1334,8 +1438,12 @@ def main():
     # (data shards + the parity of the timed encodes), copied out before the
     # buffer is freed.
     cpu_sample = None
-    if rank == 0 and world == 1 and args.cpu_baseline and nobj:
+    # Column samples of every object of every timed batch, for the oracle pin
+    # inside the cpu_baseline leg (rank 0 at N = 1, as that leg).
+    samples = {} if rank == 0 and world == 1 and args.cpu_baseline else None
+    if samples is not None and nobj:
         cpu_sample = sb.buf.view(nobj, total, SS)[0, :, :L].cpu().numpy().view("uint32").copy()
+        samples["main"] = sb.sample(0x5A17)
 
     host = None
     want_host = rank == 0 and world == 1 and args.host_path
@@ -1393,15 +1501,23 @@ def main():
     for name in (x for x in args.shape_legs.split(",") if x):
         pn, pt, pm, ppg, _, _ = PRESETS[name]
         if (pn, pt, pm) != (need, total, args.object_mib):
-            shapes[name] = shape_leg(args, name, dev, rank, world, sb.buf)
+            shapes[name] = shape_leg(args, name, dev, rank, world, sb.buf, samples)
     sb.free()
-    bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj) if args.bytes_path else None
+    bytes_path = bytes_leg(args, dev, rank, need, total, erase, nobj, samples=samples, tag="object_bytes_path") \
+        if args.bytes_path else None
+    # BASELINE config 5's shape on the fused byte path, per GPU (its worst
+    # redo share: 26.8% of uniform 1 GiB objects switch to 1<<31).
+    c5n, c5t, c5m, _, _, c5e = PRESETS["c5"]
+    bytes_c5 = None
+    if args.c5_bytes and (need, total, args.object_mib) != (c5n, c5t, c5m):
+        bytes_c5 = bytes_leg(args, dev, rank, c5n, c5t, [int(x) for x in c5e.split(",")], 16, mib=c5m,
+                             samples=samples, tag="object_bytes_path_c5")
     if want_host and args.host_order == "after-free":
         host = run_host_leg()
     c5 = None
     is_c5 = (need, total, args.object_mib, args.global_objects) == (10, 14, 1024, 64)
     if args.c5_leg and not is_c5:
-        c5 = c5_leg(args, dev, rank, world)
+        c5 = c5_leg(args, dev, rank, world, samples)
 
     if rank == 0:
         line = {
@@ -1451,6 +1567,7 @@ def main():
             "c5_partitioned": c5,
             "shapes": shapes,
             "object_bytes_path": bytes_path,
+            "object_bytes_path_c5": bytes_c5,
             "allocator_probe": alloc_probe,
         }
         line["device"] = board_info(dev)
@@ -1460,12 +1577,33 @@ def main():
             line.setdefault("host_path", {})["pooled"] = pooled
         if cpu_sample is not None:
             line["cpu_baseline"] = cpu_baseline(cpu_sample, f"object 0 of this run's batch ({args.object_mib} MiB)",
-                                                need, total, erase, args.cpu_seconds)
+                                                need, total, erase, args.cpu_seconds, samples)
+            pin = line["cpu_baseline"]["oracle_pin"]
+            # `verified` = round trip of every leg AND, where the oracle ran,
+            # bit-exact vs the reference's arithmetic on every object.
+            line["verified_objects"] = {k: f"{v['verified_objects']}/{v['objects']}" for k, v in pin.items()}
+            line["verified_columns_per_object"] = ORACLE_COLS + 1
+            pinned_ok = all(v["verified_objects"] == v["objects"] for v in pin.values())
+            line["verified"] = line["verified"] and pinned_ok
+            for key, leg in (("shapes", None), ("c5_partitioned", "c5_partitioned"),
+                             ("object_bytes_path", "object_bytes_path"),
+                             ("object_bytes_path_c5", "object_bytes_path_c5")):
+                if key == "shapes":
+                    for nm, v in shapes.items():
+                        if nm in pin:
+                            v["verified_objects"] = pin[nm]["verified_objects"]
+                            v["verified"] = v["verified"] and pin[nm]["verified_objects"] == pin[nm]["objects"]
+                elif line.get(key) and leg in pin:
+                    line[key]["verified_objects"] = pin[leg]["verified_objects"]
+                    line[key]["verified"] = line[key]["verified"] and \
+                        pin[leg]["verified_objects"] == pin[leg]["objects"]
+            bad = bad or not pinned_ok
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if bad or (c5 is not None and not c5["verified"]) or not all(v["verified"] for v in shapes.values()) or \
-            (pooled is not None and not pooled["verified"]):
+            (pooled is not None and not pooled["verified"]) or (bytes_path is not None and not bytes_path["verified"]) or \
+            (bytes_c5 is not None and not bytes_c5["verified"]):
         sys.exit(3)
 
 

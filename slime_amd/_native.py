@@ -127,6 +127,9 @@ SIGNATURES = [
     ("slime_rs_encode_objects_chunked", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("slime_rs_encode_objects_phased", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("slime_rs_resolve_fallbacks_chunked", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_intp]),

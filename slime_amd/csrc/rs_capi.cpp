@@ -645,9 +645,9 @@ struct ScratchLease {
 }  // namespace
 extern "C" {
 
-extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
-                                               uint64_t chunk_stride, uint64_t object_size, uint64_t nobj,
-                                               uint32_t* mapping, uint32_t* status, void* stream) {
+extern "C" int slime_rs_encode_objects_phased(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                              uint64_t chunk_stride, uint64_t object_size, uint64_t nobj,
+                                              uint32_t* mapping, uint32_t* status, void* stream, void* phase_event) {
   if (nobj == 0) return 0;
   if (nobj > 0xFFFFFFFFull) return fail(Status::InvalidArg, "encode_objects: nobj exceeds 2^32-1");
   if (!mapping || !status) return fail(Status::InvalidArg, "encode_objects: null mapping/status");
@@ -671,6 +671,7 @@ extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* sl
   a0.sw = &sw;
   HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
+  if (phase_event) HIP_TRY(hipEventRecord((hipEvent_t)phase_event, s));
   BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 1, status, mapping);
   if (sw.switched) {
     a1.scratch = sc.ptr();
@@ -679,6 +680,13 @@ extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* sl
   HIP_TRY(launch_encode_bytes(a1, s));
   sc.release(s);
   return 0;
+}
+
+extern "C" int slime_rs_encode_objects_chunked(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,
+                                               uint64_t chunk_stride, uint64_t object_size, uint64_t nobj,
+                                               uint32_t* mapping, uint32_t* status, void* stream) {
+  return slime_rs_encode_objects_phased(plan, slots, slot_stride, chunk_stride, object_size, nobj, mapping, status,
+                                        stream, nullptr);
 }
 
 extern "C" int slime_rs_encode_objects(slime_rs_plan_t plan, uint8_t* slots, uint64_t slot_stride,

@@ -309,18 +309,25 @@ def _chunk_stride(L: int, chunk_stride: int) -> int:
 
 def encode_objects(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,
                    mapping: torch.Tensor, status: torch.Tensor, stream: Optional[torch.cuda.Stream] = None,
-                   chunk_stride: int = 0) -> None:
+                   chunk_stride: int = 0, phase_event: Optional[torch.cuda.Event] = None) -> None:
     """Device writeChunks: chunks of every object slot, gf.MapToGF's mapping per object.
-    Chunk c of a slot is at slot + c*chunk_stride (0: 4L, the object's bytes in place)."""
+    Chunk c of a slot is at slot + c*chunk_stride (0: 4L, the object's bytes in place).
+    phase_event (a recorded torch.cuda.Event) is recorded again on the stream
+    between the speculative pass and the 1<<31 re-encode."""
     L, _, _ = slot_geometry(object_size, plan.k, plan.k + plan.rows)
     dev = _check_slots(slots, slot_stride, nobj, _chunk_stride(L, chunk_stride) * (plan.k + plan.rows))
     for t in (mapping, status):
         if t.numel() < nobj or t.dtype not in (torch.int32, torch.uint32) or _dev_index(t) != dev:
             raise ValueError("mapping/status need nobj int32 words on the slots' device")
-    N.check(lib.slime_rs_encode_objects_chunked(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride,
-                                                chunk_stride, object_size, nobj,
-                                                ctypes.c_void_p(mapping.data_ptr()),
-                                                ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream)))
+    ev = None
+    if phase_event is not None:
+        if not phase_event.cuda_event:
+            raise ValueError("phase_event must have been recorded once (torch creates events lazily)")
+        ev = ctypes.c_void_p(phase_event.cuda_event)
+    N.check(lib.slime_rs_encode_objects_phased(plan._h, ctypes.c_void_p(slots.data_ptr()), slot_stride,
+                                               chunk_stride, object_size, nobj,
+                                               ctypes.c_void_p(mapping.data_ptr()),
+                                               ctypes.c_void_p(status.data_ptr()), _stream_handle(dev, stream), ev))
 
 
 def resolve_fallbacks(plan: Plan, slots: torch.Tensor, slot_stride: int, object_size: int, nobj: int,

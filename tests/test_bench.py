@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -146,15 +148,17 @@ def test_committed_traffic_matches_shipped_kernel_code():
     assert abs(tj["hbm_bytes_per_launch"] / alg - 1) < 0.01  # no wasted re-reads
 
 
-def test_committed_byte_traffic_matches_shipped_kernel_code():
-    """The byte path's PMC summary (profiles/r04/pmc_bytes.json, replayed into
-    object_bytes_path) covers C3 and C5 on 256 B chunk strides, was measured on
-    the machine code of every kernel it names, and its first pass and repair
-    move their algorithmic bytes 4L(k+r) / 4L(k+e)."""
+@pytest.mark.parametrize("rnd", ["r04", "r06"])
+def test_committed_byte_traffic_matches_shipped_kernel_code(rnd):
+    """The byte path's PMC summaries (profiles/r06/pmc_bytes.json, then r04's,
+    replayed into object_bytes_path and object_bytes_path_c5) cover C3 and C5
+    on 256 B chunk strides, were measured on the machine code of every kernel
+    they name, and their first pass and repair move their algorithmic bytes
+    4L(k+r) / 4L(k+e)."""
     import sys
     sys.path.insert(0, ROOT)
     from slime_amd.codeobj import kernel_code_id
-    entries = json.load(open(os.path.join(ROOT, "profiles", "r04", "pmc_bytes.json")))
+    entries = json.load(open(os.path.join(ROOT, "profiles", rnd, "pmc_bytes.json")))
     lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
     shapes = {"8/12 S=268435456 nobj=128 cs=33554432": (8, 12, 8388608, 128),
               "10/14 S=1073741824 nobj=16 cs=107374336": (10, 14, 26843546, 16)}
@@ -284,3 +288,48 @@ def test_committed_traffic_per_shape_matches_shipped_kernel_code():
         assert e["kernel"] == "rs_apply_queue_kernel"
         assert e["kernel_code"] == kernel_code_id(lib, (f"rs_apply_queue_kernelILi{need}E",)), e["config"]
         assert abs(e["hbm_bytes_per_launch"] / (nobj * 4 * L * total) - 1) < 0.01, e["config"]
+
+
+def test_oracle_pin_counts_every_object_and_catches_one_bad_word():
+    """bench.py's oracle pin: column_sample gathers a seeded
+    window plus the last column of every object; oracle_pin re-encodes each
+    object's sampled data columns with the oracle and recovers them from the
+    survivors.  A batch the oracle itself encoded pins every object, in the
+    symbol domain and in the byte domain (big-endian words XOR the mapping);
+    one flipped parity word, or one flipped rebuilt data word, fails exactly
+    that object."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, ROOT)
+    from oracle import oracle_c as OC
+    bench = _load("bench.py", "bench_mod_pin")
+    need, total, L, SS, nobj = 4, 6, 9000, 9024, 5
+    erase = [0, 1]
+    have = [i for i in range(total) if i not in erase][:need]
+    rng = np.random.default_rng(7)
+    buf = np.zeros((nobj, total, SS), dtype=np.uint32)
+    for o in range(nobj):
+        sh = np.zeros((total, L), dtype=np.uint32)
+        sh[:need] = rng.integers(0, 2**32 - 5, size=(need, L), dtype=np.uint32)
+        OC.encode_object(sh, need, total)
+        buf[o, :, :L] = sh
+    v3 = torch.from_numpy(buf.view(np.int32))
+    smp = bench.column_sample(v3, L, 11, ncols=1024)
+    assert smp["cols"].shape == (nobj, total, 1025) and smp["window"] == 1024
+    for o in range(nobj):  # the window at its offset, then column L-1
+        off = smp["offsets"][o]
+        assert np.array_equal(smp["cols"][o, :, :1024], buf[o, :, off:off + 1024])
+        assert np.array_equal(smp["cols"][o, :, 1024], buf[o, :, L - 1])
+    smp.update(need=need, total=total, have=have)
+    pin = bench.oracle_pin({"sym": smp})
+    assert pin["sym"]["verified_objects"] == nobj and pin["sym"]["columns_per_object"] == 1025
+    bad = dict(smp, cols=smp["cols"].copy())
+    bad["cols"][2, need, 17] ^= 1          # a parity word of object 2
+    bad["cols"][4, erase[1], 1024] ^= 4    # a rebuilt data word of object 4 (the last column)
+    assert bench.oracle_pin({"sym": bad})["sym"]["verified_objects"] == nobj - 2
+    # byte domain: slot words are big-endian bytes of symbol ^ mapping
+    ms = np.array([0, 1 << 31, 0x12345, 0, 1 << 31], dtype=np.uint32)
+    wire = (smp["cols"] ^ ms[:, None, None]).byteswap()
+    pin = bench.oracle_pin({"b": dict(smp, cols=wire, mapping=ms)})
+    assert pin["b"]["verified_objects"] == nobj and pin["b"]["domain"] == "bytes"
+    assert bench.oracle_pin({"b": dict(smp, cols=wire, mapping=ms ^ np.uint32(1))})["b"]["verified_objects"] == 0

@@ -713,6 +713,46 @@ def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
         assert (h[o * stride + total * chunk: (o + 1) * stride] == 0xA5).all(), "wrote past the chunks"
 
 
+@pytest.mark.parametrize("need,total", [(8, 12), (10, 14), (40, 56)])
+def test_encode_objects_phased_event_splits_the_passes(torch_dev, need, total):
+    """slime_rs_encode_objects_phased (bench.py's redo share): the same chunks
+    as the plain call, byte for byte, with objects that switch to 1<<31; the
+    event it records lies between the call's start and end on the stream, so
+    pass 0 + redo = the whole encode."""
+    torch = torch_dev
+    from slime_amd import device as D
+    rng = np.random.default_rng(need)
+    S, nobj = (4 << 20) + 4, 8
+    objs = []
+    for o in range(nobj):
+        b = bytearray(rng.integers(0, 256, size=S, dtype=np.uint8).tobytes())
+        if o % 2:
+            b[4 * (o * 1000): 4 * (o * 1000) + 4] = b"\xff\xff\xff\xfd"
+        objs.append(bytes(b))
+    plan = D.Plan.encode(need, total)
+    outs = []
+    for phased in (False, True):
+        slots, L, chunk, stride = _make_slots(torch, objs, need, total)
+        mapping = torch.empty(nobj, dtype=torch.int32, device="cuda")
+        status = torch.empty(nobj, dtype=torch.int32, device="cuda")
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[1].record()
+        ev[0].record()
+        D.encode_objects(plan, slots, stride, S, nobj, mapping, status, phase_event=ev[1] if phased else None)
+        ev[2].record()
+        torch.cuda.synchronize()
+        assert status.cpu().numpy().tolist() == [0] * nobj
+        if phased:
+            a, b = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+            assert a > 0 and b > 0 and abs(a + b - ev[0].elapsed_time(ev[2])) < 1e-3
+        outs.append((slots.cpu().numpy(), mapping.cpu().numpy().view(np.uint32)))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert (outs[1][1][1::2] == 1 << 31).all()
+    with pytest.raises(ValueError):
+        D.encode_objects(plan, slots, stride, S, nobj, mapping, status,
+                         phase_event=torch.cuda.Event(enable_timing=True))  # never recorded: no handle yet
+
+
 def test_encode_objects_random_fallback(torch_dev):
     torch = torch_dev
     from slime_amd import device as D

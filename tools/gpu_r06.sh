@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs= --pooled 0"
+NOLEGS="--cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --c5-bytes 0 --shape-legs= --pooled 0"
 
 run() {  # run <name> <limit-seconds> <command...>
   local name=$1 lim=$2; shift 2
@@ -50,6 +50,9 @@ for step in "$@"; do
     hostonly) run hostonly 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
     pmc_c3) pmc pmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
             pmc pmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
+    tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
+    bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
+             pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;
     bpmc_c5) pmc bpmc_c5_fetch FETCH_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c5_write WRITE_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
