@@ -88,6 +88,10 @@ tools/libubench.so: tools/ubench.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: ubench
 
+# Stamped twin of the product's queue apply launch (tools only): make tools/libc2stamps.so
+tools/libc2stamps.so: tools/c2_stamps.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
 # Apply-kernel variant harness (tools only): make applyvar
 applyvar: tools/libapplyvar.so
 tools/libapplyvar.so: tools/apply_variants.hip $(HDRS)

@@ -116,23 +116,27 @@ int map_buffer(int device, uint64_t bytes, uint64_t chunk, void** va_out, DevBuf
 // "Placement modes"); the buffer's contents are garbage either way.
 double placement_probe(int device, uint8_t* va, uint64_t bytes) {
   constexpr uint32_t kNeed = 8, kTotal = 12, kRows = kTotal - kNeed, kObj = 128;
-  const uint64_t L = (bytes / 4 / kTotal / kObj) & ~(uint64_t)63;
+  // The coefficient / index table goes in the buffer's last 4 KiB, past the
+  // objects: no allocation (a hipMalloc / hipFree pair synchronises the
+  // device, and is not allowed while another thread captures a graph).
+  constexpr uint64_t kTableRoom = 4096;
+  if (bytes < 2 * kTableRoom) return 0;
+  const uint64_t L = ((bytes - kTableRoom) / 4 / kTotal / kObj) & ~(uint64_t)63;
   if (L < 65536) return 0;
   std::vector<uint32_t> table(kRows * 16 + 16, 0);
   for (uint32_t i = 0; i < kRows; ++i)
     for (uint32_t j = 0; j < kNeed; ++j) table[i * 16 + j] = 0x9E3779B9u * (i * kNeed + j + 1) % kP;
   for (uint32_t j = 0; j < kNeed; ++j) table[kRows * 16 + j] = j;
   for (uint32_t i = 0; i < kRows; ++i) table[kRows * 16 + 8 + i] = kNeed + i;
-  uint32_t* d = nullptr;
-  if (hipMalloc((void**)&d, table.size() * 4) != hipSuccess) return 0;
+  uint32_t* const d = (uint32_t*)(va + bytes - kTableRoom);
   hipStream_t s = nullptr;
   hipEvent_t ev[3] = {};
   double best = 0;
   // Everything on a private non-blocking stream, waited for there only: no
   // other stream (torch's, or a capture in progress on another thread) is
-  // synchronised.
-  bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-            hipMemcpyAsync(d, table.data(), table.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess;
+  // synchronised, and nothing is allocated or freed.
+  const bool made = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  bool ok = made && hipMemcpyAsync(d, table.data(), table.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess;
   for (auto& e : ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   if (ok) {
     ApplyLaunch a;
@@ -160,10 +164,10 @@ double placement_probe(int device, uint8_t* va, uint64_t bytes) {
     }
   }
   if (!ok) (void)hipGetLastError();
+  if (made) (void)hipStreamSynchronize(s);  // the table upload reads `table`: done before it goes
   for (auto& e : ev)
     if (e) (void)hipEventDestroy(e);
   if (s) (void)hipStreamDestroy(s);
-  (void)hipFree(d);
   return best;
 }
 }  // namespace

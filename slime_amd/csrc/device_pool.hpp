@@ -90,9 +90,13 @@ struct PoolLease {
       p.calls[device].fetch_add(1, std::memory_order_relaxed);
     }
   }
-  ~PoolLease() {
+  // The call no longer counts as in flight on its device (idempotent; the
+  // destructor calls it too).
+  void release() {
     if (counted) pool->inflight[device].fetch_sub(1, std::memory_order_relaxed);
+    counted = false;
   }
+  ~PoolLease() { release(); }
 };
 
 // Per-device free list of reusable per-call resources (T has an int `device`

@@ -519,15 +519,20 @@ struct TicketWalk {
   // Once per wave, after the walk ended (live == false): count the wave out;
   // the launch's last wave returns the set to zero (see kTicketStride).
   // Zeroed with atomics, which execute at the memory side like the draws.
-  __device__ __forceinline__ void finish() {
+  __device__ __forceinline__ void finish() { (void)finish_last(); }
+  // finish(), telling lane 0 of the launch's last wave out (stamped harness).
+  __device__ __forceinline__ bool finish_last() {
+    bool last = false;
     if (lane == 0) {
       uint32_t* const done = ticket + NC * kTicketStride;
       if (atomicAdd(done, 1u) == gridDim.x * gridDim.y * (blockDim.x >> 6) - 1) {
+        last = true;
 #pragma unroll
         for (int q = 0; q < NC; ++q) atomicExch(ticket + q * kTicketStride, 0u);
         atomicExch(done, 0u);
       }
     }
+    return last;
   }
 };
 
@@ -582,19 +587,30 @@ struct ListWalk {
   }
 };
 
-// Tuning-harness knobs (the product uses TB = 1, STAMP = false): TB tickets
-// per atomic (a wave takes TB consecutive units at a time); STAMP records per
-// wave {start, end, XCD | tiles << 32} (s_memrealtime ticks) into `stamps`.
-template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, bool STAMP = false, bool SYNC = false>
+// STAMP 2: the time a wave enters its 4th, 16th and 64th tile (0 if never).
+__device__ __forceinline__ void stamp_milestone(uint32_t walked, uint64_t (&t_at)[3]) {
+  if (walked == 4 || walked == 16 || walked == 64) t_at[walked == 4 ? 0 : walked == 16 ? 1 : 2] =
+      __builtin_amdgcn_s_memrealtime();
+}
+
+// Tuning-harness knobs (the product uses TB = 1, STAMP = 0): TB tickets per
+// atomic (a wave takes TB consecutive units at a time); STAMP 1 records per
+// wave {start, end, XCD | tiles << 32} (s_memrealtime ticks, 100 MHz) into
+// `stamps`; STAMP 2 records 8 words {start, first tile's loads issued, tile
+// 4 entered, tile 16 entered, tile 64 entered, last tile's stores issued,
+// those stores retired (s_waitcnt 0), exit counted (finish)} and a ninth,
+// XCD | tiles << 32 | last-out flag << 40 -- the launch's fixed costs apart
+// (tools/c2_stamps.py).
+template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, int STAMP = 0, bool SYNC = false>
 __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
     const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t in_obj_stride, uint64_t in_shard,
     uint64_t out_obj_stride, uint64_t out_shard, const uint32_t* __restrict__ coeff,
     const uint32_t* __restrict__ in_idx, const uint32_t* __restrict__ out_idx, uint64_t ncols, uint32_t nobj,
     uint32_t rows, uint32_t k, uint32_t* __restrict__ ticket, uint64_t* __restrict__ stamps, uint32_t spread) {
   static_assert(K > 0 && NC > 0 && NC <= 64 && TB >= 1, "compile-time k only");
-  uint64_t t_start = 0;
+  uint64_t t_start = 0, t_walk = 0, t_issued = 0, t_retired = 0, t_at[3] = {0, 0, 0};
   uint32_t walked = 0;
-  if constexpr (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
+  if constexpr (STAMP > 0) t_start = __builtin_amdgcn_s_memrealtime();
   // Host guarantees: ncols < 2^30 (32-bit byte offsets), nobj * 4 * groups < 2^32.
   const uint32_t nvec = (uint32_t)(ncols >> 2);
   const uint32_t ntiles = (nvec + 64 * U - 1) / (64 * U);
@@ -617,9 +633,11 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
   if (w.live) {
     uint4 xa[U][K], xb[U][K];
     load(xa, w.obj, w.tile());
+    if constexpr (STAMP > 1) t_walk = __builtin_amdgcn_s_memrealtime();
     for (;;) {
       uint32_t co = w.obj, ct = w.tile();
-      if constexpr (STAMP) ++walked;
+      if constexpr (STAMP > 0) ++walked;
+      if constexpr (STAMP > 1) stamp_milestone(walked, t_at);
       w.advance();
       // Past the last unit the prefetch re-reads the current tile (unconditional loads, see load_tile).
       load(xb, w.live ? w.obj : co, w.live ? w.tile() : ct);
@@ -627,21 +645,48 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
       if (!w.live) break;
       co = w.obj;
       ct = w.tile();
-      if constexpr (STAMP) ++walked;
+      if constexpr (STAMP > 0) ++walked;
+      if constexpr (STAMP > 1) stamp_milestone(walked, t_at);
       w.advance();
       load(xa, w.live ? w.obj : co, w.live ? w.tile() : ct);
       store(xb, co, ct);
       if (!w.live) break;
     }
   }
-  w.finish();
-  if constexpr (STAMP) {
+  if constexpr (STAMP > 1) {
+    t_issued = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0);  // every load and store of the walk retired
+    t_retired = __builtin_amdgcn_s_memrealtime();
+  }
+  bool last_out = false;
+  if constexpr (STAMP > 1) {
+    last_out = w.finish_last();
+  } else {
+    w.finish();
+  }
+  if constexpr (STAMP == 1) {
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
       uint64_t* r = stamps + 3 * ((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6));
       r[0] = t_start;
       r[1] = t_end;
       r[2] = hw_xcc_id() | ((uint64_t)walked << 32);
+    }
+  }
+  if constexpr (STAMP > 1) {
+    __builtin_amdgcn_s_waitcnt(0);  // the exit count (and, last out, the counter reset) retired
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      uint64_t* r = stamps + 9 * ((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6));
+      r[0] = t_start;
+      r[1] = t_walk ? t_walk : t_start;
+      r[2] = t_at[0];
+      r[3] = t_at[1];
+      r[4] = t_at[2];
+      r[5] = t_issued;
+      r[6] = t_retired;
+      r[7] = t_end;
+      r[8] = hw_xcc_id() | ((uint64_t)walked << 32) | ((uint64_t)last_out << 40);
     }
   }
   // Columns past the last whole vector of each object, one per lane.

@@ -130,6 +130,10 @@ int DeviceLease::acquire() {
 }
 
 DeviceLease::~DeviceLease() {
+  // Out of the device's in-flight count first, then the host-call slot: the
+  // waiter the slot wakes routes by in-flight counts that no longer include
+  // this finished call.
+  lease.release();
   if (slot_) host_slots().leave();
 }
 

@@ -1,0 +1,47 @@
+// Stamped twin of the product's dynamic-schedule apply launch (rs_apply.hip
+// launch_queue): the same kernel template, geometry, spread and block count,
+// instantiated with STAMP = 2 (rs_apply_kernel.hpp), so each wave records
+// {start, first loads issued, tiles 4 / 16 / 64 entered, last stores issued,
+// stores retired, exit counted, XCD | tiles | last-out}.  tools/c2_stamps.py splits a launch's
+// fixed cost with it.  Tools only.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+#include "rs_apply_kernel.hpp"
+
+using namespace slime;
+using namespace slime::apply;
+
+namespace {
+template <int K, int U, int C>
+int launch(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os,
+           const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows,
+           hipStream_t s, uint32_t* ticket, uint64_t* stamps, uint32_t* nwaves) {
+  const uint32_t spread = queue_spread(nobj, ncols, U, C);
+  if (!spread) return -2;
+  const uint64_t blocks = queue_blocks(256, queue_units(nobj, ncols, U, C, spread));
+  *nwaves = (uint32_t)blocks * kWaves;
+  if (!stamps) return 0;  // the caller sizes the stamp buffer first
+  hipLaunchKernelGGL((rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true, 1, 2>), dim3((uint32_t)blocks),
+                     dim3(kBlock), 0, s, in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, (uint32_t)K, ticket,
+                     stamps, spread);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+}  // namespace
+
+// k = 4 (C2: U 4, C 2) or 8 (C3: U 3, C 2), the product's queue geometry.
+// ticket: a zeroed counter set of kQueueCounters + 1 lines of 64 words (each
+// launch leaves it zero).  stamps: 9 words per wave, or null to get the wave
+// count only (*nwaves).
+extern "C" int cs_launch(int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os,
+                         const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj,
+                         uint32_t rows, void* stream, void* ticket, void* stamps, uint32_t* nwaves) {
+  hipStream_t s = (hipStream_t)stream;
+  if (k == 4)
+    return launch<4, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves);
+  if (k == 8)
+    return launch<8, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves);
+  return -1;
+}

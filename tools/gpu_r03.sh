@@ -2,6 +2,9 @@
 # Round-3 GPU-box session: every GPU step under its own time limit; the first
 # crash/abort/timeout ends the session (nothing more runs on the GPU).
 # Usage (repo root, on the box):  bash tools/gpu_r03.sh <step> [<step>...]
+# NOTE (round 6): the A/B environment variables these steps set -- SLIME_RS_MFMA*, SLIME_RS_QUEUE,
+# SLIME_RS_PIPE, SLIME_RS_GRID_TARGET, SLIME_RS_SEGMENTS, SLIME_RS_HOST_PIPE -- were removed from the
+# library in round 5 and now do nothing: re-running a step does not reproduce its A/B.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out

@@ -55,6 +55,11 @@ for step in "$@"; do
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;
     bpmc_c5) pmc bpmc_c5_fetch FETCH_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c5_write WRITE_SIZE --preset c5 --global-objects 16 --steps 3 --warmup 1 $NOLEGS ;;
+    # C2's fixed cost per launch split by per-wave stamps, and the same under a kernel trace
+    stamps) run stamps_c2 300 python tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32,64,128 &&
+            run stamps_c3 300 python tools/c2_stamps.py --need 8 --total 12 --mib 256 --nobj 32,64,128 --reps 6 &&
+            run stamps_c2_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/stamps_c2_prof" -o st --output-format csv -- \
+              python3 tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32,64,128 ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done

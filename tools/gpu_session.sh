@@ -5,6 +5,9 @@
 # Every GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or
 # a signal) ends the session immediately.  A plain test failure (exit 1) is
 # recorded and the session continues.
+# NOTE (round 6): the A/B environment variables some steps set -- SLIME_RS_QUEUE, SLIME_RS_PIPE,
+# SLIME_RS_GRID_TARGET, SLIME_RS_SEGMENTS -- were removed from the library in round 5 and now do
+# nothing: re-running such a step does not reproduce its A/B.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
