@@ -114,7 +114,7 @@ def parse(argv=None):
                     help="device shard stride rounded up to this many symbols (64 = 256 B: every shard "
                          "starts on a cache-line boundary; 1 = packed, stride L)")
     ap.add_argument("--traffic", type=str,
-                    default=",".join(os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r05", "r04")),
+                    default=",".join(os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r06", "r05", "r04")),
                     help="PMC-derived HBM bytes per launch, comma-separated files (tools/pmc_traffic.py over "
                          "rocprofv3 --pmc passes; an entry is used only when its config and the kernel's machine "
                          "code match this build)")

@@ -151,7 +151,7 @@ hipError_t launch_queue(const ApplyLaunch& a, hipStream_t stream, bool* launched
   constexpr int U = queue_unroll<K>();
   constexpr int C = queue_unit_tiles<K>();
   *launched = false;
-  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
+  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C, (uint32_t)(a.k + a.rows));
   if (!spread) return hipSuccess;
   const uint64_t blocks = queue_blocks(kQueueBlocks, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(

@@ -26,7 +26,7 @@ hipError_t launch_k32_queue(const ApplyLaunch& a, hipStream_t stream, bool* laun
   constexpr int U = K <= 24 ? 2 : 1;
   constexpr int C = 6 / U;
   *launched = false;
-  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C);
+  const uint32_t spread = queue_spread(a.nobj, a.ncols, U, C, (uint32_t)(a.k + a.rows));
   if (!spread) return hipSuccess;
   const uint64_t blocks = queue_blocks(256, queue_units(a.nobj, a.ncols, U, C, spread));
   return with_tickets(

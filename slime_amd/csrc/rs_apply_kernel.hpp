@@ -599,7 +599,7 @@ __device__ __forceinline__ void stamp_milestone(uint32_t walked, uint64_t (&t_at
 // `stamps`; STAMP 2 records 8 words {start, first tile's loads issued, tile
 // 4 entered, tile 16 entered, tile 64 entered, last tile's stores issued,
 // those stores retired (s_waitcnt 0), exit counted (finish)} and a ninth,
-// XCD | tiles << 32 | last-out flag << 40 -- the launch's fixed costs apart
+// XCD | tiles << 32 | last-out flag << 63 -- the launch's fixed costs apart
 // (tools/c2_stamps.py).
 template <int K, int U, int C, int NC, bool NTL, bool NTS, int TB = 1, int STAMP = 0, bool SYNC = false>
 __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(kBlock) void rs_apply_queue_kernel(
       r[5] = t_issued;
       r[6] = t_retired;
       r[7] = t_end;
-      r[8] = hw_xcc_id() | ((uint64_t)walked << 32) | ((uint64_t)last_out << 40);
+      r[8] = hw_xcc_id() | ((uint64_t)walked << 32) | ((uint64_t)last_out << 63);
     }
   }
   // Columns past the last whole vector of each object, one per lane.

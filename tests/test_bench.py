@@ -270,15 +270,18 @@ def test_proxy_load_fails_loudly_without_a_gpu():
         assert rc == 10 and out[2] == 0.0 and out[8] > 0
 
 
-def test_committed_traffic_per_shape_matches_shipped_kernel_code():
-    """profiles/r05/pmc_traffic.json holds one PMC summary per BASELINE shape
-    the line reports (C3, C2, the north star's 64 MiB shards); each was
-    measured on the machine code the built library runs, and each moves its
-    algorithmic bytes 4L(k+r) per launch to within 1%."""
+@pytest.mark.parametrize("rnd", ["r05", "r06"])
+def test_committed_traffic_per_shape_matches_shipped_kernel_code(rnd):
+    """profiles/r06/pmc_traffic.json (and r05's) holds one PMC summary per
+    BASELINE shape the line reports (C3, C2, the north star's 64 MiB shards);
+    each was measured on the machine code the built library runs, and each
+    moves its algorithmic bytes 4L(k+r) per launch to within 1%.  r06's C2
+    entry is the pass after the narrow-code spread rule (8 segments per object
+    at 32 objects)."""
     import sys
     sys.path.insert(0, ROOT)
     from slime_amd.codeobj import kernel_code_id
-    entries = json.load(open(os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json")))
+    entries = json.load(open(os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")))
     lib = os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so")
     shapes = {"8/12 L=8388608 nobj=128": (8, 12, 8388608, 128), "4/6 L=4194304 nobj=32": (4, 6, 4194304, 32),
               "8/12 L=16777216 nobj=64": (8, 12, 16777216, 64)}

@@ -16,10 +16,11 @@ namespace {
 template <int K, int U, int C>
 int launch(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os,
            const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj, uint32_t rows,
-           hipStream_t s, uint32_t* ticket, uint64_t* stamps, uint32_t* nwaves) {
-  const uint32_t spread = queue_spread(nobj, ncols, U, C);
+           hipStream_t s, uint32_t* ticket, uint64_t* stamps, uint32_t* nwaves, uint32_t spread_override,
+           uint32_t blocks_override) {
+  const uint32_t spread = spread_override ? spread_override : queue_spread(nobj, ncols, U, C, K + rows);
   if (!spread) return -2;
-  const uint64_t blocks = queue_blocks(256, queue_units(nobj, ncols, U, C, spread));
+  const uint64_t blocks = blocks_override ? blocks_override : queue_blocks(256, queue_units(nobj, ncols, U, C, spread));
   *nwaves = (uint32_t)blocks * kWaves;
   if (!stamps) return 0;  // the caller sizes the stamp buffer first
   hipLaunchKernelGGL((rs_apply_queue_kernel<K, U, C, kQueueCounters, true, true, 1, 2>), dim3((uint32_t)blocks),
@@ -29,19 +30,24 @@ int launch(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t
 }
 }  // namespace
 
-// k = 4 (C2: U 4, C 2) or 8 (C3: U 3, C 2), the product's queue geometry.
+// k = 4 (C2: U 4, C 2), 8 (C3: U 3, C 2) or 10 (C5: U 3, C 2), the product's queue geometry.
 // ticket: a zeroed counter set of kQueueCounters + 1 lines of 64 words (each
 // launch leaves it zero).  stamps: 9 words per wave, or null to get the wave
-// count only (*nwaves).
+// count only (*nwaves).  spread / blocks: 0 = the product's rule, else that
+// many segments per object / blocks (A/B of the geometry).
 extern "C" int cs_launch(int k, const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t oo, uint64_t os,
                          const uint32_t* coeff, const uint32_t* ii, const uint32_t* oi, uint64_t ncols, uint32_t nobj,
-                         uint32_t rows, void* stream, void* ticket, void* stamps, uint32_t* nwaves) {
+                         uint32_t rows, void* stream, void* ticket, void* stamps, uint32_t* nwaves, uint32_t spread,
+                         uint32_t blocks) {
   hipStream_t s = (hipStream_t)stream;
   if (k == 4)
     return launch<4, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
-                           (uint64_t*)stamps, nwaves);
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 10)
+    return launch<10, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                            (uint64_t*)stamps, nwaves, spread, blocks);
   if (k == 8)
     return launch<8, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
-                           (uint64_t*)stamps, nwaves);
+                           (uint64_t*)stamps, nwaves, spread, blocks);
   return -1;
 }

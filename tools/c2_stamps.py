@@ -55,8 +55,8 @@ def fit(xs, ys):
 def analyse(rec: np.ndarray, event_ms: float) -> dict:
     t0, tw, t4, t16, t64, ti, tr, te = (rec[:, i].astype(np.float64) for i in range(8))
     meta = rec[:, 8].astype(np.uint64)
-    tiles = ((meta >> np.uint64(32)) & np.uint64(0xFF)).astype(np.int64)
-    last = ((meta >> np.uint64(40)) & np.uint64(1)).astype(bool)
+    tiles = ((meta >> np.uint64(32)) & np.uint64(0x7FFFFFFF)).astype(np.int64)
+    last = (meta >> np.uint64(63)).astype(bool)
     base = t0.min()
     us = lambda v: round(float(v) * TICK_US, 2)  # noqa: E731
     span = te.max() - base
@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--nobj", type=str, default="32,64,128")
     ap.add_argument("--reps", type=int, default=12)
+    ap.add_argument("--geometry", type=str, default="0:0",
+                    help="stamped twin geometries spread:blocks (0 = the product's rule), comma list; the split is "
+                         "reported for the first")
     args = ap.parse_args()
     need, total = args.need, args.total
     r = total - need
@@ -103,7 +106,7 @@ def main():
     lib.cs_launch.restype = ctypes.c_int
     lib.cs_launch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p] * 3 + \
         [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-         ctypes.POINTER(ctypes.c_uint32)]
+         ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_uint32]
     L = -(-(args.mib << 20) // 4 // need)
     SS = -(-L // 64) * 64  # the bench's line-aligned shard stride
     counts = [int(x) for x in args.nobj.split(",")]
@@ -129,17 +132,24 @@ def main():
             enc(b, lay, b, lay, L, nobj, stream=s, dst_offset=need * SS)
 
         nw = ctypes.c_uint32(0)
-        rc = lib.cs_launch(need, b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
-                           ii.data_ptr(), oi.data_ptr(), L, nobj, r, ctypes.c_void_p(s.cuda_stream),
-                           ticket.data_ptr(), None, ctypes.byref(nw))
-        assert rc == 0, rc
-        st = torch.zeros(nw.value * 9, dtype=torch.int64, device="cuda")
-
-        def stamped():
+        geos = [tuple(int(v) for v in g.split(":")) for g in args.geometry.split(",")]
+        nws = {}
+        for g in geos:
             rc = lib.cs_launch(need, b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
                                ii.data_ptr(), oi.data_ptr(), L, nobj, r, ctypes.c_void_p(s.cuda_stream),
-                               ticket.data_ptr(), st.data_ptr(), ctypes.byref(nw))
+                               ticket.data_ptr(), None, ctypes.byref(nw), g[0], g[1])
             assert rc == 0, rc
+            nws[g] = nw.value
+        st = torch.zeros(max(nws.values()) * 9, dtype=torch.int64, device="cuda")
+
+        def stamped_at(g):
+            def fn():
+                rc = lib.cs_launch(need, b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
+                                   ii.data_ptr(), oi.data_ptr(), L, nobj, r, ctypes.c_void_p(s.cuda_stream),
+                                   ticket.data_ptr(), st.data_ptr(), ctypes.byref(nw), g[0], g[1])
+                assert rc == 0, rc
+            return fn
+        stamped = stamped_at(geos[0])
 
         product()
         torch.cuda.synchronize()
@@ -148,19 +158,23 @@ def main():
         # launches enqueued without a host wait, so an interval is GPU time
         # from one launch's start to the next's (the gap between kernels
         # included), never the host's enqueue latency.
-        times, recs = {}, []
-        for name, fn in (("product", product), ("stamped", stamped), ("product2", product)):
+        times, recs, good = {}, [], True
+        runs = [("product", product), ("stamped", stamped)] + \
+            [(f"stamped_{g[0]}:{g[1]}", stamped_at(g)) for g in geos[1:]] + [("product2", product)]
+        for name, fn in runs:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
             ev[0].record(s)
             for i in range(args.reps):
                 fn()
                 ev[i + 1].record(s)
             torch.cuda.synchronize()
+            good = good and bool(torch.equal(par(), want))  # every variant writes the product's parity
+            par().zero_()
             times[name] = [ev[i].elapsed_time(ev[i + 1]) for i in range(1, args.reps)]  # the first one warms
             if name == "stamped":
-                recs.append((times[name][-1], st.view(nw.value, 9).cpu().numpy().copy()))
+                recs.append((times[name][-1], st.view(-1, 9)[: nws[geos[0]]].cpu().numpy().copy()))
         times["product"] += times.pop("product2")
-        ok = bool(torch.equal(par(), want))
+        ok = good
         med = {k: statistics.median(v) for k, v in times.items()}
         # the stamped launch nearest its median time
         ms, rec = recs[0]  # the last stamped launch of its back-to-back run
@@ -169,6 +183,8 @@ def main():
         res["batches"][str(nobj)] = {
             "product_ms": round(med["product"], 4), "stamped_ms": round(med["stamped"], 4),
             "product_frac": round(alg / (med["product"] * 1e-3) / 8e12, 4), "stamped_matches_product": ok,
+            "geometries": {k: {"ms": round(v, 4), "frac": round(alg / (v * 1e-3) / 8e12, 4)}
+                           for k, v in med.items() if k.startswith("stamped")},
             "split": a}
         ev_fit.append(med["product"] * 1e3)
         span_fit.append(a["wave_span_us"])

@@ -50,6 +50,8 @@ for step in "$@"; do
     hostonly) run hostonly 400 python bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
     pmc_c3) pmc pmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
             pmc pmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
+    pmc_c2) pmc pmc_c2_fetch FETCH_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
+            pmc pmc_c2_write WRITE_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
     tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
     bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;
@@ -60,6 +62,30 @@ for step in "$@"; do
             run stamps_c3 300 python tools/c2_stamps.py --need 8 --total 12 --mib 256 --nobj 32,64,128 --reps 6 &&
             run stamps_c2_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/stamps_c2_prof" -o st --output-format csv -- \
               python3 tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32,64,128 ;;
+    # C2 geometry A/B on the stamped twin: segments per object x blocks
+    c2geo) run c2geo 300 python tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32 --reps 16 \
+             --geometry 0:0,1:256,2:256,4:256,8:256,2:512,4:512,1:512 &&
+           run c2geo_c3 300 python tools/c2_stamps.py --need 8 --total 12 --mib 256 --nobj 128 --reps 6 \
+             --geometry 0:0,2:256,1:512 ;;
+    # segments per object (TicketWalk spread) across the BASELINE shapes, on the stamped twin
+    spreadsweep) C="python tools/c2_stamps.py"
+      run ss_c2_32 300 $C --need 4 --total 6 --mib 64 --nobj 32 --reps 16 --geometry 0:0,4:0,8:0,16:0,32:0 &&
+      run ss_c2_64 300 $C --need 4 --total 6 --mib 64 --nobj 64 --reps 12 --geometry 0:0,2:0,4:0,8:0 &&
+      run ss_c2_128 300 $C --need 4 --total 6 --mib 64 --nobj 128 --reps 8 --geometry 0:0,2:0,4:0 &&
+      run ss_c3_128 300 $C --need 8 --total 12 --mib 256 --nobj 128 --reps 6 --geometry 0:0,2:0,4:0 &&
+      run ss_c3_32 300 $C --need 8 --total 12 --mib 256 --nobj 32 --reps 8 --geometry 0:0,4:0,8:0,16:0 &&
+      run ss_ns64 300 $C --need 8 --total 12 --mib 512 --nobj 64 --reps 6 --geometry 0:0,2:0,4:0,8:0 &&
+      run ss_c5_64 300 $C --need 10 --total 14 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0,4:0 &&
+      run ss_c5_16 300 $C --need 10 --total 14 --mib 1024 --nobj 16 --reps 6 --geometry 0:0,8:0,16:0,32:0 ;;
+    spreadsweep2) C="python tools/c2_stamps.py"
+      for rep in 1 2; do
+        run ss2_c2_32_$rep 300 $C --need 4 --total 6 --mib 64 --nobj 32 --reps 20 --geometry 0:0,8:0,16:0,2:0,4:0 &&
+        run ss2_c2_64_$rep 300 $C --need 4 --total 6 --mib 64 --nobj 64 --reps 12 --geometry 0:0,4:0,2:0 &&
+        run ss2_c3_32_$rep 300 $C --need 8 --total 12 --mib 256 --nobj 32 --reps 10 --geometry 0:0,8:0,4:0 &&
+        run ss2_c3_128_$rep 300 $C --need 8 --total 12 --mib 256 --nobj 128 --reps 6 --geometry 0:0,2:0 &&
+        run ss2_c5_64_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0 &&
+        run ss2_c5_8_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 8 --reps 8 --geometry 0:0,16:0,4:0,32:0 || exit 1
+      done ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
