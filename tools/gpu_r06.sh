@@ -86,6 +86,13 @@ for step in "$@"; do
         run ss2_c5_64_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0 &&
         run ss2_c5_8_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 8 --reps 8 --geometry 0:0,16:0,4:0,32:0 || exit 1
       done ;;
+    # the driver's command under the profiler, without the pooled leg (the profiler's own fault, s1_segv)
+    profdrv) run profdrv 700 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 --pooled 0 &&
+            python tools/prof_summary.py "$OUT/prof" > "$OUT/prof_summary.json" ;;
+    rehearse2) run rehearse2 500 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --cpu-baseline 0 --alloc-probe 0 &&
+               run rehearse2_torchrun 500 env SLIME_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --cpu-baseline 0 --alloc-probe 0 ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
