@@ -539,7 +539,8 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                             0x5A3D + need)
         smp.update(need=need, total=total, have=have, mapping=ms.copy())
         samples[tag] = smp
-    elapsed, = batch.max_over_ranks([elapsed])
+    elapsed, bad_ranks = batch.max_over_ranks([elapsed, 0.0 if ok else 1.0])
+    world = len(batch.gather_strings(""))
     del slots, words, truth
     torch.cuda.empty_cache()
     # Roofline of each leg (SURVEY.md §8(d) algorithmic bytes: encode 4L(k+r),
@@ -560,7 +561,9 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
         return {"kernels": [f"{k}<{need},...>" for k in kernels[what]], "alg_bytes": alg,
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": t, "traffic_over_alg": round(t / alg, 4) if t else None}
-    return {"value": round(2 * nobj * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
+    # value: every rank's objects (weak: nobj per GPU) over the slowest rank's time.
+    return {"value": round(2 * nobj * world * S * args.steps / GIB / elapsed, 2), "unit": "GiB/s",
+            "scaling": "weak", "n_ranks": world,
             "config": f"need={need} total={total}, {S >> 20} MiB objects x {nobj} per GPU, chunk stride {cs} B; "
                       f"encode (both passes) + repair erased {erase}",
             "encode_gibs": round(nobj * S / GIB / (enc_ms * 1e-3), 2),
@@ -572,7 +575,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                          "traffic_source": replay.get("source")},
             "mappings": {"0": int((ms == 0).sum()), "1<<31": int((ms == 0x80000000).sum()),
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
-            "fallback_redraws": redraws, "verified": ok, "placement": placement,
+            "fallback_redraws": redraws, "verified": bad_ranks == 0.0, "placement": placement,
             "chunk_stride": cs, "chunk_bytes": 4 * L,
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
                     "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
