@@ -9,14 +9,19 @@
 //     memcpy pointers, so the buffer that ran out can be named;
 // then restores the handler it replaced (the profiler's or Python's) and
 // returns, so the faulting access repeats and that handler runs as before.
-// Diagnostics only: nothing in the library installs signal handlers.
+// Diagnostics only: nothing in the library installs signal handlers.  The
+// text is formatted by hand into stack buffers and written with write(2)
+// (no stdio, no allocation); backtrace() and dladdr() are not on POSIX's
+// async-signal-safe list -- the unwinder is loaded at install() so the
+// handler does not load it, and a fault taken while the dynamic loader's
+// lock is held would hang the report, the cost every such reporter
+// (glog's included) accepts.
 #pragma once
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <fcntl.h>
 #include <signal.h>
 #include <stdint.h>
-#include <stdio.h>
 #include <string.h>
 #include <sys/syscall.h>
 #include <ucontext.h>
@@ -29,20 +34,52 @@ inline bool g_installed = false;
 
 inline void say(const char* s) { (void)!write(2, s, strlen(s)); }
 
+// Appends to a fixed buffer without stdio (Line::add / hex / dec).
+struct Line {
+  char b[1024];
+  size_t n = 0;
+  Line& add(const char* s) {
+    while (*s && n + 1 < sizeof b) b[n++] = *s++;
+    b[n] = 0;
+    return *this;
+  }
+  Line& hex(uint64_t v, int digits = 0) {  // 0x-less; `digits` pads with zeros
+    char t[17];
+    int i = 16;
+    t[i] = 0;
+    do {
+      t[--i] = "0123456789abcdef"[v & 15];
+      v >>= 4;
+    } while ((v || 16 - i < digits) && i > 0);
+    return add(t + i);
+  }
+  Line& dec(int64_t v) {
+    char t[24];
+    int i = 23;
+    t[i] = 0;
+    const bool neg = v < 0;
+    uint64_t u = neg ? 0 - (uint64_t)v : (uint64_t)v;
+    do {
+      t[--i] = (char)('0' + u % 10);
+      u /= 10;
+    } while (u && i > 1);
+    if (neg) t[--i] = '-';
+    return add(t + i);
+  }
+  void out() { say(b); }
+};
+
 inline void frame_line(const char* tag, void* pc) {
-  char buf[768];
+  Line l;
+  l.add("  ").add(tag).add(" 0x").hex((uintptr_t)pc).add("  ");
   Dl_info di;
   if (dladdr(pc, &di) && di.dli_fname) {
-    const uintptr_t off = (uintptr_t)pc - (uintptr_t)di.dli_fbase;
-    if (di.dli_sname)
-      snprintf(buf, sizeof buf, "  %s %p  %s+0x%lx  (%s+0x%lx)\n", tag, pc, di.dli_fname, (unsigned long)off,
-               di.dli_sname, (unsigned long)((uintptr_t)pc - (uintptr_t)di.dli_saddr));
-    else
-      snprintf(buf, sizeof buf, "  %s %p  %s+0x%lx\n", tag, pc, di.dli_fname, (unsigned long)off);
+    l.add(di.dli_fname).add("+0x").hex((uintptr_t)pc - (uintptr_t)di.dli_fbase);
+    if (di.dli_sname) l.add("  (").add(di.dli_sname).add("+0x").hex((uintptr_t)pc - (uintptr_t)di.dli_saddr).add(")");
   } else {
-    snprintf(buf, sizeof buf, "  %s %p  (no object)\n", tag, pc);
+    l.add("(no object)");
   }
-  say(buf);
+  l.add("\n").out();
 }
 
 inline uintptr_t parse_hex(const char*& p) {
@@ -95,25 +132,30 @@ inline void on_fault(int sig, siginfo_t* si, void* ctx) {
   const greg_t* g = uc->uc_mcontext.gregs;
   const uintptr_t addr = (uintptr_t)si->si_addr;
   const unsigned long err = (unsigned long)g[REG_ERR];
-  char buf[1024];
-  snprintf(buf, sizeof buf,
-           "\n=== proxy_load crash report: signal %d code %d at %p (%s access, page-fault error 0x%lx) tid %ld\n"
-           "  rip %016llx rsp %016llx rdi %016llx rsi %016llx rdx %016llx rcx %016llx\n"
-           "  rax %016llx rbx %016llx r8  %016llx r9  %016llx r10 %016llx r11 %016llx\n",
-           sig, si->si_code, si->si_addr, (err & 16) ? "instruction" : (err & 2) ? "write" : "read", err,
-           (long)syscall(SYS_gettid), (unsigned long long)g[REG_RIP], (unsigned long long)g[REG_RSP],
-           (unsigned long long)g[REG_RDI], (unsigned long long)g[REG_RSI], (unsigned long long)g[REG_RDX],
-           (unsigned long long)g[REG_RCX], (unsigned long long)g[REG_RAX], (unsigned long long)g[REG_RBX],
-           (unsigned long long)g[REG_R8], (unsigned long long)g[REG_R9], (unsigned long long)g[REG_R10],
-           (unsigned long long)g[REG_R11]);
-  say(buf);
+  Line h;
+  h.add("\n=== proxy_load crash report: signal ").dec(sig).add(" code ").dec(si->si_code).add(" at 0x").hex(addr)
+      .add(" (").add((err & 16) ? "instruction" : (err & 2) ? "write" : "read").add(" access, page-fault error 0x")
+      .hex(err).add(") tid ").dec((int64_t)syscall(SYS_gettid)).add("\n");
+  h.out();
+  static const struct {
+    const char* name;
+    int reg;
+  } regs[2][6] = {{{"rip", REG_RIP}, {"rsp", REG_RSP}, {"rdi", REG_RDI}, {"rsi", REG_RSI}, {"rdx", REG_RDX}, {"rcx", REG_RCX}},
+                  {{"rax", REG_RAX}, {"rbx", REG_RBX}, {"r8 ", REG_R8}, {"r9 ", REG_R9}, {"r10", REG_R10}, {"r11", REG_R11}}};
+  for (const auto& row : regs) {
+    Line r;
+    r.add(" ");
+    for (const auto& x : row) r.add(" ").add(x.name).add(" ").hex((uint64_t)g[x.reg], 16);
+    r.add("\n").out();
+  }
   frame_line("pc   ", (void*)g[REG_RIP]);
   void* frames[64];
   const int nf = backtrace(frames, 64);
   for (int i = 0; i < nf; ++i) {
-    char tag[16];
-    snprintf(tag, sizeof tag, "#%-4d", i);
-    frame_line(tag, frames[i]);
+    Line t;
+    t.add("#").dec(i);
+    while (t.n < 5) t.add(" ");
+    frame_line(t.b, frames[i]);
   }
   say("  mappings within 2 MiB of the fault address, rdi and rsi:\n");
   const uintptr_t at[3] = {addr, (uintptr_t)g[REG_RDI], (uintptr_t)g[REG_RSI]};
