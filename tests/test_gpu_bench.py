@@ -97,3 +97,36 @@ def test_callers_beyond_the_host_call_slots_queue_and_finish():
     assert out[0] >= threads
     put_p50, put_p99 = out[4], out[5]
     assert put_p99 < max(20 * put_p50, 25.0), (put_p50, put_p99)  # no starved caller (ms)
+
+
+@pytest.mark.parametrize("alloc", ["torch", "vmm"])
+def test_device_legs_pin_every_object_to_the_oracle(alloc):
+    """bench.py's device legs at small sizes, end to end on the GPU: a symbol
+    batch (SymbolBatch.run, then .sample) at 4/6 and 10/14, and the fused byte
+    leg at 10/14 through the phased encode, each sampled and pinned by
+    oracle_pin -- every object verified, the byte leg's pass split adding up.
+    (Few 8 MiB objects switch to 1<<31; the switch and its redo are pinned by
+    test_gpu_parity.py's mid-object-switch and phased-event tests.)"""
+    import types
+
+    import torch
+    bench = _bench()
+    args = types.SimpleNamespace(object_mib=8, chunk_align=256, allocator=alloc, warmup=1, steps=2, shard_align=64,
+                                 traffic="")
+    samples = {}
+    for name, (need, total, erase, nobj) in {"s46": (4, 6, [0, 1], 5), "s1014": (10, 14, [0, 3, 10, 13], 3)}.items():
+        sb = bench.SymbolBatch(args, 0, 0x5A5A + need, need, total, (8 << 20) + 12, nobj, erase)
+        res = sb.run(2, 1)
+        assert res["ok"]
+        samples[name] = sb.sample(7 + need)
+        assert samples[name]["cols"].shape == (nobj, total, 4097)
+        sb.free()
+    leg = bench.bytes_leg(args, 0, 0, 10, 14, [0, 1, 2, 3], 6, mib=8, samples=samples, tag="bytes")
+    assert leg["verified"] and leg["n_ranks"] == 1
+    km = leg["kernel_ms"]
+    assert 0 < km["encode_pass0"] <= km["encode_both_passes"] and km["encode_redo"] >= 0
+    pin = bench.oracle_pin(samples)
+    assert {k: (v["verified_objects"], v["objects"]) for k, v in pin.items()} == \
+        {"s46": (5, 5), "s1014": (3, 3), "bytes": (6, 6)}
+    assert pin["bytes"]["domain"] == "bytes"
+    torch.cuda.synchronize()
