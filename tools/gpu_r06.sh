@@ -93,6 +93,12 @@ for step in "$@"; do
     rehearse2) run rehearse2 500 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --cpu-baseline 0 --alloc-probe 0 &&
                run rehearse2_torchrun 500 env SLIME_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --objects 32 --steps 5 --warmup 1 --cpu-baseline 0 --alloc-probe 0 ;;
+    # what one fused byte encode call enqueues, and the gaps between (C5 and C3 shapes)
+    etl) run etl_c5_plain 300 python tools/encode_timeline.py run &&
+         run etl_c5 300 rocprofv3 --kernel-trace -d "$OUT/etl_c5" -o etl --output-format csv -- python3 tools/encode_timeline.py run &&
+         python3 tools/encode_timeline.py show "$OUT/etl_c5" > "$OUT/etl_c5_show.txt" &&
+         run etl_c3 300 rocprofv3 --kernel-trace -d "$OUT/etl_c3" -o etl --output-format csv -- python3 tools/encode_timeline.py run --need 8 --total 12 --mib 256 --nobj 128 &&
+         python3 tools/encode_timeline.py show "$OUT/etl_c3" > "$OUT/etl_c3_show.txt" ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
