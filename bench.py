@@ -540,7 +540,7 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
         smp.update(need=need, total=total, have=have, mapping=ms.copy())
         samples[tag] = smp
     elapsed, bad_ranks = batch.max_over_ranks([elapsed, 0.0 if ok else 1.0])
-    world = len(batch.gather_strings(""))
+    world = dist.get_world_size() if dist.is_initialized() else 1
     del slots, words, truth
     torch.cuda.empty_cache()
     # Roofline of each leg (SURVEY.md §8(d) algorithmic bytes: encode 4L(k+r),
