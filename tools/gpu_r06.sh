@@ -99,6 +99,12 @@ for step in "$@"; do
          python3 tools/encode_timeline.py show "$OUT/etl_c5" > "$OUT/etl_c5_show.txt" &&
          run etl_c3 300 rocprofv3 --kernel-trace -d "$OUT/etl_c3" -o etl --output-format csv -- python3 tools/encode_timeline.py run --need 8 --total 12 --mib 256 --nobj 128 &&
          python3 tools/encode_timeline.py show "$OUT/etl_c3" > "$OUT/etl_c3_show.txt" ;;
+    # C5's per-GPU share at N = 8 / 4 / 2 (8 / 16 / 32 objects of 1 GiB, 10/14) on the stamped twin
+    c5share) C="python tools/c2_stamps.py --need 10 --total 14 --mib 1024"
+      run c5s_8 300 $C --nobj 8 --reps 10 --geometry 0:0,4:0,2:0,8:512,4:512 &&
+      run c5s_16 300 $C --nobj 16 --reps 8 --geometry 0:0,2:0,8:0,4:512 &&
+      run c5s_32 300 $C --nobj 32 --reps 6 --geometry 0:0,1:0,4:0,2:512 &&
+      run c5s_8b 300 $C --nobj 8 --reps 10 --geometry 0:0,4:0,2:0 ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
