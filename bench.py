@@ -1396,6 +1396,10 @@ def main():
                                              "objects_per_rank": PRESETS[n][3], "scaling": "weak"}
                                          for n in args.shape_legs.split(",") if n and
                                          PRESETS[n][:3] != (args.need, args.total, args.object_mib)},
+                              "object_bytes_paths": [name for name, on in (
+                                  ("object_bytes_path", args.bytes_path),
+                                  ("object_bytes_path_c5", args.c5_bytes and
+                                   (args.need, args.total, args.object_mib) != PRESETS["c5"][:3])) if on],
                               "host_path.pooled": None if not args.pooled else
                               {"driver_rank": 0, "threads": args.pool_threads, "devices": devices,
                                "pool_env": os.environ.get("SLIME_RS_DEVICES"),
