@@ -105,6 +105,8 @@ for step in "$@"; do
       run c5s_16 300 $C --nobj 16 --reps 8 --geometry 0:0,2:0,8:0,4:512 &&
       run c5s_32 300 $C --nobj 32 --reps 6 --geometry 0:0,1:0,4:0,2:512 &&
       run c5s_8b 300 $C --nobj 8 --reps 10 --geometry 0:0,4:0,2:0 ;;
+    # four ranks on one GPU: the N = 4 code paths (shape legs limited to C2 so four ranks fit in one HBM)
+    rehearse4) run rehearse4 500 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 4 --objects 32 --steps 3 --warmup 1 --cpu-baseline 0 --alloc-probe 0 --shape-legs=c2 ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
