@@ -1592,18 +1592,14 @@ def main():
             line["verified_columns_per_object"] = ORACLE_COLS + 1
             pinned_ok = all(v["verified_objects"] == v["objects"] for v in pin.values())
             line["verified"] = line["verified"] and pinned_ok
-            for key, leg in (("shapes", None), ("c5_partitioned", "c5_partitioned"),
-                             ("object_bytes_path", "object_bytes_path"),
-                             ("object_bytes_path_c5", "object_bytes_path_c5")):
-                if key == "shapes":
-                    for nm, v in shapes.items():
-                        if nm in pin:
-                            v["verified_objects"] = pin[nm]["verified_objects"]
-                            v["verified"] = v["verified"] and pin[nm]["verified_objects"] == pin[nm]["objects"]
-                elif line.get(key) and leg in pin:
-                    line[key]["verified_objects"] = pin[leg]["verified_objects"]
-                    line[key]["verified"] = line[key]["verified"] and \
-                        pin[leg]["verified_objects"] == pin[leg]["objects"]
+            def pinned(leg: dict | None, name: str) -> None:  # the leg's own verdict AND its pin
+                if leg is not None and name in pin:
+                    leg["verified_objects"] = pin[name]["verified_objects"]
+                    leg["verified"] = leg["verified"] and pin[name]["verified_objects"] == pin[name]["objects"]
+            for nm, v in shapes.items():
+                pinned(v, nm)
+            for key in ("c5_partitioned", "object_bytes_path", "object_bytes_path_c5"):
+                pinned(line.get(key), key)
             bad = bad or not pinned_ok
         print(json.dumps(line), flush=True)
     if world > 1:
