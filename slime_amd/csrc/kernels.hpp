@@ -122,17 +122,19 @@ inline uint64_t queue_blocks(uint64_t full, uint64_t units) {
 // (in-process sweeps, profiles/r02/s61_spread/, s62_spread2/: best S = 1 at
 // 64 and 128 objects, 2 at C2's 32, 4 at C5's 16; more segments cost up to 4%).
 // `streams` = k + rows of an apply launch (0: not given, the byte kernels):
-// the apply kernel over six streams or fewer an object (4/6 and narrower)
-// takes about 256 segments, one per wave group in flight -- C2's 32 objects
-// at S = 8 ran +1.0 to +2.8% and 64 objects at S = 4 +1.3 to +2.1% on four
-// boxes, where 8/12 and 10/14 gained nothing consistent from more
-// (profiles/r06/s5_spread/, s6_spread2/; tools/c2_stamps.py).
+// an apply launch over six streams an object (4/6) takes about 256 segments,
+// one per wave group in flight -- C2's 32 objects at S = 8 ran +1.0 to +2.8%
+// and 64 objects at S = 4 +1.3 to +2.1% on four boxes, where 8/12 and 10/14
+// gained nothing consistent from more (profiles/r06/s5_spread/,
+// s6_spread2/), and slime's default 3/5 lost up to 3% at S = 8 on a slow
+// allocation and was level on a fast one (s13_spread35/): it keeps the 64
+// (tools/c2_stamps.py).
 // 0 when the launch has too many units for 32-bit tickets, or at most one
 // block's (below): the caller takes the static kernel.
 inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C, uint32_t streams = 0) {
   const uint64_t ntiles = ((ncols >> 2) + 64ull * U - 1) / (64ull * U);
   const uint64_t groups = (ntiles + 4ull * C - 1) / (4ull * C);
-  const uint64_t target = streams && streams <= 6 ? 256 : 64;
+  const uint64_t target = streams == 6 ? 256 : 64;
   uint64_t S = (target + (uint64_t)nobj - 1) / (nobj ? nobj : 1);
   if (S > groups) S = groups ? groups : 1;
   const uint64_t B = (groups + S - 1) / S;

@@ -107,6 +107,15 @@ for step in "$@"; do
       run c5s_8b 300 $C --nobj 8 --reps 10 --geometry 0:0,4:0,2:0 ;;
     # four ranks on one GPU: the N = 4 code paths (shape legs limited to C2 so four ranks fit in one HBM)
     rehearse4) run rehearse4 500 env SLIME_BENCH_SHARE_GPU=1 python bench.py --gpus 4 --objects 32 --steps 3 --warmup 1 --cpu-baseline 0 --alloc-probe 0 --shape-legs=c2 ;;
+    # slime's default redundancy 3/5 (multi_config.go:139,152) as a device batch: the narrow-code spread rule
+    spread35) C="python tools/c2_stamps.py --need 3 --total 5 --mib 64"
+      run ss35_32 300 $C --nobj 32 --reps 16 --geometry 0:0,2:0,4:0,16:0 &&
+      run ss35_64 300 $C --nobj 64 --reps 12 --geometry 0:0,1:0,2:0 &&
+      run ss35_32b 300 $C --nobj 32 --reps 16 --geometry 0:0,2:0 ;;
+    spread35b) for rep in 1 2 3; do
+        run ss35b_$rep 300 python tools/c2_stamps.py --need 3 --total 5 --mib 64 --nobj 32 --reps 16 --geometry 0:0,2:0,4:0 &&
+        run ss46b_$rep 300 python tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32 --reps 16 --geometry 0:0,2:0,4:0 || exit 1
+      done ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
