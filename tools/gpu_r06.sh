@@ -43,7 +43,9 @@ for step in "$@"; do
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     # the driver's command under the profiler WITH the pooled leg
     profpool) run profpool 700 rocprofv3 --kernel-trace --stats -d "$OUT/profpool" -o bench --output-format csv -- \
-            python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 &&
+            python tools/prof_summary.py "$OUT/profpool" > "$OUT/profpool_summary.json" &&
+            rm -f "$OUT/profpool/bench_kernel_trace.csv" ;;
     # only the pooled leg under the profiler (short), to reproduce the r05 fault quickly
     profpoolonly) run profpoolonly 400 rocprofv3 --kernel-trace --stats -d "$OUT/profpoolonly" -o pool --output-format csv -- \
             python3 bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --cpu-baseline 0 --host-path 0 --alloc-probe 0 --c5-leg 0 --shape-legs= ;;
@@ -115,6 +117,13 @@ for step in "$@"; do
     spread35b) for rep in 1 2 3; do
         run ss35b_$rep 300 python tools/c2_stamps.py --need 3 --total 5 --mib 64 --nobj 32 --reps 16 --geometry 0:0,2:0,4:0 &&
         run ss46b_$rep 300 python tools/c2_stamps.py --need 4 --total 6 --mib 64 --nobj 32 --reps 16 --geometry 0:0,2:0,4:0 || exit 1
+      done ;;
+    # the profiler's fault against the number of concurrent callers (first crash ends the session)
+    profthreads) for t in ${PROF_THREADS:-2 4 8 16}; do
+        run profpool_t$t 400 rocprofv3 --kernel-trace --stats -d "$OUT/profpool_t$t" -o pool --output-format csv -- \
+          python3 bench.py --objects 8 --steps 2 --warmup 1 --bytes-path 0 --c5-bytes 0 --cpu-baseline 0 --host-path 0 \
+          --alloc-probe 0 --c5-leg 0 --shape-legs= --pool-threads $t || exit 1
+        rm -f "$OUT/profpool_t$t/pool_kernel_trace.csv"  # tens of MB a run; the stats CSV stays
       done ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
