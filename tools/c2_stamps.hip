@@ -30,8 +30,9 @@ int launch(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t
 }
 }  // namespace
 
-// k = 3 (slime's default 3/5: U 4, C 2), 4 (C2: U 4, C 2), 8 (C3: U 3, C 2) or 10 (C5: U 3, C 2),
-// the product's queue geometry.
+// k = 3 (slime's default 3/5: U 4, C 2), 4 (C2: U 4, C 2), 8 (C3: U 3, C 2), 10 (C5: U 3, C 2),
+// 12 (U 3, C 2) or 16 (U 1, C 6): the product's queue geometry (rs_apply.hip queue_unroll /
+// queue_unit_tiles).
 // ticket: a zeroed counter set of kQueueCounters + 1 lines of 64 words (each
 // launch leaves it zero).  stamps: 9 words per wave, or null to get the wave
 // count only (*nwaves).  spread / blocks: 0 = the product's rule, else that
@@ -47,6 +48,12 @@ extern "C" int cs_launch(int k, const uint32_t* in, uint32_t* out, uint64_t io, 
   if (k == 4)
     return launch<4, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
                            (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 12)
+    return launch<12, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                            (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 16)
+    return launch<16, 1, 6>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                            (uint64_t*)stamps, nwaves, spread, blocks);
   if (k == 10)
     return launch<10, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
                             (uint64_t*)stamps, nwaves, spread, blocks);

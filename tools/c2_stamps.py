@@ -115,7 +115,7 @@ def main():
     D.fill_symbols(buf, 0x5113E)
     enc = D.Plan.encode(need, total)
     lay = D.layout_of(total, L, SS)
-    coeff = np.zeros((r, 16), dtype=np.uint32)
+    coeff = np.zeros((r, max(16, -(-need // 16) * 16)), dtype=np.uint32)
     coeff[:, :need] = enc.coefficients()
     c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
     ii = torch.arange(need, dtype=torch.int32, device="cuda")

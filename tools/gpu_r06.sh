@@ -125,6 +125,14 @@ for step in "$@"; do
           --alloc-probe 0 --c5-leg 0 --shape-legs= --pool-threads $t || exit 1
         rm -f "$OUT/profpool_t$t/pool_kernel_trace.csv"  # tens of MB a run; the stats CSV stays
       done ;;
+    # two segments an object for wide codes at 64 objects? 10/14, 12/16, 16/20 (k + rows 14, 16, 20)
+    spreadwide) C="python tools/c2_stamps.py"
+      for rep in 1 2; do
+        run sw_c5_64_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0 &&
+        run sw_12_64_$rep 300 $C --need 12 --total 16 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0 &&
+        run sw_16_64_$rep 300 $C --need 16 --total 20 --mib 1024 --nobj 64 --reps 4 --geometry 0:0,2:0 &&
+        run sw_16_128_$rep 300 $C --need 16 --total 20 --mib 256 --nobj 128 --reps 6 --geometry 0:0,2:0 || exit 1
+      done ;;
     *) echo "unknown step $step" | tee -a "$OUT/session.log"; exit 2 ;;
   esac
 done
