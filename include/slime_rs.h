@@ -263,7 +263,8 @@ int slime_rs_decode_objects_chunked(slime_rs_plan_t reconstruct_plan, uint8_t *s
 /* encode_objects_chunked that also records the hipEvent_t `phase_event` (may be
  * null) on `stream` between its two passes: after the speculative pass and the
  * mapping selection, before the re-encode of the objects mapped with 1<<31 --
- * so a caller can time the re-encode's share of the call. */
+ * so a caller can time the re-encode's share of the call.  A call with nothing
+ * to encode (nobj or the object size 0) records nothing. */
 int slime_rs_encode_objects_phased(slime_rs_plan_t encode_plan, uint8_t *slots, uint64_t slot_stride,
                                    uint64_t chunk_stride, uint64_t object_size, uint64_t nobj, uint32_t *mapping,
                                    uint32_t *status, void *stream, void *phase_event);
