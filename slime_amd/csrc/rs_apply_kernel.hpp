@@ -554,27 +554,15 @@ __host__ __device__ inline uint32_t walk_units(uint32_t ntiles, uint32_t spread)
 // unit, `*count` of them): wave w takes entries w, w + nwaves, ...  Same
 // interface as TicketWalk, for kernels that redo a chosen subset of a
 // TicketWalk launch's units.
-// PF: the entry after the current one is loaded one unit ahead, so entering a
-// unit does not wait on the list.
-// SEG > 0: the walk's index x reads entry (x % SEG) * ceil(n / SEG) + x / SEG,
-// so the units in flight at once come from SEG far-apart stretches of the
-// list instead of one.
-template <int C, bool PF = false, int SEG = 0>
+template <int C>
 struct ListWalk {
   const uint32_t* list;
   uint32_t n, e, step, units, ntiles;
-  uint32_t nreal, seg_len = 0;  // SEG: the list's entries, entries per stretch
-  uint32_t nv = 0;  // PF: list[e + step]
   uint32_t obj = 0, tb = 0, cnt = 0, i = 0;
   bool live = true;
   __device__ __forceinline__ ListWalk(const uint32_t* list_, uint32_t n_, uint32_t first, uint32_t step_,
                                       uint32_t units_, uint32_t ntiles_)
-      : list(list_), n(n_), e(first - step_), step(step_), units(units_), ntiles(ntiles_), nreal(n_) {
-    if (SEG) {
-      seg_len = (n_ + SEG - 1) / SEG;
-      n = seg_len * SEG;
-    }
-    if (PF && first < n_) nv = list_[first];
+      : list(list_), n(n_), e(first - step_), step(step_), units(units_), ntiles(ntiles_) {
     next_unit();
   }
   __device__ __forceinline__ void next_unit() {
@@ -584,118 +572,6 @@ struct ListWalk {
         live = false;
         return;
       }
-      uint32_t v;
-      if constexpr (SEG > 0) {
-        const uint64_t at = (uint64_t)(e % SEG) * seg_len + e / SEG;
-        if (at >= nreal) continue;
-        v = list[at];
-      } else if constexpr (PF) {
-        v = nv;
-        if ((uint64_t)e + step < n) nv = list[e + step];
-      } else {
-        v = list[e];
-      }
-      obj = v / units;
-      tb = unit_tile_base<C>(v % units);
-      i = 0;
-      cnt = tb < ntiles ? (ntiles - tb + 3) / 4 : 0;
-      if (cnt > C) cnt = C;
-      if (cnt) return;
-    }
-  }
-  __device__ __forceinline__ uint32_t tile() const { return tb + 4 * i; }
-  __device__ __forceinline__ void advance() {
-    if (++i >= cnt) next_unit();
-  }
-};
-
-// The same list dealt one tile at a time (entry x / C, its tile x % C):
-// wave w takes tiles w, w + nwaves, ... of the n * C, so the waves' shares
-// differ by at most one tile instead of one unit.  The next tile's entry is
-// loaded a tile ahead.
-template <int C>
-struct ListTileWalk {
-  const uint32_t* list;
-  uint64_t x, step, end;
-  uint32_t units, ntiles;
-  uint32_t nv = 0;  // list[(x + step) / C]
-  uint32_t obj = 0, tb = 0;
-  bool live = true;
-  __device__ __forceinline__ ListTileWalk(const uint32_t* list_, uint32_t n_, uint32_t first, uint32_t step_,
-                                          uint32_t units_, uint32_t ntiles_)
-      : list(list_), x((uint64_t)first - step_), step(step_), end((uint64_t)n_ * C), units(units_), ntiles(ntiles_) {
-    if (first < end) nv = list_[first / C];
-    next_unit();
-  }
-  __device__ __forceinline__ void next_unit() {
-    for (;;) {
-      x += step;
-      if (x >= end) {
-        live = false;
-        return;
-      }
-      const uint32_t v = nv;
-      if (x + step < end) nv = list[(x + step) / C];
-      obj = v / units;
-      tb = unit_tile_base<C>(v % units) + 4 * (uint32_t)(x % C);
-      if (tb < ntiles) return;
-    }
-  }
-  __device__ __forceinline__ uint32_t tile() const { return tb; }
-  __device__ __forceinline__ void advance() { next_unit(); }
-};
-
-// The same list dealt by tickets instead of a static share, so the faster
-// XCDs take more of it: groups of four consecutive entries (one 4C-tile window
-// when the entries are consecutive units) over NC partitions, drawn as
-// TicketWalk draws its groups, with its counter-set protocol (zero at launch;
-// the launch's last wave out re-zeroes the set: finish()).
-template <int C, int NC>
-struct ListTicketWalk {
-  const uint32_t* list;
-  uint32_t* ticket;
-  uint32_t n, ngrp, units, ntiles, lane;
-  uint32_t p, dry = 0;
-  uint32_t obj = 0, tb = 0, cnt = 0, i = 0, pend = 0;
-  bool live = true;
-  __device__ __forceinline__ ListTicketWalk(const uint32_t* list_, uint32_t* ticket_, uint32_t n_, uint32_t units_,
-                                            uint32_t ntiles_, uint32_t lane_)
-      : list(list_), ticket(ticket_), n(n_), ngrp((n_ + 3) / 4), units(units_), ntiles(ntiles_), lane(lane_) {
-    p = hw_xcc_id() % NC;
-    if (!skip_empty()) return;
-    request();
-    next_unit();
-  }
-  __device__ __forceinline__ bool skip_empty() {  // as TicketWalk::skip_empty
-    if (p < ngrp) return true;
-    dry += NC - p;
-    p = 0;
-    if (ngrp == 0 || dry >= NC) {
-      live = false;
-      return false;
-    }
-    return true;
-  }
-  __device__ __forceinline__ void request() {
-    pend = 0;
-    if (lane == 0) pend = atomicAdd(ticket + p * kTicketStride, 1u);
-  }
-  __device__ __forceinline__ void next_unit() {
-    for (;;) {
-      const uint32_t l = __builtin_amdgcn_readlane(pend, 0);  // lane 0 drew it, whatever the exec mask
-      if (l >= 4 * ((ngrp + NC - 1 - p) / NC)) {
-        if (++dry >= NC) {
-          live = false;
-          return;
-        }
-        p = p + 1 == NC ? 0 : p + 1;
-        if (!skip_empty()) return;
-        request();
-        continue;
-      }
-      request();
-      const uint32_t e = ((l >> 2) * NC + p) * 4 + (l & 3);
-      if (e >= n) continue;
       const uint32_t v = list[e];
       obj = v / units;
       tb = unit_tile_base<C>(v % units);
@@ -708,16 +584,6 @@ struct ListTicketWalk {
   __device__ __forceinline__ uint32_t tile() const { return tb + 4 * i; }
   __device__ __forceinline__ void advance() {
     if (++i >= cnt) next_unit();
-  }
-  __device__ __forceinline__ void finish() {  // as TicketWalk::finish
-    if (lane == 0) {
-      uint32_t* const done = ticket + NC * kTicketStride;
-      if (atomicAdd(done, 1u) == gridDim.x * gridDim.y * (blockDim.x >> 6) - 1) {
-#pragma unroll
-        for (int q = 0; q < NC; ++q) atomicExch(ticket + q * kTicketStride, 0u);
-        atomicExch(done, 0u);
-      }
-    }
   }
 };
 

@@ -801,44 +801,13 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
 // mapping came out 1<<31 (status 0) that phase 0 encoded with mapping 0,
 // as entries obj * units + unit, appended in any order; *count (zero on
 // entry) receives their number.
-// AGG: one count atomic per block and pass instead of one per wave (the
-// block's entries land contiguous).
-template <int C, bool AGG = false>
+template <int C>
 __global__ __launch_bounds__(kBlock) void redo_list_kernel(const uint8_t* __restrict__ record,
                                                            const uint32_t* __restrict__ mapping,
                                                            const uint32_t* __restrict__ status, uint32_t nobj,
                                                            uint32_t units, uint32_t nint, uint32_t* __restrict__ list,
                                                            uint32_t* __restrict__ count) {
   const uint32_t lane = threadIdx.x & 63;
-  if constexpr (AGG) {
-    __shared__ uint32_t wcount[kWaves];
-    __shared__ uint32_t bbase;
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint64_t total = (uint64_t)nobj * units;
-    for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < total; base += (uint64_t)gridDim.x * kBlock) {
-      const uint64_t e = base + threadIdx.x;
-      bool need = false;
-      if (e < total) {
-        const uint32_t o = (uint32_t)(e / units), u = (uint32_t)(e % units);
-        need = mapping[o] != 0 && status[o] == 0 && apply::unit_tile_base<C>(u) < nint && record[e] == 0;
-      }
-      const uint64_t mask = __ballot(need);
-      if (lane == 0) wcount[wv] = (uint32_t)__popcll(mask);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-#pragma unroll
-        for (int q = 0; q < kWaves; ++q) tot += wcount[q];
-        bbase = tot ? atomicAdd(count, tot) : 0u;
-      }
-      __syncthreads();
-      uint32_t at = bbase;
-      for (uint32_t q = 0; q < wv; ++q) at += wcount[q];
-      if (need) list[at + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = (uint32_t)e;
-      __syncthreads();  // wcount / bbase are rewritten by the next pass
-    }
-    return;
-  }
   const uint64_t wave = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t total = (uint64_t)nobj * units;
@@ -861,17 +830,14 @@ __global__ __launch_bounds__(kBlock) void redo_list_kernel(const uint8_t* __rest
 // Phase 1 after a switched phase 0: re-encode with the object's mapping the
 // listed interior units (redo_list_kernel), then every edge tile and column
 // tail of the objects mapped with 1<<31 (phase 0 wrote those with mapping 0).
-// The interior walk is the queue kernel's pipeline over the list: WALK 0 a
-// static share (wave w takes entries w, w + nwaves, ...), 1 the same with the
-// next entry loaded a unit ahead, 2 dealt by tickets from `ticket` (a counter
-// set of NC partitions, zero at launch and left zero), 3 a static share of
-// single tiles, 4 / 5 the static share over 16 / 64 stretches of the list.
-template <int K, int U, int C, int WALK = 0, int NC = 8>
+// The interior walk is the queue kernel's pipeline over a static share of the
+// list.
+template <int K, int U, int C>
 __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     const uint32_t* __restrict__ status, const uint32_t* __restrict__ mapping, const uint32_t* __restrict__ list,
-    const uint32_t* __restrict__ count, uint32_t units, uint32_t* __restrict__ ticket) {
+    const uint32_t* __restrict__ count, uint32_t units) {
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -892,8 +858,8 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
     encode_interior_tile<K, U, false>(r, window(o) + (uint64_t)K * chunk, chunk, mapping[o], rows, coeff, out_idx,
                                       t * (64 * U) + lane, nvec, unused);
   };
-  auto walk = [&](auto& w) {
-    if (!w.live) return;
+  apply::ListWalk<C> w(list, *count, wave, nwaves, units, nint);
+  if (w.live) {
     uint4 ra[U][K], rb[U][K];
     load(ra, w.obj, w.tile());
     for (;;) {
@@ -909,20 +875,6 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
       compute(rb, co, ct);
       if (!w.live) break;
     }
-  };
-  if constexpr (WALK == 2) {
-    apply::ListTicketWalk<C, NC> w(list, ticket, *count, units, nint, lane);
-    walk(w);
-    w.finish();
-  } else if constexpr (WALK == 3) {
-    apply::ListTileWalk<C> w(list, *count, wave, nwaves, units, nint);
-    walk(w);
-  } else if constexpr (WALK >= 4) {  // 4: 16 stretches, 5: 64
-    apply::ListWalk<C, false, WALK == 4 ? 16 : 64> w(list, *count, wave, nwaves, units, nint);
-    walk(w);
-  } else {
-    apply::ListWalk<C, WALK == 1> w(list, *count, wave, nwaves, units, nint);
-    walk(w);
   }
   // Edge tiles and column tails of the objects mapped with 1<<31.
   const uint32_t nedge = ntiles - nint;

@@ -70,7 +70,7 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock),
                      0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
-                     a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units, nullptr);
+                     a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units);
   return hipGetLastError();
 }
 

@@ -49,58 +49,32 @@ extern "C" int bqv_encode(int variant, uint8_t* slots, uint64_t stride, uint64_t
 
 // Second pass after a switched first pass (record from bqv_encode): the redo
 // list and the redo kernel, the latter on `blocks` blocks.  count: 1 word,
-// zeroed here; list: nobj x units words.  walk: encode_bytes_redo_kernel's
-// WALK (0 static share, product; 1 static with the next entry loaded ahead;
-// 2 ticketed on `ticket`, left zero; 3 static share of single tiles; 4 / 5 static share over 16 / 64 list stretches); agg: redo_list_kernel's AGG.
-template <int K, int U, int C, int WALK, bool AGG>
+// zeroed here; list: nobj x units words.
+template <int K, int U, int C>
 int redo(uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows,
          const uint32_t* coeff, const uint32_t* out_idx, const uint32_t* mapping, const uint32_t* status,
-         const uint8_t* record, uint32_t* list, uint32_t* count, uint32_t blocks, uint32_t* ticket, hipStream_t s) {
+         const uint8_t* record, uint32_t* list, uint32_t* count, uint32_t blocks, hipStream_t s) {
   const uint32_t spread = queue_spread(nobj, L, U, C);
   if (!spread) return -2;
   const uint32_t nint = bytes::encode_interior_tiles(S, L, 0, L, K, U);
   const uint32_t units = apply::walk_units<C>(nint, spread);
   if (hipMemsetAsync(count, 0, 4, s) != hipSuccess) return -1;
-  hipLaunchKernelGGL((bytes::redo_list_kernel<C, AGG>), dim3(1024), dim3(apply::kBlock), 0, s, record, mapping, status,
-                     nobj, units, nint, list, count);
-  hipLaunchKernelGGL((bytes::encode_bytes_redo_kernel<K, U, C, WALK, kQueueCounters>), dim3(blocks),
-                     dim3(apply::kBlock), 0, s, slots, stride, L, cstride, (uint64_t)0, L, S, nobj, rows, coeff,
-                     out_idx, status, mapping, list, count, units, ticket);
+  hipLaunchKernelGGL(bytes::redo_list_kernel<C>, dim3(1024), dim3(apply::kBlock), 0, s, record, mapping, status, nobj,
+                     units, nint, list, count);
+  hipLaunchKernelGGL((bytes::encode_bytes_redo_kernel<K, U, C>), dim3(blocks), dim3(apply::kBlock), 0, s, slots,
+                     stride, L, cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, status, mapping, list, count,
+                     units);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int K, int U, int C>
-int redo_any(int walk, int agg, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S,
-             uint32_t nobj, uint32_t rows, const uint32_t* coeff, const uint32_t* out_idx, const uint32_t* mapping,
-             const uint32_t* status, const uint8_t* record, uint32_t* list, uint32_t* count, uint32_t blocks,
-             uint32_t* ticket, hipStream_t s) {
-#define SLIME_BQV_REDO(W, A) \
-  if (walk == W && !!agg == A) \
-    return redo<K, U, C, W, A>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, mapping, status, record, \
-                               list, count, blocks, ticket, s);
-  SLIME_BQV_REDO(0, false)
-  SLIME_BQV_REDO(0, true)
-  SLIME_BQV_REDO(1, false)
-  SLIME_BQV_REDO(1, true)
-  SLIME_BQV_REDO(2, false)
-  SLIME_BQV_REDO(2, true)
-  SLIME_BQV_REDO(3, false)
-  SLIME_BQV_REDO(3, true)
-  SLIME_BQV_REDO(4, true)
-  SLIME_BQV_REDO(5, true)
-#undef SLIME_BQV_REDO
-  return -3;
-}
-
-extern "C" int bqv_redo(int variant, int walk, int agg, uint8_t* slots, uint64_t stride, uint64_t cstride,
-                        uint64_t L, uint64_t S, uint32_t nobj, uint32_t rows, const uint32_t* coeff,
-                        const uint32_t* out_idx, const uint32_t* mapping, const uint32_t* status,
-                        const uint8_t* record, uint32_t* list, uint32_t* count, uint32_t blocks, uint32_t* ticket,
-                        void* stream) {
+extern "C" int bqv_redo(int variant, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_t L, uint64_t S,
+                        uint32_t nobj, uint32_t rows, const uint32_t* coeff, const uint32_t* out_idx,
+                        const uint32_t* mapping, const uint32_t* status, const uint8_t* record, uint32_t* list,
+                        uint32_t* count, uint32_t blocks, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
-    case 0: return redo_any<8, 2, 3>(walk, agg, slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, mapping, status, record, list, count, blocks, ticket, s);
-    case 3: return redo_any<10, 1, 6>(walk, agg, slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, mapping, status, record, list, count, blocks, ticket, s);
+    case 0: return redo<8, 2, 3>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, mapping, status, record, list, count, blocks, s);
+    case 3: return redo<10, 1, 6>(slots, stride, cstride, L, S, nobj, rows, coeff, out_idx, mapping, status, record, list, count, blocks, s);
     default: return -3;
   }
 }

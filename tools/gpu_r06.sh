@@ -54,9 +54,7 @@ for step in "$@"; do
             pmc pmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
     pmc_c2) pmc pmc_c2_fetch FETCH_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
             pmc pmc_c2_write WRITE_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
-    # second-pass walk variants of the fused byte encode (static / prefetched / ticketed list; list-count atomics)
-    redowalk) run redowalk 500 python tools/bytes_queue_variants.py --shapes c5,c3 --rounds 9 --redo-blocks 512 \
-              --redo-walks 0:0,0:1,3:1,4:1,5:1 ;;
+    # second-pass walk variants (s19): the harness at commit b1d0ca6 only, its variants were not kept
     tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
     bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;
