@@ -110,6 +110,12 @@ tools/libbqvar.so: tools/bytes_queue_variants.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 .PHONY: bqvar
 
+# Byte encode second pass: re-encode vs top-bit correction (tools only): make topbits
+topbits: tools/libtopbits.so
+tools/libtopbits.so: tools/topbits_fix.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+.PHONY: topbits
+
 # Hash throughput probe for §8(f3) (tools only): make hashprobe
 hashprobe: tools/libhashprobe.so
 tools/libhashprobe.so: tools/hash_probe.hip

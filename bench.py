@@ -554,6 +554,8 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
     alg_enc = nobj * 4 * L * total
     alg_dec = nobj * 4 * L * (need + len(erase))
     kernels = {"encode": ["encode_bytes_queue_kernel", "encode_bytes_redo_kernel"], "decode": ["decode_bytes_queue_kernel"]}
+    if _top_bits(need, S):  # the second pass corrects from top bits (rs_bytes_launch.hpp)
+        kernels["encode"] = ["encode_bytes_queue_bits_kernel", "encode_bytes_fix_kernel", "encode_bytes_redo_kernel"]
     if _matrix_cores(need, total - need) and need >= 25:
         kernels["encode"] = ["encode_bytes_mfma_kernel"]
     if _matrix_cores(need, len(erase)):
@@ -582,10 +584,19 @@ def bytes_leg(args, dev: int, rank: int, need: int, total: int, erase: list[int]
                          "other": int(((ms != 0) & (ms != 0x80000000)).sum())},
             "fallback_redraws": redraws, "verified": bad_ranks == 0.0, "placement": placement,
             "chunk_stride": cs, "chunk_bytes": 4 * L,
+            "second_pass": "top-bit correction" if _top_bits(need, S) else "re-encode",
             "what": "object bytes in HBM -> MapToGF + encode + MapFromGF (speculative pass that switches an object "
-                    "to 1<<31 once a word >= p is seen, then a redo of the units encoded before) and repair of "
+                    "to 1<<31 once a word >= p is seen, then a redo of the units encoded before: re-encoded, or "
+                    "corrected from the top bits the first pass stored, second_pass) and repair of "
                     "erased chunks from chunk bytes; encode_pass0 / encode_redo split at a HIP event the library "
                     "records between the passes (the redo includes its list build and the 1<<31 edge columns)"}
+
+
+def _top_bits(need: int, S: int) -> bool:
+    """Whether the fused encode's second pass corrects the switched units from
+    top bits (slime_rs_switch_bits: mode 0 = objects >= 1 GiB at need <= 10)."""
+    mode = D.N.lib.slime_rs_switch_bits(-1)
+    return need <= 10 and (mode == 1 or (mode == 0 and S >= 1 << 30))
 
 
 def _bytes_traffic(args, config: str, need: int, kernels: dict) -> dict:

@@ -104,6 +104,17 @@ int slime_rs_kernel_schedule(int mode);
  * int8-limb kernel on v_mfma_i32_16x16x64_i8 (default), 0 = the VALU kernels.
  * mode < 0 queries.  Results are identical; the parity tests run both. */
 int slime_rs_kernel_matrix_cores(int mode);
+/* Second pass of the fused byte encode (writeChunks on device) for need <= 10
+ * (process-wide).  The first pass assumes MapToGF's mapping 0; the units it
+ * encoded before an object's first word >= p must be redone with 1<<31.
+ * 0 = by object size (default): objects of 1 GiB and more (uniform bytes
+ * switch in 27% of them) have the first pass also store each mapping-0
+ * column's need top bits (need/8 bytes a column of device scratch), and the
+ * second pass corrects those units' parity from the bits and the parity
+ * itself instead of re-reading the data; smaller objects re-encode the units.
+ * 1 = always correct, 2 = always re-encode.  mode < 0 queries.  Results are
+ * identical; the parity tests run every mode. */
+int slime_rs_switch_bits(int mode);
 
 /* ==== internal/rs/gf ===================================================== */
 

@@ -76,6 +76,7 @@ SIGNATURES = [
     ("slime_rs_kernel_pipeline", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_schedule", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_kernel_matrix_cores", ctypes.c_int, [ctypes.c_int]),
+    ("slime_rs_switch_bits", ctypes.c_int, [ctypes.c_int]),
     ("slime_rs_device_alloc", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     ("slime_rs_device_free", ctypes.c_int, [ctypes.c_void_p]),
     ("slime_rs_device_alloc_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(AllocInfo)]),

@@ -68,6 +68,13 @@ void set_pipelined_kernels(bool on);
 // static shares.  Process-wide; see rs_apply.hip.
 int queue_mode();
 void set_queue_mode(int m);
+// Second pass of the fused byte encode at need <= 10 on the ticket walk:
+// 0 = correct the switched units' parity from top bits phase 0 stored when
+// objects are >= 1 GiB (where uniform bytes switch in more than a quarter of
+// the objects), else re-encode them (default); 1 = always correct; 2 =
+// always re-encode.  Process-wide; see rs_bytes_launch.hpp.
+int switch_bits_mode();
+void set_switch_bits_mode(int m);
 // Whether a launch on `s` may take the dynamic schedule under the mode (a
 // captured launch replays on the set it was captured with: mode 2 only).
 bool queue_allowed(hipStream_t s);
@@ -177,6 +184,7 @@ inline uint32_t queue_spread(uint32_t nobj, uint64_t ncols, int U, int C, uint32
 // state that another thread may have changed in between.
 struct SwitchRecord {
   bool switched = false;
+  bool bits = false;  // phase 0 stored its mapping-0 tiles' top bits (switch_bits_mode)
   uint32_t spread = 0, nint = 0, units = 0;
   uint32_t nseg = 0;  // matrix-core form: the column segments per object phase 0 ran with
 };

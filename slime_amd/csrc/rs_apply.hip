@@ -435,6 +435,9 @@ bool queue_allowed(hipStream_t s) {
 }
 void set_queue_mode(int m) { g_queue_mode.store(m, std::memory_order_relaxed); }
 void set_pipelined_kernels(bool on) { g_pipelined.store(on ? 1 : 0, std::memory_order_relaxed); }
+static std::atomic<int> g_switch_bits{0};
+int switch_bits_mode() { return g_switch_bits.load(std::memory_order_relaxed); }
+void set_switch_bits_mode(int m) { g_switch_bits.store(m, std::memory_order_relaxed); }
 
 namespace {
 // The pipelined kernel addresses a shard with 32-bit byte offsets: it needs

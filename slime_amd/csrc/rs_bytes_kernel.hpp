@@ -659,6 +659,79 @@ __host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L
   return (uint32_t)(end_max / (64 * (uint64_t)U));
 }
 
+// Top bits of a mapping-0 tile, for the second pass's parity correction
+// (encode_bytes_fix_kernel): a lane's string holds, for vector u and column
+// c, the K top bits of its column as one K-bit field at bit (u*4 + c)*K (bit
+// j of the field = bit 31 of chunk j's packed word = bit 7 of the raw
+// little-endian load), so the correction reads a column's field as one table
+// index.  Planes of 32 bits per lane (plane q at tile + 256 q,
+// lane-contiguous), the last plane only as wide as the bits left: K/8 bytes
+// per column.
+template <int K, int U>
+struct TopBits {
+  static constexpr int kBits = K * U * 4;
+  static constexpr int kWords = (kBits + 31) / 32;
+  static constexpr int kLastBits = kBits - 32 * (kWords - 1);
+  static constexpr int kLastBytes = kLastBits <= 8 ? 1 : kLastBits <= 16 ? 2 : 4;
+  static constexpr uint64_t kTileBytes = 64ull * (4 * (kWords - 1) + kLastBytes);
+};
+// Widest code the correction takes: its table holds 2^K entries per row.
+constexpr int kTopBitsMaxK = 10;
+
+template <int K, int U>
+__device__ __forceinline__ void store_top_bits(const uint4 (&r)[U][K], uint8_t* __restrict__ tile, uint32_t lane) {
+  using T = TopBits<K, U>;
+  uint32_t w[T::kWords];
+#pragma unroll
+  for (int q = 0; q < T::kWords; ++q) w[q] = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t t[4] = {(r[u][j].x >> 7) & 1u, (r[u][j].y >> 7) & 1u, (r[u][j].z >> 7) & 1u,
+                             (r[u][j].w >> 7) & 1u};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = (u * 4 + c) * K + j;
+        w[b >> 5] |= t[c] << (b & 31);
+      }
+    }
+#pragma unroll
+  for (int q = 0; q + 1 < T::kWords; ++q)
+    __builtin_nontemporal_store(w[q], reinterpret_cast<uint32_t*>(tile + 256 * q) + lane);
+  uint8_t* const last = tile + 256 * (T::kWords - 1);
+  if constexpr (T::kLastBytes == 1)
+    last[lane] = (uint8_t)w[T::kWords - 1];
+  else if constexpr (T::kLastBytes == 2)
+    reinterpret_cast<uint16_t*>(last)[lane] = (uint16_t)w[T::kWords - 1];
+  else
+    __builtin_nontemporal_store(w[T::kWords - 1], reinterpret_cast<uint32_t*>(last) + lane);
+}
+
+template <int K, int U>
+__device__ __forceinline__ void load_top_bits(const uint8_t* __restrict__ tile, uint32_t lane,
+                                              uint32_t (&w)[TopBits<K, U>::kWords]) {
+  using T = TopBits<K, U>;
+#pragma unroll
+  for (int q = 0; q + 1 < T::kWords; ++q) w[q] = reinterpret_cast<const uint32_t*>(tile + 256 * q)[lane];
+  const uint8_t* const last = tile + 256 * (T::kWords - 1);
+  if constexpr (T::kLastBytes == 1)
+    w[T::kWords - 1] = last[lane];
+  else if constexpr (T::kLastBytes == 2)
+    w[T::kWords - 1] = reinterpret_cast<const uint16_t*>(last)[lane];
+  else
+    w[T::kWords - 1] = reinterpret_cast<const uint32_t*>(last)[lane];
+}
+
+// The K-bit field of vector u, column c from a lane's loaded planes.
+template <int K, int U>
+__device__ __forceinline__ uint32_t top_field(const uint32_t (&w)[TopBits<K, U>::kWords], int u, int c) {
+  const int b = (u * 4 + c) * K, q = b >> 5;
+  uint64_t v = w[q];
+  if (q + 1 < TopBits<K, U>::kWords) v |= (uint64_t)w[q + 1] << 32;
+  return (uint32_t)(v >> (b & 31)) & ((1u << K) - 1);
+}
+
 // MODE 0 (speculative) encode on the ticket walk: the interior tiles are
 // dealt as units; the few edge tiles and column tails of every object follow,
 // spread over all waves (mapping 0).  MapToGF's flags (map.go:35-62) are OR-ed
@@ -672,12 +745,17 @@ __host__ __device__ inline uint32_t encode_interior_tiles(uint64_t S, uint64_t L
 // from the one the object ends with -- the units encoded before the first
 // word >= p was seen -- instead of the whole object.  A stale flag read only
 // delays the switch: the record always tells what the unit wrote.
-template <int K, int U, int C, int NC>
-__global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
+//
+// BITS (encode_bytes_queue_bits_kernel): every interior tile encoded with
+// mapping 0 also stores its top bits (TopBits) at bits + (obj * nint + tile)
+// * kTileBytes, so phase 1 corrects the listed units' parity
+// (encode_bytes_fix_kernel) instead of re-encoding them.
+template <int K, int U, int C, int NC, bool BITS>
+__device__ __forceinline__ void encode_queue_body(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
-    uint32_t units) {
+    uint32_t units, uint8_t* __restrict__ bits) {
   const ObjWords ow{(S + 3) / 4, S % 4 ? 0xFFFFFFFFu << (8 * (4 - S % 4)) : 0xFFFFFFFFu};
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -718,6 +796,8 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
       sent = 0;
     }
     if (sw && first && lane == 0) record[(uint64_t)o * units + unit] = m ? 1 : 0;
+    if constexpr (BITS)
+      if (m == 0) store_top_bits<K, U>(r, bits + ((uint64_t)o * nint + t) * TopBits<K, U>::kTileBytes, lane);
     encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, m, rows, coeff, out_idx,
                                      t * (64 * U) + lane, nvec, fl);
     publish();
@@ -795,6 +875,26 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     const uint32_t f = f1.bits();
     if (f) atomicOr(&flags[o], f);  // per lane: tails are a handful of columns per object
   }
+}
+
+template <int K, int U, int C, int NC>
+__global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
+    uint32_t units) {
+  encode_queue_body<K, U, C, NC, false>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
+                                        ticket, spread, record, units, nullptr);
+}
+// The same with the top-bit store (record != nullptr, K <= kTopBitsMaxK).
+template <int K, int U, int C, int NC>
+__global__ __launch_bounds__(kBlock) void encode_bytes_queue_bits_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
+    uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
+    uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
+    uint32_t units, uint8_t* __restrict__ bits) {
+  encode_queue_body<K, U, C, NC, true>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
+                                       ticket, spread, record, units, bits);
 }
 
 // The redo list of a switched phase 0: every interior unit of an object whose
@@ -912,6 +1012,106 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
     load_data_symbols<K, false, false>(slot, chunk, L, col0, b, 1, ow, m, x, nullptr);
     fix_data_tail<K>(slot, chunk, L, col0, b, 1, ow, m, x);
     rows_out<K>(x, rows, coeff, out_idx, slot + (uint64_t)K * chunk, chunk, 4 * b, m, 1);
+  }
+}
+
+// Phase 1 after a phase 0 that stored its top bits: the listed interior units
+// (redo_list_kernel) are corrected in place instead of re-encoded.  Under
+// 1<<31 an interior symbol is x ^ 2^31 = x + 2^31 - 2^32 b = x + 2^31 - 5 b
+// (mod p), b = bit 31 of the packed word x, so parity row i becomes
+//   parity0 + 2^31 sum_j c_ij - 5 sum_j c_ij b_j   (mod p),
+// and the data chunks of an interior unit are the object's own bytes under
+// either mapping (MapFromGF(m, x ^ m) = x).  Each block first builds, for
+// four rows at a time, T_i[f] = that correction for every K-bit field f of
+// top bits (LDS), so a column costs one lookup per row.  A wave then takes
+// whole units (static share of the list): every tile's bit planes and four
+// parity rows loaded at once, corrected, stored back.  Per column 4r + K/8
+// bytes read and 4r written instead of the re-encode's 4K and 4r.  Edge tiles
+// and column tails stay with encode_bytes_redo_kernel.
+template <int K, int U, int C>
+__global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
+    uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t chunk, uint64_t col0, uint32_t rows,
+    const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping,
+    const uint8_t* __restrict__ bits, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+    uint32_t units, uint32_t nint) {
+  static_assert(K <= kTopBitsMaxK, "the correction table holds 2^K entries per row");
+  constexpr int KW = TopBits<K, U>::kWords;
+  constexpr uint32_t NF = 1u << K;
+  __shared__ uint32_t table[4][NF];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * kWaves;
+  const uint32_t n = *count;
+  for (uint32_t i0 = 0; i0 < rows; i0 += 4) {
+    for (uint32_t x = threadIdx.x; x < 4 * NF; x += kBlock) {
+      const uint32_t ii = x / NF, f = x % NF;
+      if (i0 + ii >= rows) continue;
+      const uint32_t* const c = coeff + (uint64_t)(i0 + ii) * kCoeffStride;  // reduced mod p by the plan
+      uint64_t csum = 0;
+      uint32_t acc = 0;
+      for (int j = 0; j < K; ++j) {
+        csum += c[j];
+        if ((f >> j) & 1u) {
+          const uint32_t t5 = fold96(5ull * c[j], 0);
+          const uint32_t d = t5 ? kP - t5 : 0u;  // -5 c_ij mod p
+          const uint64_t s2 = (uint64_t)acc + d;
+          acc = (uint32_t)(s2 >= kP ? s2 - kP : s2);
+        }
+      }
+      const uint64_t s2 = (uint64_t)acc + fold96((uint64_t)fold96(csum, 0) << 31, 0);  // + 2^31 sum_j c_ij
+      table[ii][f] = (uint32_t)(s2 >= kP ? s2 - kP : s2);
+    }
+    __syncthreads();
+    for (uint32_t e = wave; e < n; e += nwaves) {
+      const uint32_t v = list[e];
+      const uint32_t o = v / units, tb = apply::unit_tile_base<C>(v % units);
+      uint32_t cnt = tb < nint ? (nint - tb + 3) / 4 : 0;
+      if (cnt > C) cnt = C;
+      const uint32_t m = mapping[o];
+      uint8_t* const par = slots + (uint64_t)o * slot_stride + 4 * col0 + (uint64_t)K * chunk;
+      uint32_t tbits[C][KW];
+      uint4 pv[C][4][U];
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if ((uint32_t)i < cnt) {
+          load_top_bits<K, U>(bits + ((uint64_t)o * nint + tb + 4 * i) * TopBits<K, U>::kTileBytes, lane, tbits[i]);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+              if (i0 + ii < rows)
+                pv[i][ii][u] = apply::ld16_at<false>(
+                    reinterpret_cast<const uint32_t*>(par + (uint64_t)out_idx[i0 + ii] * chunk),
+                    ((tb + 4 * i) * (64 * U) + 64 * u + lane) << 4);
+        }
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        if ((uint32_t)i >= cnt) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          uint32_t f[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) f[c] = top_field<K, U>(tbits[i], u, c);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            if (i0 + ii >= rows) break;
+            const uint4 pw = pv[i][ii][u];
+            const uint32_t w[4] = {pw.x, pw.y, pw.z, pw.w};
+            uint32_t y[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {  // phase 0 stored BE(parity0), parity0 < p; entries < p
+              const uint64_t s2 = (uint64_t)be(w[c]) + table[ii][f[c]];
+              y[c] = be((uint32_t)(s2 >= kP ? s2 - kP : s2) ^ m);
+            }
+            const u32x4 out = {y[0], y[1], y[2], y[3]};
+            uint8_t* const orow = par + (uint64_t)out_idx[i0 + ii] * chunk;
+            __builtin_nontemporal_store(
+                out, reinterpret_cast<u32x4*>(orow + (uint32_t)(((tb + 4 * i) * (64 * U) + 64 * u + lane) << 4)));
+          }
+        }
+      }
+    }
+    __syncthreads();  // the table is rebuilt for the next four rows
   }
 }
 

@@ -15,13 +15,38 @@ namespace slime {
 // list (nobj x units words) and the per-unit mapping record (nobj x units
 // bytes) of a phase 0 on the ticket walk with C-tile units of U vectors.
 namespace bytes {
+// With top bits (switch_bits_wanted): the planes of every object's interior
+// tiles follow, 256 B-aligned (TopBits<K, U>::kTileBytes a tile).  Word 1 of
+// the header stays zero: the edge-only redo reads it as its list count.
 struct SwitchLayout {
   uint32_t spread = 0, nint = 0, units = 0;
   uint64_t bytes = 0;
+  uint64_t bits_off = 0;  // 0: no top bits
   uint32_t* count(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p); }
+  uint32_t* zero(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p) + 1; }
   uint32_t* list(uint8_t* p) const { return reinterpret_cast<uint32_t*>(p + 256); }
   uint8_t* record(uint8_t* p, uint32_t nobj) const { return p + 256 + 4ull * nobj * units; }
+  uint8_t* bits(uint8_t* p) const { return bits_off ? p + bits_off : nullptr; }
 };
+
+// Objects of at least this many bytes take the top-bit correction under
+// switch_bits_mode() 0.  A word of uniform bytes is >= p with probability
+// 5/2^32, so 1 GiB objects switch 27% of the time and redo, on the bench
+// data, 16-20% of the encode time; storing the bits costs the first pass
+// K/8 bytes a column (+2.6% at 10/14), and the correction moves 4r + K/8
+// bytes a redone column instead of 4(K + r): at 10/14 the second pass ran
+// 0.235 against 0.389 ms on the same list, at 8/12 with 256 MiB objects (7.5%
+// switch, redo 3.5%) the sum lost 1.2% (profiles/r06/s21_topbits/).
+constexpr uint64_t kTopBitsMinObject = 1ull << 30;
+template <int K>
+bool switch_bits_wanted(const BytesLaunch& a) {
+  if (K > kTopBitsMaxK) return false;
+  const int mode = switch_bits_mode();
+  return mode == 1 || (mode == 0 && a.S >= kTopBitsMinObject);
+}
+
+inline uint64_t bits_offset(uint32_t nobj, uint32_t units) { return (256 + 5ull * nobj * units + 255) & ~255ull; }
+
 template <int K, int U, int C>
 SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
   SwitchLayout l;
@@ -31,6 +56,10 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
   l.nint = encode_interior_tiles(a.S, a.L, a.col0, ncols, K, U);
   l.units = apply::walk_units<C>(l.nint, l.spread);
   l.bytes = 256 + 5ull * a.nobj * l.units;
+  if (switch_bits_wanted<K>(a) && l.nint) {
+    l.bits_off = bits_offset(a.nobj, l.units);
+    l.bytes = l.bits_off + (uint64_t)a.nobj * l.nint * TopBits<K, U>::kTileBytes;
+  }
   return l;
 }
 
@@ -61,13 +90,26 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
   l.nint = a.sw->nint;
   l.units = a.sw->units;
   uint32_t* count = l.count(a.scratch);
-  if (hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s)) return e;
+  // count and the zero word beside it
+  if (hipError_t e = hipMemsetAsync(count, 0, 2 * sizeof(uint32_t), s)) return e;
   const uint64_t batch_units = (uint64_t)a.nobj * l.units;
   const uint64_t lblocks = std::min<uint64_t>(1024, (batch_units + apply::kBlock - 1) / apply::kBlock);
   hipLaunchKernelGGL(redo_list_kernel<C>, dim3((uint32_t)std::max<uint64_t>(lblocks, 1)), dim3(apply::kBlock), 0, s,
                      l.record(a.scratch, a.nobj), a.mapping, a.flags, a.nobj, l.units, l.nint, l.list(a.scratch),
                      count);
   if (hipError_t e = hipGetLastError()) return e;
+  if constexpr (K <= kTopBitsMaxK) {
+    if (a.sw->bits) {
+      // The listed units corrected from phase 0's top bits; the redo kernel
+      // then walks an empty list (the zero word) and rewrites only the edge
+      // tiles and column tails of the objects mapped with 1<<31.
+      hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock), 0,
+                         s, a.slots, a.slot_stride, chunk_stride(a), a.col0, a.rows, a.coeff, a.out_idx, a.mapping,
+                         a.scratch + bits_offset(a.nobj, l.units), l.list(a.scratch), count, l.units, l.nint);
+      if (hipError_t e = hipGetLastError()) return e;
+      count = l.zero(a.scratch);
+    }
+  }
   hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock),
                      0, s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                      a.out_idx, a.flags, a.mapping, l.list(a.scratch), count, l.units);
@@ -83,12 +125,20 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
   const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
   if (!l.spread) return hipSuccess;
   uint8_t* record = a.scratch ? l.record(a.scratch, a.nobj) : nullptr;
+  uint8_t* bits = a.scratch ? l.bits(a.scratch) : nullptr;
+  const dim3 grid((uint32_t)queue_blocks(switch_grid<K>((uint64_t)a.nobj * l.units), (uint64_t)a.nobj * l.units));
   const hipError_t e = with_tickets(
       s,
       [&](uint32_t* set) {
-        hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>),
-                           dim3((uint32_t)queue_blocks(switch_grid<K>((uint64_t)a.nobj * l.units), (uint64_t)a.nobj * l.units)),
-                           dim3(apply::kBlock), 0, s,
+        if constexpr (K <= kTopBitsMaxK) {
+          if (bits) {
+            hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters>), grid, dim3(apply::kBlock), 0,
+                               s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows,
+                               a.coeff, a.out_idx, a.flags, set, l.spread, record, l.units, bits);
+            return hipGetLastError();
+          }
+        }
+        hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), grid, dim3(apply::kBlock), 0, s,
                            a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows, a.coeff,
                            a.out_idx, a.flags, set, l.spread, record, l.units);
         return hipGetLastError();
@@ -96,6 +146,7 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       launched);
   if (*launched && record && a.sw) {
     a.sw->switched = true;
+    a.sw->bits = bits != nullptr;
     a.sw->spread = l.spread;
     a.sw->nint = l.nint;
     a.sw->units = l.units;

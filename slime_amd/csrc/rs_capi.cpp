@@ -330,6 +330,15 @@ int slime_rs_kernel_schedule(int mode) {
   return 0;
 }
 
+int slime_rs_switch_bits(int mode) {
+  if (mode < 0) return switch_bits_mode();
+  if (mode > 2)
+    return fail(Status::InvalidArg,
+                "switch_bits: mode must be 0 (by object size), 1 (always correct) or 2 (always re-encode)");
+  set_switch_bits_mode(mode);
+  return 0;
+}
+
 int slime_rs_kernel_matrix_cores(int mode) {
   if (mode < 0) return matrix_core_mode();
   if (mode > 1) return fail(Status::InvalidArg, "kernel_matrix_cores: mode must be 0 (VALU) or 1 (matrix cores)");

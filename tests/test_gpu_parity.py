@@ -617,9 +617,33 @@ def kernel_form(request):
     N.lib.slime_rs_kernel_schedule(before[1])
 
 
+@pytest.fixture
+def switch_bits(request):
+    """The second pass of the byte encode (slime_rs_switch_bits): mode 0 by
+    object size (objects under 1 GiB here: the re-encode), 1 = always the
+    top-bit correction.  Restored afterwards."""
+    before = N.lib.slime_rs_switch_bits(-1)
+    yield lambda m: N.lib.slime_rs_switch_bits(m)
+    N.lib.slime_rs_switch_bits(before)
+
+
+def test_switch_bits_mode_round_trip(torch_dev, switch_bits):
+    assert switch_bits(-1) == 0
+    for m in (1, 2, 0):
+        assert switch_bits(m) == 0 and switch_bits(-1) == m
+    assert switch_bits(3) == N.ERR_INVALID_ARG and switch_bits(-1) == 0
+
+
+@pytest.mark.parametrize("bits", [0, 1], ids=["by_size", "topbits"])
 @pytest.mark.parametrize("need,total", [(2, 3), (4, 6), (8, 12), (10, 14), (3, 5), (16, 20), (17, 20), (33, 50)])
 @pytest.mark.parametrize("S", [1, 3, 4, 5, 31, 32, 33, 1000, 4096, 65537, 1 << 20, 3 * (1 << 20) + 7])
-def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total, S):
+def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, switch_bits, bits, need, total, S):
+    """Device writeChunks against the reference framing, every chunk byte, in
+    every kernel form; `topbits` corrects the switched units from stored top
+    bits (need <= 10) instead of re-encoding them."""
+    if bits and need > 10:
+        pytest.skip("the top-bit correction takes need <= 10")
+    assert switch_bits(bits) == 0
     torch = torch_dev
     from slime_amd import device as D
     rng = np.random.default_rng(S * 31 + need)
@@ -654,7 +678,8 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, need, total
                                                (25, 32, (3 << 20) + 1, 8), (40, 48, (4 << 20) + 2, 8),
                                                (64, 80, (8 << 20) + 3, 8), (80, 100, (6 << 20) + 1, 8),
                                                (33, 40, (2 << 20) + 7, 16), (72, 90, (5 << 20) + 2, 8)])
-def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
+@pytest.mark.parametrize("bits", [0, 1], ids=["by_size", "topbits"])
+def test_encode_objects_mid_object_switch(torch_dev, switch_bits, bits, need, total, S, nobj):
     """The dynamic-schedule encode (and the matrix-core encode of wide codes)
     switches an object to 1<<31 as soon as a word >= p has been seen and the
     second pass redoes only the units (tiles) encoded before that
@@ -662,7 +687,11 @@ def test_encode_objects_mid_object_switch(torch_dev, need, total, S, nobj):
     a quarter, half, 90 % and the last whole word, two such words, none, and
     one that needs the random fallback (a word >= p after a word 1<<31 cannot
     map); every chunk byte against the reference framing (map.go:15-67,
-    multi_store.go:526-554)."""
+    multi_store.go:526-554).  `topbits`: the second pass corrects the listed
+    units from the top bits the first pass stored (slime_rs_switch_bits(1))."""
+    if bits and need > 10:
+        pytest.skip("the top-bit correction takes need <= 10")
+    assert switch_bits(bits) == 0
     torch = torch_dev
     from slime_amd import device as D
     assert N.lib.slime_rs_kernel_pipeline(-1) == 1 and N.lib.slime_rs_kernel_schedule(-1) == 1

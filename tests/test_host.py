@@ -412,3 +412,46 @@ def test_proxy_load_crash_report_names_the_mapping():
            and int(ln.split()[1].split("-")[0], 16) <= fault < int(ln.split()[1].split("-")[1], 16)]
     assert hit and hit[0].split()[2] == "---p", hit
     assert "=== end of crash report" in err
+
+
+def test_top_bit_correction_matches_the_reencode():
+    """The byte encode's second pass may correct a switched unit's parity
+    instead of re-encoding it (encode_bytes_fix_kernel, rs_bytes_kernel.hpp):
+    parity under 1<<31 = parity0 + T_i[f], T_i[f] = 2^31 sum_j c_ij - 5 sum_{j
+    in f} c_ij (mod p), f = the column's top bits.  The table entry is built
+    here exactly as the kernel builds it (d_j = -5 c_j mod p summed with
+    conditional subtracts, then 2^31 sum_j c_j folded once) and checked
+    against a re-encode of x ^ 2^31 with the reference's arithmetic
+    (vector.go:90-102) on the encode rows of ParityMatrix."""
+    import random as _r
+    from oracle import oracle_py as OP
+    p = OP.MaxVal
+    rng = _r.Random(0x70B175)
+    for need, total in [(1, 2), (2, 3), (4, 6), (8, 12), (10, 14), (3, 10)]:
+        rows = OP.parity_matrix(need, total - need)[need:]
+        for _ in range(300):
+            x = [rng.getrandbits(32) for _ in range(need)]
+            if rng.random() < 0.3:  # words >= p and runs of top bits
+                x = [w | 0xFFFFFFF8 if rng.random() < 0.5 else w for w in x]
+            f = sum(((w >> 31) & 1) << j for j, w in enumerate(x))
+            for c in rows:
+                c = [v % p for v in c]
+                parity0 = 0
+                for w, cj in zip(x, c):
+                    parity0 = ((w * cj) % p + parity0) % p
+                want = 0
+                for w, cj in zip(x, c):
+                    want = (((w ^ (1 << 31)) * cj) % p + want) % p
+                acc, csum = 0, 0
+                for j, cj in enumerate(c):
+                    csum += cj
+                    if (f >> j) & 1:
+                        t5 = (5 * cj) % p
+                        d = p - t5 if t5 else 0
+                        acc = acc + d - p if acc + d >= p else acc + d
+                    assert acc < p
+                entry = acc + ((csum % p) << 31) % p
+                entry = entry - p if entry >= p else entry
+                got = parity0 + entry
+                got = got - p if got >= p else got
+                assert got == want, (need, total, x, c)

@@ -55,6 +55,8 @@ for step in "$@"; do
     pmc_c2) pmc pmc_c2_fetch FETCH_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 &&
             pmc pmc_c2_write WRITE_SIZE --preset c2 --steps 3 --warmup 1 $NOLEGS --bytes-path 0 ;;
     # second-pass walk variants (s19): the harness at commit b1d0ca6 only, its variants were not kept
+    # the byte encode's second pass: re-encode vs top-bit correction (tools/topbits_fix.*)
+    topbits) run topbits 500 python tools/topbits_fix.py --shapes c5,c3 --rounds 6 --fix-blocks 512,256 ;;
     tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
     bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;

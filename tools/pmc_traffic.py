@@ -104,7 +104,8 @@ def kernel_code(kernel: str, need: int) -> str | None:
     return kernel_code_id(os.path.join(ROOT, "slime_amd", "lib", "libslime_rs.so"), (f"{kernel}ILi{need}E",))
 
 
-BYTE_KERNELS = ("encode_bytes_queue_kernel", "encode_bytes_redo_kernel", "decode_bytes_queue_kernel")
+BYTE_KERNELS = ("encode_bytes_queue_kernel", "encode_bytes_queue_bits_kernel", "encode_bytes_fix_kernel",
+                "encode_bytes_redo_kernel", "decode_bytes_queue_kernel")
 
 
 def byte_kernels(fetch_dir, write_dir, config, session, existing=None):
