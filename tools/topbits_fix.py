@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """A/B of the byte encode's second pass: the product's re-encode of the units
 a switched object encoded with mapping 0, against a parity correction from
-top bits the first pass stored (tools/topbits_fix.hip).  In one process on
-one allocation per shape, alternating: first pass without / with the bit
-store (interior walk only), then the redo list and the re-encode / the
-correction.  The corrected chunks must equal the re-encoded ones on every
+top bits the first pass stored per tile or per walk unit
+(tools/topbits_fix.hip, the product kernels).  In one process on one
+allocation per shape, alternating: the first pass without / with the bit
+store, then the redo list and the re-encode / the correction (plus the
+edge-only redo).  The corrected chunks must equal the re-encoded ones on every
 object MapToGF maps to 0 or 1<<31.  Prints per-variant median ms.
 
     make tools/libtopbits.so && python tools/topbits_fix.py [--shapes c5,c3 --rounds 6]
@@ -30,20 +31,6 @@ from slime_amd import device as D  # noqa: E402
 SHAPES = {"c5": (1, 10, 14, 1024, 16, 256, 512), "c3": (0, 8, 12, 256, 128, 256, 512)}
 
 
-P = (1 << 32) - 5
-
-
-def fix_table(coeff: np.ndarray, need: int) -> np.ndarray:
-    """Per parity row: -5 c_ij mod p for j < need, and 2^31 sum_j c_ij mod p in word 15."""
-    t = np.zeros((coeff.shape[0], 16), dtype=np.uint32)
-    for i in range(coeff.shape[0]):
-        c = [int(x) % P for x in coeff[i, :need]]
-        for j, cj in enumerate(c):
-            t[i, j] = (-5 * cj) % P
-        t[i, 15] = ((1 << 31) * sum(c)) % P
-    return t
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="c5,c3")
@@ -54,7 +41,7 @@ def main():
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libtopbits.so"))
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.tbf_pass0.argtypes = [i32, i32, vp, u64, u64, u64, u64, u32, u32, vp, vp, vp, vp, u32, vp, vp, vp]
-    lib.tbf_second.argtypes = [i32, i32, vp, u64, u64, u64, u64, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    lib.tbf_second.argtypes = [i32, i32, vp, u64, u64, u64, u64, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
     lib.tbf_bits_bytes.restype = u64
     lib.tbf_bits_bytes.argtypes = [i32, u64, u64, u32]
     lib.tbf_units.restype = u32
@@ -72,7 +59,6 @@ def main():
         coeff = np.zeros((rows, 16), dtype=np.uint32)
         coeff[:, :need] = D.Plan.encode(need, total).coefficients()
         c_t = torch.from_numpy(coeff.view(np.int32).reshape(-1)).cuda()
-        d_t = torch.from_numpy(fix_table(coeff, need).view(np.int32).reshape(-1)).cuda()
         oi = torch.arange(rows, dtype=torch.int32, device="cuda")
         flags = torch.zeros(nobj, dtype=torch.int32, device="cuda")
         mapping = torch.zeros(nobj, dtype=torch.int32, device="cuda")
@@ -80,7 +66,7 @@ def main():
         units = lib.tbf_units(sid, S, L, nobj)
         record = torch.zeros(nobj * units, dtype=torch.uint8, device="cuda")
         lst = torch.zeros(nobj * units, dtype=torch.int32, device="cuda")
-        count = torch.zeros(1, dtype=torch.int32, device="cuda")
+        count = torch.zeros(2, dtype=torch.int32, device="cuda")
         bits = torch.zeros(lib.tbf_bits_bytes(sid, S, L, nobj), dtype=torch.uint8, device="cuda")
         par = slots.view(nobj, slot)[:, need * cs: total * cs]
         alg0 = nobj * 4 * L * total  # the first pass's algorithmic bytes (interior ~ all)
@@ -99,18 +85,17 @@ def main():
             ev2 = torch.cuda.Event(enable_timing=True)
             ev2.record(s)
             assert lib.tbf_second(sid, fix, slots.data_ptr(), slot, cs, L, S, nobj, rows, c_t.data_ptr(),
-                                  d_t.data_ptr(), oi.data_ptr(), mapping.data_ptr(), status.data_ptr(),
-                                  record.data_ptr(),
+                                  oi.data_ptr(), mapping.data_ptr(), status.data_ptr(), record.data_ptr(),
                                   bits.data_ptr(), lst.data_ptr(), count.data_ptr(), fblocks, s.cuda_stream) == 0
             ev[2].record(s)
             torch.cuda.synchronize()
             assert int(ticket.abs().sum().item()) == 0
-            return ev[0].elapsed_time(ev[1]), ev2.elapsed_time(ev[2]), int(count.item())
+            return ev[0].elapsed_time(ev[1]), ev2.elapsed_time(ev[2]), int(count[0].item())
 
         ok = None
         ref = None
         times = {}
-        variants = [(0, blocks)] + [(1, int(b)) for b in args.fix_blocks.split(",")]
+        variants = [(0, blocks)] + [(lay, int(b)) for lay in (1, 2) for b in args.fix_blocks.split(",")]
         for r in range(args.rounds + 1):
             for fix, fb in variants:
                 t0, t1, listed = run(fix, fb)
@@ -124,7 +109,7 @@ def main():
                     assert torch.equal(got, ref), (shape, fix, fb, "parity differs")
                 del got
                 if r:
-                    key = "re-encode" if not fix else f"correction b{fb}"
+                    key = "re-encode" if not fix else f"correction {('per tile', 'per unit')[fix - 1]} b{fb}"
                     times.setdefault(key, {"pass0": [], "second": [], "listed": []})
                     times[key]["pass0"].append(t0)
                     times[key]["second"].append(t1)
