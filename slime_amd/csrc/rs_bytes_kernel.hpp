@@ -732,54 +732,6 @@ __device__ __forceinline__ uint32_t top_field(const uint32_t (&w)[TopBits<K, U>:
   return (uint32_t)(v >> (b & 31)) & ((1u << K) - 1);
 }
 
-// The same fields per walk unit (C tiles tb + 4i, i < C): field (i*U + u)*4
-// + c at bit ((i*U + u)*4 + c)*K of a lane's string, kept in registers while
-// the wave walks the unit and stored once at its end as whole 256-byte
-// planes (two full lines per plane and wave).
-template <int K, int U, int C>
-struct UnitBits {
-  static constexpr int kBits = C * U * 4 * K;
-  static constexpr int kWords = (kBits + 31) / 32;
-  static constexpr uint64_t kUnitBytes = 256ull * kWords;
-};
-template <int K, int U, int C, int I>
-__device__ __forceinline__ void add_unit_bits(const uint4 (&r)[U][K], uint32_t (&w)[UnitBits<K, U, C>::kWords]) {
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t t[4] = {(r[u][j].x >> 7) & 1u, (r[u][j].y >> 7) & 1u, (r[u][j].z >> 7) & 1u,
-                             (r[u][j].w >> 7) & 1u};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int b = ((I * U + u) * 4 + c) * K + j;
-        w[b >> 5] |= t[c] << (b & 31);
-      }
-    }
-}
-// Tile i of the unit (wave-uniform): a branch per compile-time position.
-template <int K, int U, int C>
-__device__ __forceinline__ void add_unit_bits(const uint4 (&r)[U][K], uint32_t (&w)[UnitBits<K, U, C>::kWords],
-                                              uint32_t i) {
-  static_assert(C <= 6, "units of at most six tiles");
-  switch (i) {
-    case 0: add_unit_bits<K, U, C, 0>(r, w); break;
-    case 1: if constexpr (C > 1) add_unit_bits<K, U, C, 1>(r, w); break;
-    case 2: if constexpr (C > 2) add_unit_bits<K, U, C, 2>(r, w); break;
-    case 3: if constexpr (C > 3) add_unit_bits<K, U, C, 3>(r, w); break;
-    case 4: if constexpr (C > 4) add_unit_bits<K, U, C, 4>(r, w); break;
-    case 5: if constexpr (C > 5) add_unit_bits<K, U, C, 5>(r, w); break;
-    default: break;
-  }
-}
-template <int K, int U, int C>
-__device__ __forceinline__ uint32_t unit_field(const uint32_t (&w)[UnitBits<K, U, C>::kWords], int i, int u, int c) {
-  const int b = ((i * U + u) * 4 + c) * K, q = b >> 5;
-  uint64_t v = w[q];
-  if (q + 1 < UnitBits<K, U, C>::kWords) v |= (uint64_t)w[q + 1] << 32;
-  return (uint32_t)(v >> (b & 31)) & ((1u << K) - 1);
-}
-
 // MODE 0 (speculative) encode on the ticket walk: the interior tiles are
 // dealt as units; the few edge tiles and column tails of every object follow,
 // spread over all waves (mapping 0).  MapToGF's flags (map.go:35-62) are OR-ed
@@ -794,12 +746,14 @@ __device__ __forceinline__ uint32_t unit_field(const uint32_t (&w)[UnitBits<K, U
 // word >= p was seen -- instead of the whole object.  A stale flag read only
 // delays the switch: the record always tells what the unit wrote.
 //
-// TB (encode_bytes_queue_bits_kernel): every interior tile encoded with
-// mapping 0 also stores its top bits, so phase 1 corrects the listed units'
-// parity (encode_bytes_fix_kernel) instead of re-encoding them.  TB 1: per
-// tile (TopBits) at bits + (obj * nint + tile) * kTileBytes; TB 2: per unit
-// (UnitBits) at bits + (obj * units + unit) * kUnitBytes.
-template <int K, int U, int C, int NC, int TB>
+// BITS (encode_bytes_queue_bits_kernel): every interior tile encoded with
+// mapping 0 also stores its top bits (TopBits) at bits + (obj * nint + tile)
+// * kTileBytes, so phase 1 corrects the listed units' parity
+// (encode_bytes_fix_kernel) instead of re-encoding them.  Kept per tile:
+// buffering a unit's bits in registers and storing them as whole lines at the
+// unit's end cost the first pass the same (+2.4% vs +2.2% at 10/14,
+// profiles/r06/s22_layout/).
+template <int K, int U, int C, int NC, bool BITS>
 __device__ __forceinline__ void encode_queue_body(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
@@ -838,20 +792,6 @@ __device__ __forceinline__ void encode_queue_body(
       sent |= wf;
     }
   };
-  // TB 2: the current unit's top bits (mapping-0 units only) and where they go.
-  uint32_t ubw[TB == 2 ? UnitBits<K, U, C>::kWords : 1];
-  bool ub_on = false;
-  uint8_t* ub_at = nullptr;
-  auto flush_unit_bits = [&] {
-    if constexpr (TB == 2) {
-      if (ub_on) {
-#pragma unroll
-        for (int q = 0; q < UnitBits<K, U, C>::kWords; ++q)
-          __builtin_nontemporal_store(ubw[q], reinterpret_cast<uint32_t*>(ub_at + 256 * q) + lane);
-      }
-      ub_on = false;
-    }
-  };
   auto compute = [&](uint4(&r)[U][K], uint32_t o, uint32_t t, uint32_t m, bool first, uint32_t unit) {
     if (o != fobj) {
       fl = Flags();
@@ -859,18 +799,8 @@ __device__ __forceinline__ void encode_queue_body(
       sent = 0;
     }
     if (sw && first && lane == 0) record[(uint64_t)o * units + unit] = m ? 1 : 0;
-    if constexpr (TB == 1)
+    if constexpr (BITS)
       if (m == 0) store_top_bits<K, U>(r, bits + ((uint64_t)o * nint + t) * TopBits<K, U>::kTileBytes, lane);
-    if constexpr (TB == 2) {
-      if (first) {
-        flush_unit_bits();
-        ub_on = m == 0;
-        ub_at = bits + ((uint64_t)o * units + unit) * UnitBits<K, U, C>::kUnitBytes;
-#pragma unroll
-        for (int q = 0; q < UnitBits<K, U, C>::kWords; ++q) ubw[q] = 0;
-      }
-      if (ub_on) add_unit_bits<K, U, C>(r, ubw, (t - apply::unit_tile_base<C>(unit)) >> 2);
-    }
     encode_interior_tile<K, U, true>(r, window(o) + (uint64_t)K * chunk, chunk, m, rows, coeff, out_idx,
                                      t * (64 * U) + lane, nvec, fl);
     publish();
@@ -903,7 +833,6 @@ __device__ __forceinline__ void encode_queue_body(
         if (!w.live) break;
       }
     }
-    flush_unit_bits();
     w.finish();
   }
   // Edge tiles [nint, ntiles) of every object (encode_bytes_kernel's edge step).
@@ -957,18 +886,18 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_queue_kernel(
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
     uint32_t units) {
-  encode_queue_body<K, U, C, NC, 0>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
-                                    ticket, spread, record, units, nullptr);
+  encode_queue_body<K, U, C, NC, false>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
+                                        ticket, spread, record, units, nullptr);
 }
 // The same with the top-bit store (record != nullptr, K <= kTopBitsMaxK).
-template <int K, int U, int C, int NC, int TB>
+template <int K, int U, int C, int NC>
 __global__ __launch_bounds__(kBlock) void encode_bytes_queue_bits_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t L, uint64_t chunk, uint64_t col0, uint64_t ncols, uint64_t S,
     uint32_t nobj, uint32_t rows, const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx,
     uint32_t* __restrict__ flags, uint32_t* __restrict__ ticket, uint32_t spread, uint8_t* __restrict__ record,
     uint32_t units, uint8_t* __restrict__ bits) {
-  encode_queue_body<K, U, C, NC, TB>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
-                                     ticket, spread, record, units, bits);
+  encode_queue_body<K, U, C, NC, true>(slots, slot_stride, L, chunk, col0, ncols, S, nobj, rows, coeff, out_idx, flags,
+                                       ticket, spread, record, units, bits);
 }
 
 // The redo list of a switched phase 0: every interior unit of an object whose
@@ -1102,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_redo_kernel(
 // parity rows loaded at once, corrected, stored back.  Per column 4r + K/8
 // bytes read and 4r written instead of the re-encode's 4K and 4r.  Edge tiles
 // and column tails stay with encode_bytes_redo_kernel.
-template <int K, int U, int C, int TB>
+template <int K, int U, int C>
 __global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
     uint8_t* __restrict__ slots, uint64_t slot_stride, uint64_t chunk, uint64_t col0, uint32_t rows,
     const uint32_t* __restrict__ coeff, const uint32_t* __restrict__ out_idx, const uint32_t* __restrict__ mapping,
@@ -1110,7 +1039,6 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
     uint32_t units, uint32_t nint) {
   static_assert(K <= kTopBitsMaxK, "the correction table holds 2^K entries per row");
   constexpr int KW = TopBits<K, U>::kWords;
-  constexpr int UW = UnitBits<K, U, C>::kWords;
   constexpr uint32_t NF = 1u << K;
   __shared__ uint32_t table[4][NF];
   const uint32_t lane = threadIdx.x & 63;
@@ -1144,19 +1072,12 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
       if (cnt > C) cnt = C;
       const uint32_t m = mapping[o];
       uint8_t* const par = slots + (uint64_t)o * slot_stride + 4 * col0 + (uint64_t)K * chunk;
-      uint32_t tbits[TB == 1 ? C : 1][KW];
-      uint32_t ubits[UW];
-      if constexpr (TB == 2) {
-        const uint8_t* const at = bits + (uint64_t)v * UnitBits<K, U, C>::kUnitBytes;  // v = obj * units + unit
-#pragma unroll
-        for (int q = 0; q < UW; ++q) ubits[q] = reinterpret_cast<const uint32_t*>(at + 256 * q)[lane];
-      }
+      uint32_t tbits[C][KW];
       uint4 pv[C][4][U];
 #pragma unroll
       for (int i = 0; i < C; ++i)
         if ((uint32_t)i < cnt) {
-          if constexpr (TB == 1)
-            load_top_bits<K, U>(bits + ((uint64_t)o * nint + tb + 4 * i) * TopBits<K, U>::kTileBytes, lane, tbits[i]);
+          load_top_bits<K, U>(bits + ((uint64_t)o * nint + tb + 4 * i) * TopBits<K, U>::kTileBytes, lane, tbits[i]);
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -1173,12 +1094,7 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_fix_kernel(
         for (int u = 0; u < U; ++u) {
           uint32_t f[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if constexpr (TB == 1)
-              f[c] = top_field<K, U>(tbits[i], u, c);
-            else
-              f[c] = unit_field<K, U, C>(ubits, i, u, c);
-          }
+          for (int c = 0; c < 4; ++c) f[c] = top_field<K, U>(tbits[i], u, c);
 #pragma unroll
           for (int ii = 0; ii < 4; ++ii) {
             if (i0 + ii >= rows) break;

@@ -38,9 +38,6 @@ struct SwitchLayout {
 // 0.235 against 0.389 ms on the same list, at 8/12 with 256 MiB objects (7.5%
 // switch, redo 3.5%) the sum lost 1.2% (profiles/r06/s21_topbits/).
 constexpr uint64_t kTopBitsMinObject = 1ull << 30;
-// Where the first pass keeps the bits: 1 per tile, 2 per walk unit
-// (rs_bytes_kernel.hpp TopBits / UnitBits).
-constexpr int kTopBitsLayout = 1;
 template <int K>
 bool switch_bits_wanted(const BytesLaunch& a) {
   if (K > kTopBitsMaxK) return false;
@@ -61,8 +58,7 @@ SwitchLayout switch_layout(const BytesLaunch& a, uint64_t ncols, hipStream_t s) 
   l.bytes = 256 + 5ull * a.nobj * l.units;
   if (switch_bits_wanted<K>(a) && l.nint) {
     l.bits_off = bits_offset(a.nobj, l.units);
-    l.bytes = l.bits_off + (kTopBitsLayout == 1 ? (uint64_t)a.nobj * l.nint * TopBits<K, U>::kTileBytes
-                                                : (uint64_t)a.nobj * l.units * UnitBits<K, U, C>::kUnitBytes);
+    l.bytes = l.bits_off + (uint64_t)a.nobj * l.nint * TopBits<K, U>::kTileBytes;
   }
   return l;
 }
@@ -107,7 +103,7 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
       // The listed units corrected from phase 0's top bits; the redo kernel
       // then walks an empty list (the zero word) and rewrites only the edge
       // tiles and column tails of the objects mapped with 1<<31.
-      hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C, kTopBitsLayout>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock), 0,
+      hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C>), dim3(switch_grid<K>(batch_units)), dim3(apply::kBlock), 0,
                          s, a.slots, a.slot_stride, chunk_stride(a), a.col0, a.rows, a.coeff, a.out_idx, a.mapping,
                          a.scratch + bits_offset(a.nobj, l.units), l.list(a.scratch), count, l.units, l.nint);
       if (hipError_t e = hipGetLastError()) return e;
@@ -136,7 +132,7 @@ hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t
       [&](uint32_t* set) {
         if constexpr (K <= kTopBitsMaxK) {
           if (bits) {
-            hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters, kTopBitsLayout>), grid, dim3(apply::kBlock), 0,
+            hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters>), grid, dim3(apply::kBlock), 0,
                                s, a.slots, a.slot_stride, a.L, chunk_stride(a), a.col0, ncols, a.S, a.nobj, a.rows,
                                a.coeff, a.out_idx, a.flags, set, l.spread, record, l.units, bits);
             return hipGetLastError();

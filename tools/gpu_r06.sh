@@ -57,6 +57,8 @@ for step in "$@"; do
     # second-pass walk variants (s19): the harness at commit b1d0ca6 only, its variants were not kept
     # the byte encode's second pass: re-encode vs top-bit correction (tools/topbits_fix.*)
     topbits) run topbits 500 python tools/topbits_fix.py --shapes c5,c3 --rounds 6 --fix-blocks 512,256 ;;
+    # the same through the product API (slime_rs_switch_bits 2 vs 1) on the bench's data
+    topbits_ab) run topbits_ab 500 python tools/topbits_ab.py --shapes c5,c3,c5_512 --rounds 8 ;;
     tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
     bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;

@@ -2,12 +2,10 @@
 // 10 on the ticket walk: the product kernels (rs_bytes_kernel.hpp) launched
 // as rs_bytes_launch.hpp launches them, with the first pass storing no top
 // bits (then the re-encode of the listed units), or storing them per tile
-// (TopBits, layout 1) or per walk unit (UnitBits, layout 2) for
-// encode_bytes_fix_kernel.  tools/topbits_fix.py drives it and checks every
-// variant's chunks against the re-encode's.
+// (TopBits, layout 1) for encode_bytes_fix_kernel.  tools/topbits_fix.py
+// drives it and checks every variant's chunks against the re-encode's.  (A
+// per-unit layout, commit 34ad9c0, measured the same and was removed.)
 #include <hip/hip_runtime.h>
-
-#include <algorithm>
 
 #include "rs_bytes_launch.hpp"
 
@@ -39,14 +37,10 @@ int pass0(int layout, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64_
   if (layout == 0)
     hipLaunchKernelGGL((encode_bytes_queue_kernel<K, U, C, kQueueCounters>), grid, block, 0, s, slots, stride, L,
                        cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket, g.spread, record, g.units);
-  else if (layout == 1)
-    hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters, 1>), grid, block, 0, s, slots, stride,
-                       L, cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket, g.spread, record,
-                       g.units, bits);
   else
-    hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters, 2>), grid, block, 0, s, slots, stride,
-                       L, cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket, g.spread, record,
-                       g.units, bits);
+    hipLaunchKernelGGL((encode_bytes_queue_bits_kernel<K, U, C, kQueueCounters>), grid, block, 0, s, slots, stride, L,
+                       cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, flags, ticket, g.spread, record, g.units,
+                       bits);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -62,13 +56,11 @@ int second(int layout, uint8_t* slots, uint64_t stride, uint64_t cstride, uint64
   hipLaunchKernelGGL(redo_list_kernel<C>, dim3(1024), dim3(apply::kBlock), 0, s, record, mapping, status, nobj, g.units,
                      g.nint, list, count);
   const uint32_t* n = count;
-  if (layout == 1)
-    hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C, 1>), dim3(blocks), dim3(apply::kBlock), 0, s, slots, stride,
+  if (layout) {
+    hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C>), dim3(blocks), dim3(apply::kBlock), 0, s, slots, stride,
                        cstride, (uint64_t)0, rows, coeff, out_idx, mapping, bits, list, count, g.units, g.nint);
-  if (layout == 2)
-    hipLaunchKernelGGL((encode_bytes_fix_kernel<K, U, C, 2>), dim3(blocks), dim3(apply::kBlock), 0, s, slots, stride,
-                       cstride, (uint64_t)0, rows, coeff, out_idx, mapping, bits, list, count, g.units, g.nint);
-  if (layout) n = count + 1;
+    n = count + 1;
+  }
   hipLaunchKernelGGL((encode_bytes_redo_kernel<K, U, C>), dim3(blocks), dim3(apply::kBlock), 0, s, slots, stride, L,
                      cstride, (uint64_t)0, L, S, nobj, rows, coeff, out_idx, status, mapping, list, n, g.units);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -96,18 +88,10 @@ extern "C" int tbf_second(int shape, int layout, uint8_t* slots, uint64_t stride
   return -3;
 }
 
-// Bytes of the top-bit buffer (the larger of the two layouts) and units per object.
+// Bytes of the top-bit buffer and units per object.
 extern "C" uint64_t tbf_bits_bytes(int shape, uint64_t S, uint64_t L, uint32_t nobj) {
-  if (shape == 0) {
-    const Geo g = geo<8, 2, 3>(S, L, nobj);
-    return std::max((uint64_t)nobj * g.nint * TopBits<8, 2>::kTileBytes,
-                    (uint64_t)nobj * g.units * UnitBits<8, 2, 3>::kUnitBytes);
-  }
-  if (shape == 1) {
-    const Geo g = geo<10, 1, 6>(S, L, nobj);
-    return std::max((uint64_t)nobj * g.nint * TopBits<10, 1>::kTileBytes,
-                    (uint64_t)nobj * g.units * UnitBits<10, 1, 6>::kUnitBytes);
-  }
+  if (shape == 0) return (uint64_t)nobj * geo<8, 2, 3>(S, L, nobj).nint * TopBits<8, 2>::kTileBytes;
+  if (shape == 1) return (uint64_t)nobj * geo<10, 1, 6>(S, L, nobj).nint * TopBits<10, 1>::kTileBytes;
   return 0;
 }
 extern "C" uint32_t tbf_units(int shape, uint64_t S, uint64_t L, uint32_t nobj) {

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the byte encode's second pass: the product's re-encode of the units
 a switched object encoded with mapping 0, against a parity correction from
-top bits the first pass stored per tile or per walk unit
-(tools/topbits_fix.hip, the product kernels).  In one process on one
+top bits the first pass stored (tools/topbits_fix.hip, the product
+kernels).  In one process on one
 allocation per shape, alternating: the first pass without / with the bit
 store, then the redo list and the re-encode / the correction (plus the
 edge-only redo).  The corrected chunks must equal the re-encoded ones on every
@@ -95,7 +95,7 @@ def main():
         ok = None
         ref = None
         times = {}
-        variants = [(0, blocks)] + [(lay, int(b)) for lay in (1, 2) for b in args.fix_blocks.split(",")]
+        variants = [(0, blocks)] + [(1, int(b)) for b in args.fix_blocks.split(",")]
         for r in range(args.rounds + 1):
             for fix, fb in variants:
                 t0, t1, listed = run(fix, fb)
@@ -109,7 +109,7 @@ def main():
                     assert torch.equal(got, ref), (shape, fix, fb, "parity differs")
                 del got
                 if r:
-                    key = "re-encode" if not fix else f"correction {('per tile', 'per unit')[fix - 1]} b{fb}"
+                    key = "re-encode" if not fix else f"correction b{fb}"
                     times.setdefault(key, {"pass0": [], "second": [], "listed": []})
                     times[key]["pass0"].append(t0)
                     times[key]["second"].append(t1)
