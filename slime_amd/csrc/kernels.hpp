@@ -209,6 +209,7 @@ struct BytesLaunch {
   // if sw->switched) redoes just the units that used the wrong mapping.
   // Null: phase 1 re-encodes whole objects.
   uint8_t* scratch = nullptr;
+  uint64_t scratch_bytes = 0;  // bytes at scratch: a layout that needs more runs without the record
   SwitchRecord* sw = nullptr;
   uint64_t cstride = 0;  // bytes between a slot's chunks (0: 4L, the wire layout)
   // Matrix-core form (rs_bytes_mfma.hip): the plan's byte-order digit table

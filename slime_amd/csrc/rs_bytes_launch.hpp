@@ -122,10 +122,20 @@ hipError_t launch_redo(const BytesLaunch& a, uint64_t ncols, hipStream_t s) {
 template <int K, int U, int C>
 hipError_t launch_encode_queue(const BytesLaunch& a, uint64_t ncols, hipStream_t s, bool* launched) {
   *launched = false;
-  const SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
+  SwitchLayout l = switch_layout<K, U, C>(a, ncols, s);
   if (!l.spread) return hipSuccess;
-  uint8_t* record = a.scratch ? l.record(a.scratch, a.nobj) : nullptr;
-  uint8_t* bits = a.scratch ? l.bits(a.scratch) : nullptr;
+  // The caller sized the scratch by encode_switch_bytes; the top-bit choice
+  // reads process-wide state (switch_bits_mode) that may have changed since,
+  // so the layout is checked against the bytes actually held: without room
+  // for the bits the switch runs without them, without room for the record
+  // the second pass re-encodes whole objects.
+  if (a.scratch && l.bytes > a.scratch_bytes && l.bits_off) {
+    l.bytes = 256 + 5ull * a.nobj * l.units;
+    l.bits_off = 0;
+  }
+  const bool fits = a.scratch && l.bytes <= a.scratch_bytes;
+  uint8_t* record = fits ? l.record(a.scratch, a.nobj) : nullptr;
+  uint8_t* bits = fits ? l.bits(a.scratch) : nullptr;
   const dim3 grid((uint32_t)queue_blocks(switch_grid<K>((uint64_t)a.nobj * l.units), (uint64_t)a.nobj * l.units));
   const hipError_t e = with_tickets(
       s,

@@ -639,6 +639,7 @@ struct ScratchLease {
     return 0;
   }
   uint8_t* ptr() const { return held ? buf.p : nullptr; }
+  uint64_t bytes() const { return held ? buf.bytes : 0; }
   // Back to the pool behind an event on `s` (after the sequence's last launch).
   void release(hipStream_t s) {
     if (!held) return;
@@ -681,6 +682,7 @@ extern "C" int slime_rs_encode_objects_phased(slime_rs_plan_t plan, uint8_t* slo
   if (int rc = sc.take(plan->device, encode_switch_bytes(a0, s), s)) return rc;
   SwitchRecord sw;
   a0.scratch = sc.ptr();
+  a0.scratch_bytes = sc.bytes();
   a0.sw = &sw;
   HIP_TRY(launch_encode_bytes(a0, s));
   HIP_TRY(launch_select_mapping(mapping, status, (uint32_t)nobj, s));
@@ -688,6 +690,7 @@ extern "C" int slime_rs_encode_objects_phased(slime_rs_plan_t plan, uint8_t* slo
   BytesLaunch a1 = bytes_launch(plan, slots, slot_stride, chunk_stride, L, object_size, nobj, 1, status, mapping);
   if (sw.switched) {
     a1.scratch = sc.ptr();
+    a1.scratch_bytes = sc.bytes();
     a1.sw = &sw;
   }
   HIP_TRY(launch_encode_bytes(a1, s));
