@@ -673,6 +673,11 @@ def test_encode_objects_matches_write_chunks(torch_dev, kernel_form, switch_bits
 @pytest.mark.parametrize("need,total,S,nobj", [(8, 12, 16 << 20, 12), (10, 14, (8 << 20) + 5, 12),
                                                (4, 6, (6 << 20) + 3, 18), (20, 24, (4 << 20) + 1, 6),
                                                (3, 5, 1 << 20, 36), (16, 20, (5 << 20) + 2, 6),
+                                               # more than four parity rows (the correction's table is
+                                               # rebuilt per four rows), and need 1 / 9 (narrow and odd
+                                               # bit fields)
+                                               (6, 14, (3 << 20) + 1, 8), (2, 9, (2 << 20) + 6, 8),
+                                               (1, 3, (1 << 20) + 2, 8), (9, 16, (4 << 20) + 3, 8),
                                                # the matrix-core encode's switch (rs_bytes_mfma.hip): 2..5 K
                                                # steps, four- and two-column lane tiles, many segments
                                                (25, 32, (3 << 20) + 1, 8), (40, 48, (4 << 20) + 2, 8),
