@@ -135,7 +135,11 @@ hipError_t launch_pipe(const ApplyLaunch& a, hipStream_t stream) {
 // (s39_queue3/, s41_queue4/); 16/20 3.737 -> 3.600, C2 (4/6) 0.586 -> 0.575
 // (s42_queuek/).  Geometry: 256 blocks (one per CU) for every k; U = 4 up to
 // k = 4, 3 up to 12, 1 above; a unit is C tiles with C x U about 6 (C = 2 at
-// U >= 3), dealt over kQueueCounters ticket counters.
+// U = 3), dealt over kQueueCounters ticket counters.  At k <= 4 a unit is
+// three tiles: the narrow codes' tiles are short (24 KiB a wave at 4/6), and
+// fewer draws per byte ran 4/6 at 32 objects +0.4 to +1.2% and slime's default
+// 3/5 +1.1 to +2.0% on the stamped twin (64 objects +0 to +0.8%; four and six
+// tiles no better; profiles/r06/s30_c2unit/).
 constexpr uint64_t kQueueBlocks = 256;
 template <int K>
 constexpr int queue_unroll() {
@@ -143,7 +147,7 @@ constexpr int queue_unroll() {
 }
 template <int K>
 constexpr int queue_unit_tiles() {
-  return queue_unroll<K>() >= 3 ? 2 : 6 / queue_unroll<K>();
+  return K <= 4 ? 3 : queue_unroll<K>() >= 3 ? 2 : 6 / queue_unroll<K>();
 }
 
 template <int K>

@@ -30,7 +30,7 @@ int launch(const uint32_t* in, uint32_t* out, uint64_t io, uint64_t is, uint64_t
 }
 }  // namespace
 
-// k = 3 (slime's default 3/5: U 4, C 2), 4 (C2: U 4, C 2), 8 (C3: U 3, C 2), 10 (C5: U 3, C 2),
+// k = 3 (slime's default 3/5: U 4, C 3), 4 (C2: U 4, C 3), 8 (C3: U 3, C 2), 10 (C5: U 3, C 2),
 // 12 (U 3, C 2) or 16 (U 1, C 6): the product's queue geometry (rs_apply.hip queue_unroll /
 // queue_unit_tiles).
 // ticket: a zeroed counter set of kQueueCounters + 1 lines of 64 words (each
@@ -43,10 +43,49 @@ extern "C" int cs_launch(int k, const uint32_t* in, uint32_t* out, uint64_t io, 
                          uint32_t blocks) {
   hipStream_t s = (hipStream_t)stream;
   if (k == 3)
-    return launch<3, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+    return launch<3, 4, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
                            (uint64_t*)stamps, nwaves, spread, blocks);
   if (k == 4)
+    return launch<4, 4, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  // the round-6 s30 product form, units of two tiles: 1104 (4/6), 1203 (3/5)
+  if (k == 1104)
     return launch<4, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 1203)
+    return launch<3, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  // 4/6 unroll / unit variants (k code 100 * variant + 4): U 2 C 3, U 3 C 2, U 1 C 6, U 6 C 1, U 4 C 1, U 4 C 3,
+  // U 4 C 4, U 4 C 6; 3/5: 903 U 4 C 3, 1003 U 4 C 4
+  if (k == 104)
+    return launch<4, 2, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 204)
+    return launch<4, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 304)
+    return launch<4, 1, 6>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 404)
+    return launch<4, 6, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 504)
+    return launch<4, 4, 1>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 604)
+    return launch<4, 4, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 704)
+    return launch<4, 4, 4>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 804)
+    return launch<4, 4, 6>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 903)  // 3/5 (slime's default) with units of 3 tiles
+    return launch<3, 4, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 1003)
+    return launch<3, 4, 4>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
                            (uint64_t*)stamps, nwaves, spread, blocks);
   if (k == 12)
     return launch<12, 3, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,

@@ -97,7 +97,8 @@ def main():
     ap.add_argument("--nobj", type=str, default="32,64,128")
     ap.add_argument("--reps", type=int, default=12)
     ap.add_argument("--geometry", type=str, default="0:0",
-                    help="stamped twin geometries spread:blocks (0 = the product's rule), comma list; the split is "
+                    help="stamped twin geometries spread:blocks[:kcode] (0 = the product's rule; kcode selects a "
+                         "unroll/unit variant of tools/c2_stamps.hip, default need), comma list; the split is "
                          "reported for the first")
     args = ap.parse_args()
     need, total = args.need, args.total
@@ -132,10 +133,11 @@ def main():
             enc(b, lay, b, lay, L, nobj, stream=s, dst_offset=need * SS)
 
         nw = ctypes.c_uint32(0)
-        geos = [tuple(int(v) for v in g.split(":")) for g in args.geometry.split(",")]
+        geos = [tuple(int(v) for v in (g + ":" + str(need) if g.count(":") == 1 else g).split(":"))
+                for g in args.geometry.split(",")]
         nws = {}
         for g in geos:
-            rc = lib.cs_launch(need, b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
+            rc = lib.cs_launch(g[2], b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
                                ii.data_ptr(), oi.data_ptr(), L, nobj, r, ctypes.c_void_p(s.cuda_stream),
                                ticket.data_ptr(), None, ctypes.byref(nw), g[0], g[1])
             assert rc == 0, rc
@@ -144,7 +146,7 @@ def main():
 
         def stamped_at(g):
             def fn():
-                rc = lib.cs_launch(need, b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
+                rc = lib.cs_launch(g[2], b.data_ptr(), b.data_ptr(), total * SS, SS, total * SS, SS, c_t.data_ptr(),
                                    ii.data_ptr(), oi.data_ptr(), L, nobj, r, ctypes.c_void_p(s.cuda_stream),
                                    ticket.data_ptr(), st.data_ptr(), ctypes.byref(nw), g[0], g[1])
                 assert rc == 0, rc
@@ -160,7 +162,7 @@ def main():
         # included), never the host's enqueue latency.
         times, recs, good = {}, [], True
         runs = [("product", product), ("stamped", stamped)] + \
-            [(f"stamped_{g[0]}:{g[1]}", stamped_at(g)) for g in geos[1:]] + [("product2", product)]
+            [(f"stamped_{g[0]}:{g[1]}:{g[2]}", stamped_at(g)) for g in geos[1:]] + [("product2", product)]
         for name, fn in runs:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
             ev[0].record(s)

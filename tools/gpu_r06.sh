@@ -59,6 +59,22 @@ for step in "$@"; do
     topbits) run topbits 500 python tools/topbits_fix.py --shapes c5,c3 --rounds 6 --fix-blocks 512,256 ;;
     # the same through the product API (slime_rs_switch_bits 2 vs 1) on the bench's data
     topbits_ab) run topbits_ab 500 python tools/topbits_ab.py --shapes c5,c3,c5_512 --rounds 8 ;;
+    # 4/6 (C2) unroll / unit variants of the queue apply on the stamped twin, twice
+    c2var) C="python tools/c2_stamps.py --need 4 --total 6 --mib 64"
+      G="0:0,0:0:104,0:0:204,0:0:304,0:0:404,0:0:504,0:0:604,0:512:104,0:512:304,0:1024:304,0:512:204"
+      run c2var_1 300 $C --nobj 32 --reps 16 --geometry $G &&
+      run c2var_2 300 $C --nobj 32 --reps 16 --geometry $G &&
+      run c2var_64 300 $C --nobj 64 --reps 12 --geometry $G ;;
+    # the product's three-tile units at k <= 4 against the old two-tile form (twin), 4/6 and 3/5
+    c2unit_check) C="python tools/c2_stamps.py --mib 64"
+      run c2chk_46 300 $C --need 4 --total 6 --nobj 32,64 --reps 16 --geometry 0:0,0:0:1104 &&
+      run c2chk_35 300 $C --need 3 --total 5 --nobj 32,64 --reps 16 --geometry 0:0,0:0:1203 ;;
+    # units of 3 / 4 / 6 tiles at 4/6 and 3/5 (the C of the queue walk), twice, and 8/12 for reference
+    c2unit) C="python tools/c2_stamps.py --mib 64"
+      for rep in 1 2; do
+        run c2unit_46_$rep 300 $C --need 4 --total 6 --nobj 32,64 --reps 16 --geometry 0:0,0:0:604,0:0:704,0:0:804 &&
+        run c2unit_35_$rep 300 $C --need 3 --total 5 --nobj 32,64 --reps 16 --geometry 0:0,0:0:903,0:0:1003 || exit 1
+      done ;;
     tests_phased) run pytest_phased 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k "phased" ;;
     bpmc_c3) pmc bpmc_c3_fetch FETCH_SIZE --steps 3 --warmup 1 $NOLEGS &&
              pmc bpmc_c3_write WRITE_SIZE --steps 3 --warmup 1 $NOLEGS ;;
