@@ -48,6 +48,19 @@ extern "C" int cs_launch(int k, const uint32_t* in, uint32_t* out, uint64_t io, 
   if (k == 4)
     return launch<4, 4, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
                            (uint64_t*)stamps, nwaves, spread, blocks);
+  // 8/12 and 10/14 unit variants: 1308 U 3 C 3, 1408 U 3 C 4, 1508 U 2 C 3, 1310 U 3 C 3
+  if (k == 1308)
+    return launch<8, 3, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 1408)
+    return launch<8, 3, 4>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 1508)
+    return launch<8, 2, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                           (uint64_t*)stamps, nwaves, spread, blocks);
+  if (k == 1310)
+    return launch<10, 3, 3>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,
+                            (uint64_t*)stamps, nwaves, spread, blocks);
   // the round-6 s30 product form, units of two tiles: 1104 (4/6), 1203 (3/5)
   if (k == 1104)
     return launch<4, 4, 2>(in, out, io, is, oo, os, coeff, ii, oi, ncols, nobj, rows, s, (uint32_t*)ticket,

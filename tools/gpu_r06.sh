@@ -69,6 +69,13 @@ for step in "$@"; do
     c2unit_check) C="python tools/c2_stamps.py --mib 64"
       run c2chk_46 300 $C --need 4 --total 6 --nobj 32,64 --reps 16 --geometry 0:0,0:0:1104 &&
       run c2chk_35 300 $C --need 3 --total 5 --nobj 32,64 --reps 16 --geometry 0:0,0:0:1203 ;;
+    # unit size at 8/12 (C3, 64 MiB shards) and 10/14 on the twin, twice
+    c3unit) C="python tools/c2_stamps.py"
+      for rep in 1 2; do
+        run c3unit_$rep 300 $C --need 8 --total 12 --mib 256 --nobj 128 --reps 6 --geometry 0:0,0:0:1308,0:0:1408,0:0:1508 &&
+        run c3unit_ns64_$rep 300 $C --need 8 --total 12 --mib 512 --nobj 64 --reps 6 --geometry 0:0,0:0:1308,0:0:1408 &&
+        run c5unit_$rep 300 $C --need 10 --total 14 --mib 1024 --nobj 16 --reps 6 --geometry 0:0,0:0:1310 || exit 1
+      done ;;
     # units of 3 / 4 / 6 tiles at 4/6 and 3/5 (the C of the queue walk), twice, and 8/12 for reference
     c2unit) C="python tools/c2_stamps.py --mib 64"
       for rep in 1 2; do
