@@ -340,9 +340,9 @@ int slime_rs_device_alloc(int device, uint64_t bytes, void **ptr);
  * SLIME_RS_PLACEMENT_PROBE_GIB GiB (default 16; 0 disables) are probed when
  * created: the apply kernel's C3-shaped read/write walk over the whole buffer
  * (GB/s of algorithmic traffic).  Below SLIME_RS_PLACEMENT_MIN_GBS (default
- * 6100) the allocator tries up to two other placements (1 GiB chunks, then
- * one hipMalloc), holding the first meanwhile, and keeps the fastest
- * (DESIGN.md "Placement"). */
+ * 6350, the top of the rates seen, so in practice always) the allocator tries
+ * up to two other placements (1 GiB chunks, then one hipMalloc), holding the
+ * first meanwhile, and keeps the fastest (DESIGN.md "Placement"). */
 typedef struct slime_rs_alloc_info {
   int kind;                /* kept placement: 0 = physical chunks mapped into one range, 1 = hipMalloc */
   int probes;              /* placements probed (0: buffer too small, not probed) */
@@ -357,15 +357,16 @@ int slime_rs_device_alloc_info(const void *ptr, slime_rs_alloc_info_t *info);
  * algorithmic traffic of the C3-shaped read/write walk, 0 when the range is
  * too small to measure (under ~400 MB).  The physical placement of a large
  * buffer fixes, for its whole life, whether the kernels stream in the fast
- * mode (~6.2 TB/s at C3) or the slow one (~5.3): a buffer that probes below
- * slime_rs_placement_threshold() is worth re-allocating, or allocating with
+ * mode (~6.0-6.4 TB/s at C3) or the slow one (~5.3-5.7): a buffer that
+ * probes in the slow mode is worth re-allocating, or allocating with
  * slime_rs_device_alloc, which probes and re-places by itself.
  * OVERWRITES the range: probe a buffer before filling it.  The range must lie
  * inside one device allocation on `device` (else SLIME_RS_ERR_INVALID_ARG).
  * Synchronous. */
 int slime_rs_probe_placement(void *ptr, uint64_t bytes, int device, double *gbs);
-/* The fast-mode threshold of the probe, GB/s (env SLIME_RS_PLACEMENT_MIN_GBS,
- * default 6100: the C3 apply kernel at <= 8.45 ms). */
+/* The allocator's re-placement threshold, GB/s (env SLIME_RS_PLACEMENT_MIN_GBS,
+ * default 6350: a first placement below it is re-placed, keeping the fastest
+ * of up to three; 6350 is about the C3 apply kernel at 8.2 ms). */
 double slime_rs_placement_threshold(void);
 /* Frees a buffer from slime_rs_device_alloc (its base).  Waits for the device
  * first (hipDeviceSynchronize), so work still queued on it cannot fault.

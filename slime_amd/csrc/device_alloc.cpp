@@ -179,9 +179,11 @@ extern "C" {
 
 // Placement: a buffer of at least SLIME_RS_PLACEMENT_PROBE_GIB (default 16)
 // is probed once created (placement_probe).  Below SLIME_RS_PLACEMENT_MIN_GBS
-// (default 6100: the C3 apply kernel at <= 8.45 ms) the library tries the
-// other placements -- 1 GiB chunks, then one hipMalloc -- while still holding
-// the first, while the device has room for both, and keeps the fastest.
+// (default 6350, the top of the rates seen: so in practice always) the library
+// tries the other placements -- 1 GiB chunks, then one hipMalloc -- while
+// still holding the first, while the device has room for both, and keeps the
+// fastest.  Fast placements differ by ~3% among themselves (C3 frac 0.761 to
+// 0.783 at one threshold of 6100, profiles/r06/s34_placement_aim).
 int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
   if (!ptr || bytes == 0) return fail(Status::InvalidArg, "device_alloc: null ptr or zero bytes");
   *ptr = nullptr;
@@ -238,7 +240,7 @@ int slime_rs_device_alloc(int device, uint64_t bytes, void** ptr) {
   return 0;
 }
 
-double slime_rs_placement_threshold(void) { return env_double("SLIME_RS_PLACEMENT_MIN_GBS", 6100.0); }
+double slime_rs_placement_threshold(void) { return env_double("SLIME_RS_PLACEMENT_MIN_GBS", 6350.0); }
 
 // The allocator's probe over a caller's range.  The range must lie inside one
 // device allocation (hipMalloc, or a slime_rs_device_alloc buffer): the probe

@@ -45,6 +45,10 @@ _log = logging.getLogger("slime_amd")
 _known_placement: set = set()
 _warned_placement: set = set()
 PLACEMENT_WARN_BYTES = 16 << 30
+# probe_placement's slow mode: below this fraction of the allocator's
+# threshold (5300-5700 GB/s vs fast placements at 5950-6370 on this
+# project's boxes, profiles/r06/s34_placement_aim).
+SLOW_PLACEMENT = 0.92
 
 
 def _capturing() -> bool:
@@ -118,20 +122,21 @@ def probe_placement(t: torch.Tensor) -> float:
     """The library's placement probe over a caller's FRESH buffer t (it
     overwrites t): GB/s of the C3-shaped read/write walk over its storage, 0
     if too small to measure (slime_rs_probe_placement).  Logs a warning when
-    the rate is below the fast-mode threshold: such a buffer runs the kernels
-    about 10% slower for its whole life -- re-allocate it, or use
-    device_empty(), which probes and re-places by itself."""
+    the rate is in the slow mode (below SLOW_PLACEMENT x the allocator's
+    threshold): such a buffer runs the kernels about 10% slower for its whole
+    life -- re-allocate it, or use device_empty(), which probes and re-places
+    by itself."""
     dev = _dev_index(t)
     base = t.untyped_storage().data_ptr()
     nbytes = t.untyped_storage().nbytes()
     gbs = ctypes.c_double()
     N.check(lib.slime_rs_probe_placement(ctypes.c_void_p(base), nbytes, dev, ctypes.byref(gbs)))
     _known_placement.add(base)
-    want = float(lib.slime_rs_placement_threshold())
-    if 0 < gbs.value < want:
-        _log.warning("slime_amd: buffer at 0x%x (%.1f GiB) probes %.0f GB/s, below the fast placement's %.0f: "
+    slow = SLOW_PLACEMENT * float(lib.slime_rs_placement_threshold())
+    if 0 < gbs.value < slow:
+        _log.warning("slime_amd: buffer at 0x%x (%.1f GiB) probes %.0f GB/s, the slow placement (< %.0f): "
                      "the kernels will stream ~10%% slower on it; allocate batches with "
-                     "slime_amd.device.device_empty (slime_rs_device_alloc)", base, nbytes / 2**30, gbs.value, want)
+                     "slime_amd.device.device_empty (slime_rs_device_alloc)", base, nbytes / 2**30, gbs.value, slow)
     return gbs.value
 
 

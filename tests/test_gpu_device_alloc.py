@@ -166,14 +166,17 @@ def test_probe_placement_of_caller_buffers(torch_dev, caplog):
     want = float(N.lib.slime_rs_placement_threshold())
     assert lib_gbs > 0 and t_gbs > 0
     # The library's promise: its buffer is re-placed until it probes at the
-    # threshold (keeping the fastest of its tries when none does).  So it
-    # matches the hipMalloc buffer within noise, or it clears the threshold
-    # within noise (a fast-mode hipMalloc buffer may probe up to ~4% above a
-    # kept one: 6100-6370 GB/s across this project's boxes), or every try
-    # was slow.
-    every_try_slow = len(lib_info["probes"]) > 1 and all(p["probe_gbs"] < want for p in lib_info["probes"])
+    # threshold, keeping the fastest of its tries when none does (the default
+    # threshold sits at the top of the rates seen, so it nearly always tries
+    # all three).  So it matches the hipMalloc buffer within noise, or it
+    # clears the threshold within noise (fast placements differ by up to ~4%:
+    # 5950-6370 GB/s across this project's boxes), or every try was below it.
+    rates = [p["probe_gbs"] for p in lib_info["probes"]]
+    assert lib_info["chosen"] == rates.index(max(rates)), lib_info
+    every_try_slow = len(rates) > 1 and all(r < want for r in rates)
     assert lib_gbs >= 0.97 * t_gbs or lib_gbs >= 0.98 * want or every_try_slow, (lib_gbs, t_gbs, lib_info)
-    assert (t_gbs < want) == any("probes" in r.getMessage() for r in caplog.records), (t_gbs, want)
+    slow = D.SLOW_PLACEMENT * want
+    assert (t_gbs < slow) == any("probes" in r.getMessage() for r in caplog.records), (t_gbs, slow)
     gbs = ctypes.c_double()
     # past the end of the allocation: refused before any launch
     rc = N.lib.slime_rs_probe_placement(ctypes.c_void_p(t.data_ptr()), t.numel() * 4 + (64 << 20), 0,
