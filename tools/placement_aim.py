@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The allocator's re-placement threshold (SLIME_RS_PLACEMENT_MIN_GBS, read
 per allocation) as an A/B inside one process: rounds of a 48 GiB C3 batch
-from slime_rs_device_alloc under each threshold in turn -- the probes it
+from slime_rs_device_alloc under each threshold in turn -- the allocation's
+wall time, the probes it
 made, the placement it kept, and the C3 encode / in-place repair kernels on
 the kept buffer (median of 5 each) -- then the buffer back to the driver.
 A pad allocation that changes size between rounds shifts where the next
@@ -16,6 +17,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -38,10 +40,12 @@ def main():
     alg = nobj * 4 * L * total
     rows = []
     for r in range(args.rounds):
-        for thr in (float(x) for x in args.thresholds.split(",")):
-            os.environ["SLIME_RS_PLACEMENT_MIN_GBS"] = str(thr)
+        for arm in args.thresholds.split(","):
+            os.environ["SLIME_RS_PLACEMENT_MIN_GBS"] = arm
             pad = D.device_empty((1 + r % 3) * (1 << 28), torch.int32)  # 1-3 GiB: shift the placement
+            t0 = time.perf_counter()
             buf = D.device_empty(nobj * total * L, torch.int32)
+            alloc_s = time.perf_counter() - t0
             info = D.placement(buf)
             D.fill_symbols(buf, r)
             t = {"enc": [], "dec": []}
@@ -56,7 +60,7 @@ def main():
                 t["enc"].append(ev[0].elapsed_time(ev[1]))
                 t["dec"].append(ev[1].elapsed_time(ev[2]))
             e, d = statistics.median(t["enc"][1:]), statistics.median(t["dec"][1:])
-            row = {"round": r, "threshold": thr, "kept": info["kept"],
+            row = {"round": r, "threshold": arm, "alloc_s": round(alloc_s, 3), "kept": info["kept"],
                    "probes": [(p["placement"], round(p["probe_gbs"], 1)) for p in info["probes"]],
                    "enc_ms": round(e, 4), "dec_ms": round(d, 4),
                    "frac": round(alg / ((e + d) / 2 * 1e-3) / 8e12, 4)}
