@@ -455,3 +455,20 @@ def test_top_bit_correction_matches_the_reencode():
                 got = parity0 + entry
                 got = got - p if got >= p else got
                 assert got == want, (need, total, x, c)
+
+
+def test_device_policy_knobs_need_no_gpu(monkeypatch):
+    """The allocator's re-placement threshold (default 6350 GB/s, read per
+    call) and the byte encode's second-pass mode (slime_rs_switch_bits) are
+    host state: set and read without a device, bad modes refused."""
+    monkeypatch.delenv("SLIME_RS_PLACEMENT_MIN_GBS", raising=False)
+    assert N.lib.slime_rs_placement_threshold() == 6350.0
+    monkeypatch.setenv("SLIME_RS_PLACEMENT_MIN_GBS", "6100")
+    assert N.lib.slime_rs_placement_threshold() == 6100.0
+    before = N.lib.slime_rs_switch_bits(-1)
+    try:
+        for m in (1, 2, 0):
+            assert N.lib.slime_rs_switch_bits(m) == 0 and N.lib.slime_rs_switch_bits(-1) == m
+        assert N.lib.slime_rs_switch_bits(3) == N.ERR_INVALID_ARG and N.lib.slime_rs_switch_bits(-1) == 0
+    finally:
+        N.lib.slime_rs_switch_bits(before)
